@@ -1,0 +1,32 @@
+"""anomod — MI355X-native RCA-feature engine for the AnoMod dataset.
+
+Call surface:
+
+    exp = anomod.load_experiment(path_or_SynthSpec, metrics=...)
+    feats = anomod.features(exp)          # GPU: edge table, p50/p99, window z
+    ranking = anomod.rank(feats)          # GPU: personalized PageRank
+
+All compute runs in libanomod.so (hand-written HIP for gfx950) through a
+ctypes C ABI (include/anomod.h); there is no CPU fallback.
+"""
+from ._lib import (FLAG_ERROR, HIST_BINS, HIST_SUB_BITS, AnomodError, EXPORTED_SYMBOLS,
+                   LIB_PATH, lib)
+from .decode import (MetricMatrix, decode_jaeger, decode_metric_long_csv,
+                     decode_prometheus_csv_dir, decode_skywalking_payload, decode_skywalking_raw,
+                     jaeger_span_rows, merge_jaeger_dumps, skywalking_parents)
+from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec, device_count,
+                     device_count_safe,
+                     synth_generate_host, synth_services)
+from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
+                     load_experiment, rank)
+from .spans import EdgeTable, SpanSet, edge_rows
+
+__all__ = [
+    "AnomodError", "Context", "DeviceGraph", "DeviceSeries", "DeviceSpans", "EdgeTable",
+    "EXPORTED_SYMBOLS", "Experiment", "FLAG_ERROR", "Features", "HIST_BINS", "HIST_SUB_BITS",
+    "LIB_PATH", "MetricMatrix", "SpanSet", "SynthSpec", "decode_jaeger",
+    "decode_metric_long_csv", "decode_prometheus_csv_dir", "decode_skywalking_payload",
+    "decode_skywalking_raw", "default_context", "device_count", "device_count_safe", "edge_rows", "fault_target",
+    "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
+    "rank", "skywalking_parents", "synth_generate_host", "synth_services",
+]

@@ -1,0 +1,163 @@
+"""ctypes binding of libanomod.so (the C ABI declared in include/anomod.h).
+
+The library is the only compute path: if it cannot be loaded, every entry
+point raises :class:`AnomodError` — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("ANOMOD_LIB", _HERE / "libanomod.so"))
+
+ABI_VERSION = 1
+HIST_SUB_BITS = 5
+HIST_BINS = 896
+ROOT_ROWS = 2
+FLAG_ERROR = 0x1
+UNIQUE_ID_BYTES = 128
+TOPO_SN = 0
+TOPO_TT = 1
+
+OK, EINVAL, EHIP, ERCCL, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
+_STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", ESTATE: "ESTATE"}
+
+STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK = range(5)
+
+
+class AnomodError(RuntimeError):
+    """A libanomod call failed (status code + anomod_last_error message)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{_STATUS.get(status, status)}: {message}")
+        self.status = status
+
+
+class SpanSoA(C.Structure):
+    _fields_ = [
+        ("trace_hash", C.POINTER(C.c_uint64)),
+        ("span_id", C.POINTER(C.c_uint64)),
+        ("parent_span_id", C.POINTER(C.c_uint64)),
+        ("svc", C.POINTER(C.c_uint16)),
+        ("flags", C.POINTER(C.c_uint16)),
+        ("dur_us", C.POINTER(C.c_uint32)),
+    ]
+
+
+class EdgeTableC(C.Structure):
+    _fields_ = [
+        ("n_services", C.c_uint32),
+        ("n_bins", C.c_uint32),
+        ("count", C.POINTER(C.c_uint64)),
+        ("errors", C.POINTER(C.c_uint64)),
+        ("sum_us", C.POINTER(C.c_uint64)),
+        ("min_us", C.POINTER(C.c_uint32)),
+        ("max_us", C.POINTER(C.c_uint32)),
+        ("hist", C.POINTER(C.c_uint64)),
+        ("p50_us", C.POINTER(C.c_double)),
+        ("p99_us", C.POINTER(C.c_double)),
+    ]
+
+
+class SynthSpec(C.Structure):
+    _fields_ = [
+        ("topology", C.c_uint32),
+        ("fault_service", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("fault_latency_mult", C.c_uint32),
+        ("p_error_ppm", C.c_uint32),
+        ("p_fault_error_ppm", C.c_uint32),
+        ("p_orphan_ppm", C.c_uint32),
+    ]
+
+
+_vp = C.c_void_p
+_u32, _u64, _i32 = C.c_uint32, C.c_uint64, C.c_int
+_f32, _f64 = C.c_float, C.c_double
+_P = C.POINTER
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "anomod_abi_version": (_i32, []),
+    "anomod_last_error": (C.c_char_p, [_vp]),
+    "anomod_device_count": (_i32, [_P(_i32)]),
+    "anomod_ctx_create": (_i32, [_i32, _P(_vp)]),
+    "anomod_ctx_destroy": (_i32, [_vp]),
+    "anomod_ctx_synchronize": (_i32, [_vp]),
+    "anomod_ctx_stage_ms": (_i32, [_vp, _i32, _P(_f64)]),
+    "anomod_hist_bin": (_u32, [_u32]),
+    "anomod_hist_bin_bounds": (_i32, [_u32, _P(_u32), _P(_u32)]),
+    "anomod_spans_upload": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(_vp)]),
+    "anomod_spans_info": (_i32, [_vp, _P(_u64), _P(_u64)]),
+    "anomod_spans_download": (_i32, [_vp, _vp, _P(SpanSoA), _P(_u64)]),
+    "anomod_spans_free": (_i32, [_vp]),
+    "anomod_synth_n_services": (_i32, [_u32, _P(_u32)]),
+    "anomod_synth_service_name": (C.c_char_p, [_u32, _u32]),
+    "anomod_synth_count_host": (_i32, [_P(SynthSpec), _u64, _u64, _P(_u64)]),
+    "anomod_synth_generate_host": (_i32, [_P(SynthSpec), _u64, _u64, _P(SpanSoA), _P(_u64)]),
+    "anomod_spans_generate": (_i32, [_vp, _P(SynthSpec), _u64, _u64, _P(_vp)]),
+    "anomod_edge_aggregate_spans": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
+    "anomod_edge_aggregate": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(EdgeTableC)]),
+    "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
+    "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),
+    "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),
+    "anomod_series_fill_synthetic": (_i32, [_vp, _vp, _u64, _u64]),
+    "anomod_series_reset_state": (_i32, [_vp, _vp]),
+    "anomod_series_ewma_z": (_i32, [_vp, _vp, _f32, _u32, _f32, _P(_f32)]),
+    "anomod_series_free": (_i32, [_vp]),
+    "anomod_pagerank": (_i32, [_vp, _P(_u32), _P(_u32), _P(_f32), _u32, _P(_f64), _f64, _u32,
+                               _f64, _P(_f64), _P(_u32)]),
+    "anomod_graph_create": (_i32, [_vp, _P(_u32), _P(_u32), _P(_f32), _u32, _P(_vp)]),
+    "anomod_graph_synthetic": (_i32, [_vp, _u32, _u32, _u64, _P(_vp)]),
+    "anomod_graph_info": (_i32, [_vp, _P(_u32), _P(_u64)]),
+    "anomod_graph_pagerank": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _P(_f64), _P(_u32)]),
+    "anomod_graph_free": (_i32, [_vp]),
+    "anomod_comm_unique_id": (_i32, [_P(C.c_uint8)]),
+    "anomod_ctx_attach_comm": (_i32, [_vp, _P(C.c_uint8), _i32, _i32]),
+    "anomod_ctx_comm_info": (_i32, [_vp, _P(_i32), _P(_i32)]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libanomod.so once; raise loudly if it is missing or stale."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise AnomodError(
+            ESTATE,
+            f"{LIB_PATH} not found: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()')",
+        )
+    handle = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = handle.anomod_abi_version()
+    if v != ABI_VERSION:
+        raise AnomodError(ESTATE, f"libanomod ABI {v} != expected {ABI_VERSION}")
+    _lib = handle
+    return _lib
+
+
+def check(status: int, ctx=None) -> None:
+    if status != OK:
+        msg = lib().anomod_last_error(ctx)
+        raise AnomodError(status, msg.decode() if msg else "unknown error")
+
+
+def ptr(a: np.ndarray | None, ctype):
+    """ctypes pointer into a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return C.cast(None, C.POINTER(ctype))
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to libanomod must be C-contiguous"
+    return a.ctypes.data_as(C.POINTER(ctype))

@@ -1,0 +1,314 @@
+"""Device context: one HIP device + stream (+ optional RCCL communicator).
+
+Thin object layer over the C ABI; every compute method runs a hand-written
+HIP kernel in libanomod.so.  Nothing here falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .spans import EdgeTable, SpanSet, edge_rows
+
+
+@dataclass
+class SynthSpec:
+    """Synthetic workload: topology 'SN' or 'TT'."""
+
+    topology: str = "SN"
+    seed: int = 20251103
+    fault_service: str | int | None = None
+    fault_latency_mult: int = 8
+    p_error_ppm: int = 5000          # 0.5 % base error rate
+    p_fault_error_ppm: int = 200000  # 20 % on the faulty service
+    p_orphan_ppm: int = 0
+
+    @property
+    def topo_id(self) -> int:
+        return {"SN": L.TOPO_SN, "TT": L.TOPO_TT}[self.topology.upper()]
+
+    def services(self) -> list[str]:
+        return synth_services(self.topology)
+
+    def c_struct(self) -> L.SynthSpec:
+        fault = 0xFFFFFFFF
+        if self.fault_service is not None:
+            fault = (self.services().index(self.fault_service)
+                     if isinstance(self.fault_service, str) else int(self.fault_service))
+        return L.SynthSpec(self.topo_id, fault, self.seed, self.fault_latency_mult,
+                           self.p_error_ppm, self.p_fault_error_ppm, self.p_orphan_ppm)
+
+
+def synth_services(topology: str) -> list[str]:
+    lib = L.lib()
+    tid = {"SN": L.TOPO_SN, "TT": L.TOPO_TT}[topology.upper()]
+    n = C.c_uint32()
+    L.check(lib.anomod_synth_n_services(tid, C.byref(n)))
+    return [lib.anomod_synth_service_name(tid, i).decode() for i in range(n.value)]
+
+
+def synth_generate_host(spec: SynthSpec, n_traces: int, shard: int = 0) -> SpanSet:
+    """Generate a synthetic span set on the host (same generator as the GPU)."""
+    lib = L.lib()
+    cs = spec.c_struct()
+    n = C.c_uint64()
+    L.check(lib.anomod_synth_count_host(C.byref(cs), shard, n_traces, C.byref(n)))
+    ns = n.value
+    arr = dict(trace_hash=np.empty(ns, np.uint64), span_id=np.empty(ns, np.uint64),
+               parent_span_id=np.empty(ns, np.uint64), svc=np.empty(ns, np.uint16),
+               flags=np.empty(ns, np.uint16), dur_us=np.empty(ns, np.uint32))
+    ptr = np.empty(n_traces + 1, np.uint64)
+    L.check(lib.anomod_synth_generate_host(C.byref(cs), shard, n_traces,
+                                           C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)))
+    return SpanSet(spec.services(), ptr, **arr)
+
+
+def _soa_out(arr: dict) -> L.SpanSoA:
+    return L.SpanSoA(L.ptr(arr["trace_hash"], C.c_uint64), L.ptr(arr["span_id"], C.c_uint64),
+                     L.ptr(arr["parent_span_id"], C.c_uint64), L.ptr(arr["svc"], C.c_uint16),
+                     L.ptr(arr["flags"], C.c_uint16), L.ptr(arr["dur_us"], C.c_uint32))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    L.check(L.lib().anomod_device_count(C.byref(n)))
+    return n.value
+
+
+def device_count_safe() -> int:
+    """Number of visible GPUs, 0 when the HIP runtime reports none."""
+    n = C.c_int()
+    return n.value if L.lib().anomod_device_count(C.byref(n)) == L.OK else 0
+
+
+class DeviceSpans:
+    """A span set resident in HBM (owned by libanomod)."""
+
+    def __init__(self, ctx: "Context", handle: C.c_void_p, services: list[str]):
+        self.ctx, self.handle, self.services = ctx, handle, list(services)
+        ns, nt = C.c_uint64(), C.c_uint64()
+        L.check(L.lib().anomod_spans_info(handle, C.byref(ns), C.byref(nt)))
+        self.n_spans, self.n_traces = ns.value, nt.value
+
+    def download(self) -> SpanSet:
+        n = self.n_spans
+        arr = dict(trace_hash=np.empty(n, np.uint64), span_id=np.empty(n, np.uint64),
+                   parent_span_id=np.empty(n, np.uint64), svc=np.empty(n, np.uint16),
+                   flags=np.empty(n, np.uint16), dur_us=np.empty(n, np.uint32))
+        ptr = np.empty(self.n_traces + 1, np.uint64)
+        L.check(L.lib().anomod_spans_download(self.ctx.handle, self.handle,
+                                              C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)),
+                self.ctx.handle)
+        return SpanSet(self.services, ptr, **arr)
+
+    def free(self):
+        if self.handle:
+            L.lib().anomod_spans_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One GPU: ``Context(device)``; use as a context manager or call close()."""
+
+    def __init__(self, device: int = 0):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        L.check(self._lib.anomod_ctx_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    # -- lifecycle
+    def close(self):
+        if self.handle:
+            self._lib.anomod_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, status: int):
+        L.check(status, self.handle)
+
+    def synchronize(self):
+        self._check(self._lib.anomod_ctx_synchronize(self.handle))
+
+    def stage_ms(self, stage: int) -> float:
+        v = C.c_double()
+        self._check(self._lib.anomod_ctx_stage_ms(self.handle, stage, C.byref(v)))
+        return v.value
+
+    # -- multi-GPU
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * L.UNIQUE_ID_BYTES)()
+        L.check(L.lib().anomod_comm_unique_id(buf))
+        return bytes(buf)
+
+    def attach_comm(self, unique_id: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * L.UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        self._check(self._lib.anomod_ctx_attach_comm(self.handle, buf, nranks, rank))
+
+    # -- spans
+    def upload(self, spans: SpanSet) -> DeviceSpans:
+        h = C.c_void_p()
+        soa = spans.soa()
+        self._check(self._lib.anomod_spans_upload(self.handle, C.byref(soa), spans.n_spans,
+                                                  L.ptr(spans.trace_ptr, C.c_uint64),
+                                                  spans.n_traces, C.byref(h)))
+        return DeviceSpans(self, h, spans.services)
+
+    def generate(self, spec: SynthSpec, n_traces: int, shard: int = 0) -> DeviceSpans:
+        h = C.c_void_p()
+        cs = spec.c_struct()
+        self._check(self._lib.anomod_spans_generate(self.handle, C.byref(cs), shard, n_traces,
+                                                    C.byref(h)))
+        return DeviceSpans(self, h, spec.services())
+
+    def edge_aggregate(self, spans: DeviceSpans | SpanSet, with_hist: bool = True) -> EdgeTable:
+        """Edge table of a span set (uploading it first if it is on the host)."""
+        tmp = None
+        if isinstance(spans, SpanSet):
+            tmp = spans = self.upload(spans)
+        try:
+            table = EdgeTable.empty(spans.services, with_hist)
+            cs = table.c_struct()
+            self._check(self._lib.anomod_edge_aggregate_spans(
+                self.handle, spans.handle, len(spans.services), C.byref(cs)))
+            if table.hist is not None:
+                table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
+            return table
+        finally:
+            if tmp is not None:
+                tmp.free()
+
+    # -- metric series
+    def ewma_z(self, X: np.ndarray, alpha: float, W: int, eps: float = 1e-12) -> np.ndarray:
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        T, S = X.shape
+        if T % W:
+            raise ValueError(f"T={T} must be a multiple of W={W}")
+        Z = np.empty((T // W, S), np.float32)
+        if T == 0 or S == 0:
+            return Z
+        self._check(self._lib.anomod_ewma_z(self.handle, L.ptr(X, C.c_float), T, S, alpha, W,
+                                            eps, L.ptr(Z, C.c_float)))
+        return Z
+
+    # -- ranking
+    def pagerank(self, row_ptr, col, w, p, alpha=0.85, iters=100, tol=1e-10):
+        row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
+        col = np.ascontiguousarray(col, np.uint32)
+        w = np.ascontiguousarray(w, np.float32)
+        p = np.ascontiguousarray(p, np.float64)
+        N = row_ptr.shape[0] - 1
+        x = np.empty(N, np.float64)
+        done = C.c_uint32()
+        if col.size == 0:  # keep the pointers valid for an edgeless graph
+            col, w = np.zeros(1, np.uint32), np.zeros(1, np.float32)
+        self._check(self._lib.anomod_pagerank(self.handle, L.ptr(row_ptr, C.c_uint32),
+                                              L.ptr(col, C.c_uint32), L.ptr(w, C.c_float), N,
+                                              L.ptr(p, C.c_double), alpha, iters, tol,
+                                              L.ptr(x, C.c_double), C.byref(done)))
+        return x, done.value
+
+
+class DeviceGraph:
+    """A CSR graph resident in HBM for repeated PageRank solves."""
+
+    def __init__(self, ctx: Context, row_ptr=None, col=None, w=None, *, synthetic=None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        lib = L.lib()
+        if synthetic is not None:
+            N, deg, seed = synthetic
+            ctx._check(lib.anomod_graph_synthetic(ctx.handle, N, deg, seed, C.byref(h)))
+        else:
+            row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
+            col = np.ascontiguousarray(col, np.uint32)
+            w = np.ascontiguousarray(w, np.float32)
+            ctx._check(lib.anomod_graph_create(ctx.handle, L.ptr(row_ptr, C.c_uint32),
+                                               L.ptr(col, C.c_uint32), L.ptr(w, C.c_float),
+                                               row_ptr.shape[0] - 1, C.byref(h)))
+        self.handle = h
+        n, nnz = C.c_uint32(), C.c_uint64()
+        L.check(lib.anomod_graph_info(h, C.byref(n), C.byref(nnz)))
+        self.N, self.nnz = n.value, nnz.value
+
+    def pagerank(self, p, alpha=0.85, iters=100, tol=0.0):
+        p = np.ascontiguousarray(p, np.float64)
+        x = np.empty(self.N, np.float64)
+        done = C.c_uint32()
+        self.ctx._check(L.lib().anomod_graph_pagerank(self.ctx.handle, self.handle,
+                                                      L.ptr(p, C.c_double), alpha, iters, tol,
+                                                      L.ptr(x, C.c_double), C.byref(done)))
+        return x, done.value
+
+    def free(self):
+        if self.handle:
+            L.lib().anomod_graph_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceSeries:
+    """A [T][S] metric matrix resident in HBM with carried EWMA state."""
+
+    def __init__(self, ctx: Context, T: int, S: int):
+        self.ctx, self.T, self.S = ctx, T, S
+        h = C.c_void_p()
+        ctx._check(L.lib().anomod_series_create(ctx.handle, T, S, C.byref(h)))
+        self.handle = h
+
+    def upload(self, X: np.ndarray):
+        X = np.ascontiguousarray(X, np.float32)
+        assert X.shape == (self.T, self.S)
+        self.ctx._check(L.lib().anomod_series_upload(self.ctx.handle, self.handle,
+                                                     L.ptr(X, C.c_float)))
+
+    def fill_synthetic(self, seed: int, t0: int = 0):
+        self.ctx._check(L.lib().anomod_series_fill_synthetic(self.ctx.handle, self.handle,
+                                                             seed, t0))
+
+    def reset_state(self):
+        self.ctx._check(L.lib().anomod_series_reset_state(self.ctx.handle, self.handle))
+
+    def ewma_z(self, alpha: float, W: int, eps: float = 1e-12, download: bool = True):
+        Z = np.empty((self.T // W, self.S), np.float32) if download else None
+        self.ctx._check(L.lib().anomod_series_ewma_z(
+            self.ctx.handle, self.handle, alpha, W, eps,
+            L.ptr(Z, C.c_float) if Z is not None else C.cast(None, C.POINTER(C.c_float))))
+        return Z
+
+    def free(self):
+        if self.handle:
+            L.lib().anomod_series_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,0 +1,119 @@
+// Internal shared definitions of libanomod (not part of the public ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/anomod.h"
+
+namespace anomod {
+
+// Error plumbing: a per-thread message for ctx-less failures, a per-ctx one
+// otherwise (anomod_last_error).
+void set_error(anomod_ctx* ctx, const char* fmt, ...);
+
+enum Stage { kStageEdgeAgg = 0, kStageEdgeFinal = 1, kStageEdgeReduce = 2, kStageEwma = 3,
+             kStagePagerank = 4, kNumStages = 5 };
+
+}  // namespace anomod
+
+struct anomod_ctx {
+  int device = 0;
+  int num_cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_begin[anomod::kNumStages] = {};
+  hipEvent_t ev_end[anomod::kNumStages] = {};
+  bool stage_recorded[anomod::kNumStages] = {};
+  std::string err;
+  // RCCL communicator (one process per GPU)
+  ncclComm_t comm = nullptr;
+  int nranks = 1;
+  int rank = 0;
+  // Cached device workspace for the edge table.
+  void* d_table = nullptr;
+  size_t table_bytes = 0;
+};
+
+struct anomod_spans {
+  int device = 0;
+  uint64_t n_spans = 0;
+  uint64_t n_traces = 0;
+  uint32_t max_svc = 0;      // largest service index present (host-validated)
+  uint64_t* trace_hash = nullptr;
+  uint64_t* span_id = nullptr;
+  uint64_t* parent_span_id = nullptr;
+  uint16_t* svc = nullptr;
+  uint16_t* flags = nullptr;
+  uint32_t* dur_us = nullptr;
+  uint64_t* trace_ptr = nullptr;  // [n_traces + 1]
+  void* base = nullptr;           // single allocation backing every array
+};
+
+#define ANOMOD_HIP(ctx, expr)                                                               \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) {                                                                 \
+      anomod::set_error((ctx), "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),      \
+                        __FILE__, __LINE__);                                                \
+      return ANOMOD_EHIP;                                                                   \
+    }                                                                                       \
+  } while (0)
+
+#define ANOMOD_RCCL(ctx, expr)                                                              \
+  do {                                                                                      \
+    ncclResult_t _r = (expr);                                                               \
+    if (_r != ncclSuccess) {                                                                \
+      anomod::set_error((ctx), "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(_r),     \
+                        __FILE__, __LINE__);                                                \
+      return ANOMOD_ERCCL;                                                                  \
+    }                                                                                       \
+  } while (0)
+
+#define ANOMOD_REQUIRE(ctx, cond, ...)                                                      \
+  do {                                                                                      \
+    if (!(cond)) {                                                                          \
+      anomod::set_error((ctx), __VA_ARGS__);                                                \
+      return ANOMOD_EINVAL;                                                                 \
+    }                                                                                       \
+  } while (0)
+
+namespace anomod {
+
+// Make ctx's device current on this host thread.
+int bind(anomod_ctx* ctx);
+// hipEvent bracketing of a stage on the ctx stream.
+int stage_begin(anomod_ctx* ctx, Stage s);
+int stage_end(anomod_ctx* ctx, Stage s);
+// Grow-only device workspace owned by the ctx.
+int ensure_table(anomod_ctx* ctx, size_t bytes);
+
+// ---- integer latency histogram (ANOMOD_HIST_*) --------------------------
+__host__ __device__ inline uint32_t hist_bin(uint32_t v) {
+  if (v < 64u) return v;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lg = 31u - (uint32_t)__clz((int)v);
+#else
+  const uint32_t lg = 31u - (uint32_t)__builtin_clz(v);
+#endif
+  const uint32_t e = lg - ANOMOD_HIST_SUB_BITS;
+  return (e << ANOMOD_HIST_SUB_BITS) + (v >> e);
+}
+
+__host__ __device__ inline void hist_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi) {
+  if (bin < 64u) {
+    *lo = bin;
+    *hi = bin;
+    return;
+  }
+  const uint32_t e = (bin >> ANOMOD_HIST_SUB_BITS) - 1u;
+  const uint64_t m = (uint64_t)(bin & ((1u << ANOMOD_HIST_SUB_BITS) - 1u)) +
+                     (1u << ANOMOD_HIST_SUB_BITS);
+  *lo = (uint32_t)(m << e);
+  *hi = (uint32_t)(((m + 1) << e) - 1);
+}
+
+}  // namespace anomod

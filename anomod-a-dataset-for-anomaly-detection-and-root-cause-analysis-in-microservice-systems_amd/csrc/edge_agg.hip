@@ -1,0 +1,515 @@
+// Call-graph edge aggregation — the hot path.
+//
+// Replaces the per-span Python loops of
+//   SN_collection-scripts/Dataset/trace_data/jaeger_to_csv.py:21-90
+//     (parent = spanID of the first CHILD_OF reference, :34-38; service
+//      resolved through processID, :45-46; duration_us, :83)
+//   TT_collection-scripts/T-Dataset/trace_collector.py:401-481
+//     (_build_span_records: trace-local parent resolution; roots = spans
+//      whose parent is not in the trace, :443)
+//   TT_collection-scripts/T-Dataset/enhanced_trace_collector.py:216-296
+//     (per-service counts / error counts / latency stats)
+// and adds what the reference never computed: a (parent service -> child
+// service) edge table with an integer log-linear latency histogram per edge
+// and p50/p99 taken with the reference's nearest-rank index convention
+// (monitor_http_responses.py:180-190, rank = (n*q)//100).
+//
+// Design (MI355X):
+//  * one pass over the span SoA in HBM: 8 B span_id + 8 B parent_span_id +
+//    2 B svc + 2 B flags + 4 B dur_us per span + 8 B trace_ptr per trace;
+//  * persistent grid, one 1024-thread workgroup per CU; every wave owns a
+//    contiguous range of traces and walks it in chunks of <= 256 spans, so
+//    parent resolution is trace-local in that wave's LDS staging area (no
+//    inter-wave synchronisation inside the loop);
+//  * the E x 896 histogram does not fit LDS, so each workgroup privatises it
+//    in a 16 Ki-slot LDS hash table of packed (key | count) words; a count
+//    field that wraps flushes 2^cntbits to HBM with a u64 atomic, slots are
+//    flushed once at the end;
+//  * per-edge error/sum/min/max live in LDS (E <= 512) and are flushed once;
+//  * all merges are integer adds / min / max: results are bit-exact and
+//    independent of geometry, scheduling and shard count.
+#include <cmath>
+#include <limits>
+
+#include "common.h"
+
+namespace anomod {
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 16;
+constexpr int kThreads = kWave * kWavesPerWG;
+constexpr int kStage = 256;  // spans staged per wave chunk
+constexpr int kPer = kStage / kWave;
+constexpr int kHtLog2 = 14;
+constexpr uint32_t kHtSlots = 1u << kHtLog2;
+constexpr int kMaxProbe = 64;
+constexpr uint32_t kLdsEdges = 512;
+constexpr uint32_t kBins = ANOMOD_HIST_BINS;
+
+// LDS carve (bytes, every offset a multiple of 16).
+constexpr int kOffHt = 0;
+constexpr int kOffSum = kOffHt + (int)kHtSlots * 4;
+constexpr int kOffErr = kOffSum + (int)kLdsEdges * 8;
+constexpr int kOffMin = kOffErr + (int)kLdsEdges * 4;
+constexpr int kOffMax = kOffMin + (int)kLdsEdges * 4;
+constexpr int kOffWave = kOffMax + (int)kLdsEdges * 4;
+constexpr int kWSid = 0;
+constexpr int kWSvc = kWSid + kStage * 8;
+constexpr int kWTix = kWSvc + kStage * 2;
+constexpr int kWTs = kWTix + kStage;
+constexpr int kWBytes = kWTs + 144;
+constexpr int kLdsBytes = kOffWave + kWavesPerWG * kWBytes;
+static_assert(kWBytes % 16 == 0, "wave staging must stay 16-B aligned");
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+
+struct Table {
+  unsigned long long* hist;  // [E * kBins]
+  unsigned long long* err;   // [E]
+  unsigned long long* sum;   // [E]
+  unsigned int* mn;          // [E]
+  unsigned int* mx;          // [E]
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Packed LDS hash-table increment of histogram key `kidx` (edge*kBins+bin).
+// Slot word = (count << KEYBITS) | (kidx + 1); 0 = empty.
+template <int KEYBITS>
+__device__ __forceinline__ void ht_add(uint32_t* ht, uint32_t kidx,
+                                       unsigned long long* __restrict__ ghist) {
+  if constexpr (KEYBITS == 0) {
+    atomicAdd(&ghist[kidx], 1ull);
+  } else {
+    constexpr uint32_t kKeyMask = (1u << KEYBITS) - 1u;
+    constexpr uint32_t kInc = 1u << KEYBITS;
+    constexpr uint32_t kCntMax = (1u << (32 - KEYBITS)) - 1u;
+    const uint32_t key = kidx + 1u;
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - kHtLog2);
+    for (int probe = 0; probe < kMaxProbe; ++probe) {
+      uint32_t cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (cur == 0u) {
+        const uint32_t prev = atomicCAS(&ht[h], 0u, key | kInc);
+        if (prev == 0u) return;
+        cur = prev;
+      }
+      if ((cur & kKeyMask) == key) {
+        const uint32_t old = atomicAdd(&ht[h], kInc);
+        if ((old >> KEYBITS) == kCntMax) atomicAdd(&ghist[kidx], (unsigned long long)kCntMax + 1ull);
+        return;
+      }
+      h = (h + 1u) & (kHtSlots - 1u);
+    }
+    atomicAdd(&ghist[kidx], 1ull);  // table saturated: count in HBM directly
+  }
+}
+
+template <int KEYBITS, bool LDS_STATS>
+__device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
+                                       const Table& tab) {
+  ht_add<KEYBITS>(reinterpret_cast<uint32_t*>(smem + kOffHt), edge * kBins + hist_bin(d),
+                  tab.hist);
+  if constexpr (LDS_STATS) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
+    auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
+    auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
+    atomicAdd(&lsum[edge], (unsigned long long)d);
+    atomicMin(&lmin[edge], d);
+    atomicMax(&lmax[edge], d);
+    if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&lerr[edge], 1u);
+  } else {
+    atomicAdd(&tab.sum[edge], (unsigned long long)d);
+    atomicMin(&tab.mn[edge], d);
+    atomicMax(&tab.mx[edge], d);
+    if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&tab.err[edge], 1ull);
+  }
+}
+
+// A trace longer than kStage: wave-cooperative scan of the trace's span ids,
+// staged kStage at a time through the wave's LDS area (O(L^2 / 64) per trace;
+// rare — real traces are tens of spans).
+template <int KEYBITS, bool LDS_STATS>
+__device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uint64_t lo,
+                          uint64_t hi, const uint64_t* __restrict__ span_id,
+                          const uint64_t* __restrict__ parent, const uint16_t* __restrict__ svc,
+                          const uint16_t* __restrict__ flags, const uint32_t* __restrict__ dur,
+                          uint32_t S, const Table& tab) {
+  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
+  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
+  for (uint64_t i0 = lo; i0 < hi; i0 += kWave) {
+    const uint64_t i = i0 + lane;
+    const bool active = i < hi;
+    uint64_t pid = 0;
+    uint32_t d = 0, fl = 0, c = 0;
+    if (active) {
+      pid = parent[i];
+      d = dur[i];
+      fl = flags[i];
+      c = svc[i];
+    }
+    uint32_t p = (pid == 0) ? S : S + 1u;
+    bool done = !active || pid == 0;
+    for (uint64_t q0 = lo; q0 < hi; q0 += kStage) {
+      if (__all(done)) break;
+      const uint32_t m = (uint32_t)((hi - q0) < (uint64_t)kStage ? (hi - q0) : (uint64_t)kStage);
+      for (uint32_t q = lane; q < m; q += kWave) {
+        lsid[q] = span_id[q0 + q];
+        lsvc[q] = svc[q0 + q];
+      }
+      wave_sync();
+      if (!done) {
+        for (uint32_t q = 0; q < m; ++q) {
+          if (lsid[q] == pid) {
+            p = lsvc[q];
+            done = true;
+            break;
+          }
+        }
+      }
+      wave_sync();
+    }
+    if (active) record<KEYBITS, LDS_STATS>(smem, p * S + c, d, fl, tab);
+  }
+}
+
+template <int KEYBITS, bool LDS_STATS>
+__global__ __launch_bounds__(kThreads) void edge_agg_kernel(
+    const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+    const uint16_t* __restrict__ svc, const uint16_t* __restrict__ flags,
+    const uint32_t* __restrict__ dur, const uint64_t* __restrict__ trace_ptr, uint64_t n_traces,
+    uint32_t S, uint32_t E, Table tab) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wid = tid / kWave;
+
+  // ---- init LDS tables
+  {
+    auto* ht = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    for (uint32_t s = tid; s < kHtSlots; s += kThreads) ht[s] = 0u;
+    if constexpr (LDS_STATS) {
+      auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+      auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
+      auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
+      auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
+      for (uint32_t e = tid; e < E; e += kThreads) {
+        lsum[e] = 0ull;
+        lerr[e] = 0u;
+        lmin[e] = 0xFFFFFFFFu;
+        lmax[e] = 0u;
+      }
+    }
+  }
+  __syncthreads();
+
+  unsigned char* wsm = smem + kOffWave + wid * kWBytes;
+  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
+  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
+  auto* ltix = reinterpret_cast<uint8_t*>(wsm + kWTix);
+  auto* lts = reinterpret_cast<uint16_t*>(wsm + kWTs);
+
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
+  uint64_t t = n_traces * gw / nw;
+  const uint64_t t_end = n_traces * (gw + 1) / nw;
+
+  while (t < t_end) {
+    // Trace boundaries of up to 64 traces: lane j holds trace t + j.
+    const uint64_t ti = t + lane;
+    const bool valid = ti < t_end;
+    uint64_t lo = 0, hi = 0;
+    if (valid) {
+      lo = trace_ptr[ti];
+      hi = trace_ptr[ti + 1];
+    }
+    const uint64_t base = __shfl(lo, 0);
+    const bool fits = valid && (hi - base) <= (uint64_t)kStage;
+    const int k = __popcll(__ballot(fits));  // traces that fit: a prefix of the lanes
+    if (k == 0) {
+      big_trace<KEYBITS, LDS_STATS>(smem, wsm, lane, base, __shfl(hi, 0), span_id, parent, svc,
+                                    flags, dur, S, tab);
+      t += 1;
+      continue;
+    }
+    const uint32_t n = (uint32_t)(__shfl(hi, k - 1) - base);
+
+    // Issue every global load of the chunk before touching LDS.
+    uint64_t rs[kPer], rp[kPer];
+    uint32_t rd[kPer], rv[kPer], rf[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const uint32_t i = lane + r * kWave;
+      rs[r] = rp[r] = 0;
+      rd[r] = rv[r] = rf[r] = 0;
+      if (i < n) {
+        rs[r] = span_id[base + i];
+        rp[r] = parent[base + i];
+        rv[r] = svc[base + i];
+        rf[r] = flags[base + i];
+        rd[r] = dur[base + i];
+      }
+    }
+    // Local trace table: starts, and a per-span trace index.
+    if (lane < k) {
+      const uint32_t a = (uint32_t)(lo - base), b = (uint32_t)(hi - base);
+      lts[lane] = (uint16_t)a;
+      if (lane == k - 1) lts[k] = (uint16_t)b;
+      for (uint32_t i = a; i < b; ++i) ltix[i] = (uint8_t)lane;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const uint32_t i = lane + r * kWave;
+      if (i < n) {
+        lsid[i] = rs[r];
+        lsvc[i] = (uint16_t)rv[r];
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const uint32_t i = lane + r * kWave;
+      if (i < n) {
+        const uint32_t j = ltix[i];
+        const uint32_t a = lts[j], b = lts[j + 1];
+        const uint64_t pid = rp[r];
+        uint32_t p = S;  // ROOT: no parent reference
+        if (pid != 0ull) {
+          p = S + 1u;  // ORPHAN unless found in the trace
+          for (uint32_t q = a; q < b; ++q) {
+            if (lsid[q] == pid) {
+              p = lsvc[q];
+              break;
+            }
+          }
+        }
+        record<KEYBITS, LDS_STATS>(smem, p * S + rv[r], rd[r], rf[r], tab);
+      }
+    }
+    wave_sync();
+    t += (uint64_t)k;
+  }
+  __syncthreads();
+
+  // ---- flush the workgroup's private tables (integer atomics, order-free)
+  if constexpr (KEYBITS != 0) {
+    constexpr uint32_t kKeyMask = (1u << KEYBITS) - 1u;
+    auto* ht = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
+      const uint32_t v = ht[s];
+      const uint32_t cnt = v >> KEYBITS;
+      if (cnt) atomicAdd(&tab.hist[(v & kKeyMask) - 1u], (unsigned long long)cnt);
+    }
+  }
+  if constexpr (LDS_STATS) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
+    auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
+    auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      if (lmin[e] != 0xFFFFFFFFu || lmax[e] != 0u) {
+        atomicAdd(&tab.sum[e], lsum[e]);
+        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
+        atomicMin(&tab.mn[e], lmin[e]);
+        atomicMax(&tab.mx[e], lmax[e]);
+      }
+    }
+  }
+}
+
+// Count + nearest-rank quantiles per edge from the merged histogram: one
+// wave per edge, 14 contiguous bins per lane, wave prefix sum.
+constexpr int kBinsPerLane = (kBins + kWave - 1) / kWave;
+
+__device__ __forceinline__ double quantile_from(uint64_t r, uint64_t excl, uint64_t incl,
+                                                const uint64_t* v, int lane) {
+  // Called only by the lane whose [excl, incl) contains r.
+  uint64_t c = excl;
+  for (int j = 0; j < kBinsPerLane; ++j) {
+    c += v[j];
+    if (r < c) {
+      uint32_t lo, hi;
+      hist_bounds((uint32_t)(lane * kBinsPerLane + j), &lo, &hi);
+      return 0.5 * ((double)lo + (double)hi);
+    }
+  }
+  return 0.0;
+}
+
+__global__ __launch_bounds__(kWave) void edge_finalize_kernel(Table tab,
+                                                              unsigned long long* count,
+                                                              double* p50, double* p99) {
+  const uint32_t e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const unsigned long long* h = tab.hist + (uint64_t)e * kBins;
+  uint64_t v[kBinsPerLane];
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kBinsPerLane; ++j) {
+    const int b = lane * kBinsPerLane + j;
+    v[j] = (b < (int)kBins) ? h[b] : 0ull;
+    s += v[j];
+  }
+  uint64_t incl = s;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  const uint64_t total = __shfl(incl, kWave - 1);
+  const uint64_t excl = incl - s;
+  if (lane == 0) {
+    count[e] = total;
+    if (total == 0) {
+      p50[e] = NAN;
+      p99[e] = NAN;
+    }
+  }
+  if (total == 0) return;
+  const uint64_t r50 = total * 50ull / 100ull;
+  const uint64_t r99 = total * 99ull / 100ull;
+  if (r50 >= excl && r50 < incl) p50[e] = quantile_from(r50, excl, incl, v, lane);
+  if (r99 >= excl && r99 < incl) p99[e] = quantile_from(r99, excl, incl, v, lane);
+}
+
+using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint16_t*, const uint16_t*,
+                          const uint32_t*, const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
+
+KernelFn pick_kernel(uint32_t E, int* keybits) {
+  const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
+  const bool lds_stats = E <= kLdsEdges;
+  if (keys < (1ull << 18) && lds_stats) {
+    *keybits = 18;
+    return edge_agg_kernel<18, true>;
+  }
+  if (keys < (1ull << 20)) {
+    *keybits = 20;
+    return lds_stats ? edge_agg_kernel<20, true> : edge_agg_kernel<20, false>;
+  }
+  if (keys < (1ull << 22)) {
+    *keybits = 22;
+    return edge_agg_kernel<22, false>;
+  }
+  *keybits = 0;
+  return edge_agg_kernel<0, false>;
+}
+
+// Device table layout inside ctx->d_table.
+struct Layout {
+  uint64_t E;
+  size_t off_hist, off_err, off_sum, off_count, off_p50, off_p99, off_mn, off_mx, bytes;
+  explicit Layout(uint64_t e) : E(e) {
+    off_hist = 0;
+    off_err = off_hist + E * kBins * 8;
+    off_sum = off_err + E * 8;
+    off_count = off_sum + E * 8;
+    off_p50 = off_count + E * 8;
+    off_p99 = off_p50 + E * 8;
+    off_mn = off_p99 + E * 8;
+    off_mx = off_mn + E * 4;
+    bytes = off_mx + E * 4;
+  }
+};
+
+}  // namespace
+}  // namespace anomod
+
+using namespace anomod;
+
+extern "C" {
+
+int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S,
+                                anomod_edge_table* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && spans && out, "anomod_edge_aggregate_spans: NULL argument");
+  ANOMOD_REQUIRE(ctx, S >= 1 && S <= 4096, "n_services=%u out of range [1, 4096]", S);
+  ANOMOD_REQUIRE(ctx, out->n_services == S, "out->n_services=%u != n_services=%u",
+                 out->n_services, S);
+  ANOMOD_REQUIRE(ctx, out->n_bins == kBins, "out->n_bins=%u != ANOMOD_HIST_BINS=%u", out->n_bins,
+                 kBins);
+  ANOMOD_REQUIRE(ctx, spans->device == ctx->device, "span set lives on another device");
+  ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < S,
+                 "span service index %u >= n_services %u", spans->max_svc, S);
+  if (int rc = bind(ctx)) return rc;
+  const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
+  const Layout L(E);
+  if (int rc = ensure_table(ctx, L.bytes)) return rc;
+  char* base = static_cast<char*>(ctx->d_table);
+  Table tab;
+  tab.hist = reinterpret_cast<unsigned long long*>(base + L.off_hist);
+  tab.err = reinterpret_cast<unsigned long long*>(base + L.off_err);
+  tab.sum = reinterpret_cast<unsigned long long*>(base + L.off_sum);
+  tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
+  tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
+  auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
+  auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
+  auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
+
+  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum
+  ANOMOD_HIP(ctx, hipMemsetAsync(tab.mn, 0xFF, E * 4ull, ctx->stream));
+  ANOMOD_HIP(ctx, hipMemsetAsync(tab.mx, 0, E * 4ull, ctx->stream));
+
+  if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
+  if (spans->n_traces > 0) {
+    int keybits = 0;
+    KernelFn fn = pick_kernel(E, &keybits);
+    // One workgroup per CU; more only to keep a workgroup's u32 LDS counters
+    // (errors, min, max) far from 2^32 spans.
+    uint64_t grid = (uint64_t)ctx->num_cus;
+    const uint64_t per_wg_cap = 1ull << 30;
+    if (spans->n_spans / grid > per_wg_cap) grid = (spans->n_spans + per_wg_cap - 1) / per_wg_cap;
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
+                       spans->parent_span_id, spans->svc, spans->flags, spans->dur_us,
+                       spans->trace_ptr, spans->n_traces, S, E, tab);
+    ANOMOD_HIP(ctx, hipGetLastError());
+  }
+  if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
+
+  if (ctx->comm && ctx->nranks > 1) {
+    if (int rc = stage_begin(ctx, kStageEdgeReduce)) return rc;
+    ANOMOD_RCCL(ctx, ncclGroupStart());
+    // hist | err | sum are contiguous u64: one sum all-reduce.
+    ANOMOD_RCCL(ctx, ncclAllReduce(base, base, (size_t)E * kBins + 2ull * E, ncclUint64, ncclSum,
+                                   ctx->comm, ctx->stream));
+    ANOMOD_RCCL(ctx, ncclAllReduce(tab.mn, tab.mn, E, ncclUint32, ncclMin, ctx->comm, ctx->stream));
+    ANOMOD_RCCL(ctx, ncclAllReduce(tab.mx, tab.mx, E, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+    ANOMOD_RCCL(ctx, ncclGroupEnd());
+    if (int rc = stage_end(ctx, kStageEdgeReduce)) return rc;
+  }
+
+  if (int rc = stage_begin(ctx, kStageEdgeFinal)) return rc;
+  hipLaunchKernelGGL(edge_finalize_kernel, dim3(E), dim3(kWave), 0, ctx->stream, tab, count, p50,
+                     p99);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  if (int rc = stage_end(ctx, kStageEdgeFinal)) return rc;
+
+  auto d2h = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    if (!dst) return hipSuccess;
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+  };
+  ANOMOD_HIP(ctx, d2h(out->count, count, E * 8ull));
+  ANOMOD_HIP(ctx, d2h(out->errors, tab.err, E * 8ull));
+  ANOMOD_HIP(ctx, d2h(out->sum_us, tab.sum, E * 8ull));
+  ANOMOD_HIP(ctx, d2h(out->min_us, tab.mn, E * 4ull));
+  ANOMOD_HIP(ctx, d2h(out->max_us, tab.mx, E * 4ull));
+  ANOMOD_HIP(ctx, d2h(out->hist, tab.hist, (size_t)E * kBins * 8ull));
+  ANOMOD_HIP(ctx, d2h(out->p50_us, p50, E * 8ull));
+  ANOMOD_HIP(ctx, d2h(out->p99_us, p99, E * 8ull));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
+int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                          const uint64_t* trace_ptr, uint64_t n_traces, anomod_edge_table* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && soa && out, "anomod_edge_aggregate: NULL argument");
+  anomod_spans* s = nullptr;
+  if (int rc = anomod_spans_upload(ctx, soa, n_spans, trace_ptr, n_traces, &s)) return rc;
+  const int rc = anomod_edge_aggregate_spans(ctx, s, out->n_services, out);
+  anomod_spans_free(s);
+  return rc;
+}
+
+}  // extern "C"

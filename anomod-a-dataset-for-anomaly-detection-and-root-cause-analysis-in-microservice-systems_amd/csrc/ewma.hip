@@ -1,0 +1,254 @@
+// Windowed EWMA / z-score anomaly scoring over the metric matrix
+// (build-defined — the reference only exports the raw
+// series: metric_collector.py:427-443 long CSV rows, fetch_prometheus_
+// metrics.py:53-67 per-query CSV).
+//
+// X is time-major [T][S] f32, so at each step a wave reads 64 consecutive
+// series (256 B, coalesced) and the recurrence runs down T in registers, one
+// series per lane.  The state (m, v in f64, sample count) lives in HBM
+// between calls so an arbitrarily long T is streamed in chunks (400 GB at
+// 10^6 x 10^5 does not fit 288 GB of HBM).  HBM-bound: 4 B/sample read +
+// 4/W B/sample written.  Loads are double-buffered 16 steps deep per lane to
+// keep enough bytes in flight with only S/64 waves on the chip.
+#include <cmath>
+
+#include "common.h"
+#include "synth.h"
+
+struct anomod_series {
+  int device = 0;
+  uint64_t T = 0, S = 0;
+  float* X = nullptr;      // [T][S]
+  float* Z = nullptr;      // [T/W][S] (allocated lazily for the largest W seen)
+  size_t z_cap = 0;
+  double* m = nullptr;     // [S]
+  double* v = nullptr;     // [S]
+  uint32_t* n = nullptr;   // [S] valid samples seen
+};
+
+namespace anomod {
+namespace {
+
+constexpr int kU = 16;  // time steps per load block
+
+struct EwmaState {
+  double m, v;
+  uint32_t n;
+};
+
+__device__ __forceinline__ float ewma_step(EwmaState& st, float x, double alpha, double beta,
+                                           float eps) {
+  if (x != x) return 0.f;  // NaN: missing sample, state carried
+  if (st.n == 0u) {
+    st.m = (double)x;
+    st.v = 0.0;
+    st.n = 1u;
+    return 0.f;
+  }
+  const double d = (double)x - st.m;
+  const float z = (float)d * rsqrtf((float)st.v + eps);
+  st.m = fma(alpha, d, st.m);
+  st.v = beta * fma(alpha * d, d, st.v);
+  st.n += 1u;
+  return z;
+}
+
+__global__ __launch_bounds__(256) void ewma_z_kernel(const float* __restrict__ X, uint64_t T,
+                                                     uint64_t S, double alpha, uint32_t W,
+                                                     float eps, float* __restrict__ Z,
+                                                     double* __restrict__ gm,
+                                                     double* __restrict__ gv,
+                                                     uint32_t* __restrict__ gn) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const double beta = 1.0 - alpha;
+  EwmaState st{gm[s], gv[s], gn[s]};
+  float a[kU], b[kU];
+  const float* col = X + s;
+  auto load = [&](float* buf, uint64_t t0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) buf[u] = (t0 + u < T) ? col[(t0 + u) * S] : NAN;
+  };
+  float wmax = 0.f;
+  uint32_t wpos = 0;
+  uint64_t w = 0;
+  auto consume = [&](const float* buf, uint64_t t0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (t0 + u < T) {
+        const float z = ewma_step(st, buf[u], alpha, beta, eps);
+        wmax = fmaxf(wmax, fabsf(z));
+        if (++wpos == W) {
+          Z[w * S + s] = wmax;
+          ++w;
+          wpos = 0;
+          wmax = 0.f;
+        }
+      }
+    }
+  };
+  load(a, 0);
+  uint64_t t0 = 0;
+  while (t0 < T) {
+    if (t0 + kU < T) load(b, t0 + kU);
+    consume(a, t0);
+    t0 += kU;
+    if (t0 >= T) break;
+    if (t0 + kU < T) load(a, t0 + kU);
+    consume(b, t0);
+    t0 += kU;
+  }
+  gm[s] = st.m;
+  gv[s] = st.v;
+  gn[s] = st.n;
+}
+
+// Synthetic metric matrix: x = mu_s + sigma_s*N(0,1)
+// with a +6 sigma level shift on ~0.1 % of series over a random window.
+__global__ void series_fill_kernel(float* X, uint64_t T, uint64_t S, uint64_t seed, uint64_t t0) {
+  const uint64_t total = T * S;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t t = i / S + t0, s = i % S;
+    const uint64_t hs = splitmix64(seed ^ (s * 0x9E3779B97F4A7C15ull));
+    const float mu = 10.f + (float)(hs & 1023u);
+    const float sigma = 0.5f + (float)((hs >> 10) & 255u) / 32.f;
+    uint32_t c[4] = {(uint32_t)t, (uint32_t)(t >> 32), (uint32_t)s, (uint32_t)(s >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x7u);
+    const float u1 = ((float)(c[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+    float x = mu + sigma * sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
+    if (((hs >> 20) % 1000u) == 0u) {
+      const uint64_t start = (hs >> 32) % 1000003ull, len = 2000ull + ((hs >> 52) & 4095u);
+      if ((t % 1000003ull) >= start && (t % 1000003ull) < start + len) x += 6.f * sigma;
+    }
+    X[i] = x;
+  }
+}
+
+void free_series(anomod_series* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  void* p[] = {s->X, s->Z, s->m, s->v, s->n};
+  for (void* q : p)
+    if (q) (void)hipFree(q);
+  delete s;
+}
+
+}  // namespace
+}  // namespace anomod
+
+using namespace anomod;
+
+extern "C" {
+
+int anomod_series_create(anomod_ctx* ctx, uint64_t T, uint64_t S, anomod_series** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_series_create: NULL argument");
+  *out = nullptr;
+  ANOMOD_REQUIRE(ctx, S >= 1 && T >= 1, "series matrix must be non-empty (T=%llu S=%llu)",
+                 (unsigned long long)T, (unsigned long long)S);
+  if (int rc = bind(ctx)) return rc;
+  auto* s = new anomod_series();
+  s->device = ctx->device;
+  s->T = T;
+  s->S = S;
+  bool ok = hipMalloc(&s->X, T * S * 4) == hipSuccess;
+  ok = ok && hipMalloc(&s->m, S * 8) == hipSuccess;
+  ok = ok && hipMalloc(&s->v, S * 8) == hipSuccess;
+  ok = ok && hipMalloc(&s->n, S * 4) == hipSuccess;
+  if (!ok) {
+    free_series(s);
+    set_error(ctx, "hipMalloc failed for a %llu x %llu series matrix", (unsigned long long)T,
+              (unsigned long long)S);
+    return ANOMOD_ENOMEM;
+  }
+  ANOMOD_HIP(ctx, hipMemsetAsync(s->m, 0, S * 8, ctx->stream));
+  ANOMOD_HIP(ctx, hipMemsetAsync(s->v, 0, S * 8, ctx->stream));
+  ANOMOD_HIP(ctx, hipMemsetAsync(s->n, 0, S * 4, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *out = s;
+  return ANOMOD_OK;
+}
+
+int anomod_series_upload(anomod_ctx* ctx, anomod_series* ser, const float* X) {
+  ANOMOD_REQUIRE(nullptr, ctx && ser && X, "anomod_series_upload: NULL argument");
+  if (int rc = bind(ctx)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ser->X, X, ser->T * ser->S * 4, hipMemcpyHostToDevice,
+                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
+int anomod_series_fill_synthetic(anomod_ctx* ctx, anomod_series* ser, uint64_t seed,
+                                 uint64_t t0) {
+  ANOMOD_REQUIRE(nullptr, ctx && ser, "anomod_series_fill_synthetic: NULL argument");
+  if (int rc = bind(ctx)) return rc;
+  hipLaunchKernelGGL(series_fill_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
+                     ser->X, ser->T, ser->S, seed, t0);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
+int anomod_series_reset_state(anomod_ctx* ctx, anomod_series* ser) {
+  ANOMOD_REQUIRE(nullptr, ctx && ser, "anomod_series_reset_state: NULL argument");
+  if (int rc = bind(ctx)) return rc;
+  ANOMOD_HIP(ctx, hipMemsetAsync(ser->m, 0, ser->S * 8, ctx->stream));
+  ANOMOD_HIP(ctx, hipMemsetAsync(ser->v, 0, ser->S * 8, ctx->stream));
+  ANOMOD_HIP(ctx, hipMemsetAsync(ser->n, 0, ser->S * 4, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
+int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint32_t W, float eps,
+                         float* Z_host) {
+  ANOMOD_REQUIRE(nullptr, ctx && ser, "anomod_series_ewma_z: NULL argument");
+  ANOMOD_REQUIRE(ctx, W >= 1 && ser->T % W == 0, "T=%llu must be a multiple of W=%u",
+                 (unsigned long long)ser->T, W);
+  ANOMOD_REQUIRE(ctx, alpha > 0.f && alpha <= 1.f, "alpha=%g outside (0, 1]", (double)alpha);
+  ANOMOD_REQUIRE(ctx, eps >= 0.f, "eps must be >= 0");
+  if (int rc = bind(ctx)) return rc;
+  const uint64_t nw = ser->T / W;
+  const size_t zbytes = nw * ser->S * 4;
+  if (ser->z_cap < zbytes) {
+    if (ser->Z) ANOMOD_HIP(ctx, hipFree(ser->Z));
+    ser->Z = nullptr;
+    ser->z_cap = 0;
+    if (hipMalloc(&ser->Z, zbytes) != hipSuccess) {
+      set_error(ctx, "hipMalloc(%zu) for window scores failed", zbytes);
+      return ANOMOD_ENOMEM;
+    }
+    ser->z_cap = zbytes;
+  }
+  if (int rc = stage_begin(ctx, kStageEwma)) return rc;
+  const unsigned blocks = (unsigned)((ser->S + 255) / 256);
+  hipLaunchKernelGGL(ewma_z_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ser->X, ser->T,
+                     ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  if (int rc = stage_end(ctx, kStageEwma)) return rc;
+  if (Z_host)
+    ANOMOD_HIP(ctx, hipMemcpyAsync(Z_host, ser->Z, zbytes, hipMemcpyDeviceToHost, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
+int anomod_series_free(anomod_series* ser) {
+  free_series(ser);
+  return ANOMOD_OK;
+}
+
+int anomod_ewma_z(anomod_ctx* ctx, const float* X, uint64_t T, uint64_t S, float alpha,
+                  uint32_t W, float eps, float* Z) {
+  ANOMOD_REQUIRE(nullptr, ctx && X && Z, "anomod_ewma_z: NULL argument");
+  ANOMOD_REQUIRE(ctx, W >= 1 && T % W == 0, "T=%llu must be a multiple of W=%u",
+                 (unsigned long long)T, W);
+  if (T == 0 || S == 0) return ANOMOD_OK;
+  anomod_series* ser = nullptr;
+  if (int rc = anomod_series_create(ctx, T, S, &ser)) return rc;
+  int rc = anomod_series_upload(ctx, ser, X);
+  if (rc == ANOMOD_OK) rc = anomod_series_ewma_z(ctx, ser, alpha, W, eps, Z);
+  free_series(ser);
+  return rc;
+}
+
+}  // extern "C"

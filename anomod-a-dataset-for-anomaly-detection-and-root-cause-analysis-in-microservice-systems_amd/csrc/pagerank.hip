@@ -1,0 +1,329 @@
+// Personalized PageRank root-cause ranking (build-defined,
+// the reference ranks nothing).  Convention = networkx 3.4.2
+// pagerank/_pagerank_scipy: row-normalised weights, x0 = 1/N, dangling mass
+// redistributed along the personalization vector, L1 stopping rule N*tol.
+//
+// GPU form: pull SpMV over the in-edge CSR (transpose of the caller ->
+// callee graph, weights pre-divided by the caller's out-weight), eight lanes
+// per row with a shuffle reduction.  One launch per iteration; the launch
+// also emits per-block partial sums of the new vector's dangling mass (read
+// by the next launch's prologue) and of |x_new - x_old| (the stopping test),
+// so an iteration needs no extra reduction kernel.  The fixed-iteration loop
+// is captured once into a hipGraph and replayed.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "synth.h"
+
+struct anomod_graph {
+  int device = 0;
+  uint32_t N = 0;
+  uint64_t nnz = 0;
+  uint32_t grid = 0;
+  uint32_t* in_ptr = nullptr;  // [N+1]
+  uint32_t* in_col = nullptr;  // [nnz]
+  float* in_w = nullptr;       // [nnz] w / outweight(src)
+  uint8_t* dangling = nullptr; // [N]
+  double* p = nullptr;         // [N]
+  double* x[2] = {nullptr, nullptr};
+  double* dpart[2] = {nullptr, nullptr};  // [grid] dangling-mass partials
+  double* epart = nullptr;     // [grid] L1-change partials
+  // cached fixed-iteration graph
+  hipGraphExec_t exec = nullptr;
+  uint32_t exec_iters = 0;
+  double exec_alpha = 0.0;
+};
+
+namespace anomod {
+namespace {
+
+constexpr int kPprThreads = 256;
+constexpr int kRowLanes = 8;
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(kPprThreads) void ppr_init_kernel(uint32_t N, double x0,
+                                                               const uint8_t* __restrict__ dangling,
+                                                               double* __restrict__ x,
+                                                               double* __restrict__ dpart) {
+  __shared__ double red[kPprThreads / 64];
+  double acc = 0.0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    x[i] = x0;
+    if (dangling[i]) acc += x0;
+  }
+  const double s = block_sum(acc, red);
+  if (threadIdx.x == 0) dpart[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
+    uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
+    const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
+    const double* __restrict__ p, double alpha, const double* __restrict__ x_in,
+    double* __restrict__ x_out, const double* __restrict__ dpart_in, double* __restrict__ dpart_out,
+    double* __restrict__ epart) {
+  __shared__ double red[kPprThreads / 64];
+  __shared__ double s_dsum;
+  // Prologue: dangling mass of x_in from the previous launch's partials.
+  {
+    double a = 0.0;
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) a += dpart_in[i];
+    const double s = block_sum(a, red);
+    if (threadIdx.x == 0) s_dsum = s;
+    __syncthreads();
+  }
+  const double dsum = s_dsum;
+  const int sub = threadIdx.x & (kRowLanes - 1);
+  const uint32_t rows_per_pass = gridDim.x * (blockDim.x / kRowLanes);
+  double dacc = 0.0, eacc = 0.0;
+  for (uint32_t r0 = blockIdx.x * (blockDim.x / kRowLanes); r0 < N; r0 += rows_per_pass) {
+    const uint32_t r = r0 + threadIdx.x / kRowLanes;
+    double acc = 0.0;
+    if (r < N) {
+      const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
+      for (uint32_t k = b + sub; k < e; k += kRowLanes) acc += x_in[in_col[k]] * (double)in_w[k];
+    }
+#pragma unroll
+    for (int off = kRowLanes / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kRowLanes);
+    if (r < N && sub == 0) {
+      const double pr = p[r];
+      const double y = alpha * (acc + dsum * pr) + (1.0 - alpha) * pr;
+      x_out[r] = y;
+      if (dangling[r]) dacc += y;
+      eacc += fabs(y - x_in[r]);
+    }
+  }
+  const double ds = block_sum(dacc, red);
+  const double es = block_sum(eacc, red);
+  if (threadIdx.x == 0) {
+    dpart_out[blockIdx.x] = ds;
+    epart[blockIdx.x] = es;
+  }
+}
+
+void free_graph(anomod_graph* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,
+                g->x[0],   g->x[1],   g->dpart[0], g->dpart[1], g->epart};
+  for (void* q : ps)
+    if (q) (void)hipFree(q);
+  delete g;
+}
+
+// Launch iteration `it` (x[it&1] -> x[(it+1)&1]).
+void launch_iter(anomod_ctx* ctx, anomod_graph* g, double alpha, uint32_t it) {
+  const int a = it & 1, b = a ^ 1;
+  hipLaunchKernelGGL(ppr_iter_kernel, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream, g->N,
+                     g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, g->x[a], g->x[b],
+                     g->dpart[a], g->dpart[b], g->epart);
+}
+
+}  // namespace
+}  // namespace anomod
+
+using namespace anomod;
+
+extern "C" {
+
+int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t* col,
+                        const float* w, uint32_t N, anomod_graph** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_graph_create: NULL argument");
+  *out = nullptr;
+  ANOMOD_REQUIRE(ctx, N >= 1 && row_ptr && col && w, "graph needs N >= 1 and CSR arrays");
+  ANOMOD_REQUIRE(ctx, row_ptr[0] == 0, "row_ptr[0] must be 0");
+  for (uint32_t u = 0; u < N; ++u)
+    ANOMOD_REQUIRE(ctx, row_ptr[u] <= row_ptr[u + 1], "row_ptr decreases at row %u", u);
+  const uint64_t nnz = row_ptr[N];
+  std::vector<double> outw(N, 0.0);
+  std::vector<uint32_t> indeg(N + 1, 0);
+  for (uint32_t u = 0; u < N; ++u) {
+    for (uint32_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) {
+      ANOMOD_REQUIRE(ctx, col[k] < N, "col[%u]=%u out of range", k, col[k]);
+      ANOMOD_REQUIRE(ctx, std::isfinite(w[k]) && w[k] >= 0.f, "weight %u is negative or not finite",
+                     k);
+      outw[u] += (double)w[k];
+      indeg[col[k] + 1]++;
+    }
+  }
+  for (uint32_t v = 0; v < N; ++v) indeg[v + 1] += indeg[v];
+  std::vector<uint32_t> in_col(nnz ? nnz : 1), fill(indeg.begin(), indeg.end() - 1);
+  std::vector<float> in_w(nnz ? nnz : 1);
+  std::vector<uint8_t> dang(N);
+  for (uint32_t u = 0; u < N; ++u) {
+    dang[u] = outw[u] == 0.0;
+    for (uint32_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) {
+      const uint32_t pos = fill[col[k]]++;
+      in_col[pos] = u;
+      in_w[pos] = (float)((double)w[k] / outw[u]);
+    }
+  }
+  if (int rc = bind(ctx)) return rc;
+  auto* g = new anomod_graph();
+  g->device = ctx->device;
+  g->N = N;
+  g->nnz = nnz;
+  g->grid = (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>((N + kPprThreads / kRowLanes - 1) / (kPprThreads / kRowLanes),
+                            (uint64_t)ctx->num_cus * 4));
+  bool ok = hipMalloc(&g->in_ptr, (N + 1) * 4ull) == hipSuccess;
+  ok = ok && hipMalloc(&g->in_col, in_col.size() * 4) == hipSuccess;
+  ok = ok && hipMalloc(&g->in_w, in_w.size() * 4) == hipSuccess;
+  ok = ok && hipMalloc(&g->dangling, N) == hipSuccess;
+  ok = ok && hipMalloc(&g->p, N * 8ull) == hipSuccess;
+  for (int i = 0; i < 2; ++i) {
+    ok = ok && hipMalloc(&g->x[i], N * 8ull) == hipSuccess;
+    ok = ok && hipMalloc(&g->dpart[i], g->grid * 8ull) == hipSuccess;
+  }
+  ok = ok && hipMalloc(&g->epart, g->grid * 8ull) == hipSuccess;
+  if (!ok) {
+    free_graph(g);
+    set_error(ctx, "hipMalloc failed for a graph of %u nodes / %llu edges", N,
+              (unsigned long long)nnz);
+    return ANOMOD_ENOMEM;
+  }
+  hipError_t e = hipMemcpyAsync(g->in_ptr, indeg.data(), (N + 1) * 4ull, hipMemcpyHostToDevice,
+                                ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->in_col, in_col.data(), in_col.size() * 4, hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->in_w, in_w.data(), in_w.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->dangling, dang.data(), N, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    free_graph(g);
+    set_error(ctx, "graph upload failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
+  *out = g;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, uint64_t seed,
+                           anomod_graph** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_graph_synthetic: NULL argument");
+  ANOMOD_REQUIRE(ctx, N >= 2 && mean_degree >= 1, "need N >= 2 and mean_degree >= 1");
+  // Power-law (Pareto, a = 2.2) out-degrees scaled to the requested mean,
+  // 2 % dangling nodes, uniform callees, call-count weights in [1, 1000].
+  std::vector<uint32_t> row_ptr(N + 1, 0), col;
+  std::vector<float> w;
+  uint64_t st = seed;
+  auto next = [&]() { st += 0x9E3779B97F4A7C15ull; return splitmix64(st); };
+  const double a = 2.2, xmin = mean_degree * (a - 2.0) / (a - 1.0);
+  for (uint32_t u = 0; u < N; ++u) {
+    uint64_t d = 0;
+    if (next() % 50 != 0) {
+      const double uu = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+      d = (uint64_t)(xmin * std::pow(uu, -1.0 / (a - 1.0)));
+      d = std::min<uint64_t>(std::max<uint64_t>(d, 1), std::min<uint64_t>(N - 1, 1000));
+    }
+    for (uint64_t j = 0; j < d; ++j) {
+      col.push_back((uint32_t)(next() % N));
+      w.push_back((float)(1 + next() % 1000));
+    }
+    row_ptr[u + 1] = (uint32_t)col.size();
+  }
+  return anomod_graph_create(ctx, row_ptr.data(), col.data(), w.data(), N, out);
+}
+
+int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz) {
+  ANOMOD_REQUIRE(nullptr, g, "anomod_graph_info: graph is NULL");
+  if (N) *N = g->N;
+  if (nnz) *nnz = g->nnz;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
+                          uint32_t iters, double tol, double* x_out, uint32_t* iters_done) {
+  ANOMOD_REQUIRE(nullptr, ctx && g && p && x_out, "anomod_graph_pagerank: NULL argument");
+  ANOMOD_REQUIRE(ctx, alpha > 0.0 && alpha < 1.0, "alpha=%g outside (0, 1)", alpha);
+  ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
+  ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
+  const uint32_t N = g->N;
+  double psum = 0.0;
+  for (uint32_t i = 0; i < N; ++i) {
+    ANOMOD_REQUIRE(ctx, std::isfinite(p[i]) && p[i] >= 0.0, "personalization[%u] invalid", i);
+    psum += p[i];
+  }
+  ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
+  std::vector<double> pn(p, p + N);
+  for (double& v : pn) v /= psum;
+  if (int rc = bind(ctx)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, pn.data(), N * 8ull, hipMemcpyHostToDevice, ctx->stream));
+  const dim3 grid(g->grid), block(kPprThreads);
+  hipLaunchKernelGGL(ppr_init_kernel, grid, block, 0, ctx->stream, N, 1.0 / N, g->dangling,
+                     g->x[0], g->dpart[0]);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  uint32_t done = 0;
+  if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  if (tol > 0.0) {
+    // Convergence mode: host reads the L1 change after every iteration.
+    std::vector<double> ep(g->grid);
+    for (uint32_t it = 0; it < iters; ++it) {
+      launch_iter(ctx, g, alpha, it);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      ANOMOD_HIP(ctx, hipMemcpyAsync(ep.data(), g->epart, g->grid * 8ull, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      done = it + 1;
+      double err = 0.0;
+      for (double v : ep) err += v;
+      if (err < (double)N * tol) break;
+    }
+  } else {
+    // Fixed-iteration mode: replay a captured graph of `iters` launches.
+    if (!g->exec || g->exec_iters != iters || g->exec_alpha != alpha) {
+      if (g->exec) ANOMOD_HIP(ctx, hipGraphExecDestroy(g->exec));
+      g->exec = nullptr;
+      hipGraph_t graph = nullptr;
+      ANOMOD_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+      for (uint32_t it = 0; it < iters; ++it) launch_iter(ctx, g, alpha, it);
+      ANOMOD_HIP(ctx, hipStreamEndCapture(ctx->stream, &graph));
+      hipError_t e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      ANOMOD_HIP(ctx, e);
+      g->exec_iters = iters;
+      g->exec_alpha = alpha;
+    }
+    ANOMOD_HIP(ctx, hipGraphLaunch(g->exec, ctx->stream));
+    done = iters;
+  }
+  if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(x_out, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (iters_done) *iters_done = done;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_free(anomod_graph* g) {
+  free_graph(g);
+  return ANOMOD_OK;
+}
+
+int anomod_pagerank(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t* col, const float* w,
+                    uint32_t N, const double* p, double alpha, uint32_t iters, double tol,
+                    double* x_out, uint32_t* iters_done) {
+  anomod_graph* g = nullptr;
+  if (int rc = anomod_graph_create(ctx, row_ptr, col, w, N, &g)) return rc;
+  const int rc = anomod_graph_pagerank(ctx, g, p, alpha, iters, tol, x_out, iters_done);
+  free_graph(g);
+  return rc;
+}
+
+}  // extern "C"

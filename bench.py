@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Headline benchmark: spans/s aggregated into bit-exact call-graph edge
+histograms (+ % of HBM peak), with RCA PageRank iters/s and EWMA/z
+samples/s alongside (BASELINE.json metric).
+
+One process per GPU.  N=1:  python bench.py
+N>1 (driver):  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+               --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Each rank generates its own shard of synthetic DeathStarBench-SocialNetwork
+spans directly in HBM (generation is outside the
+timed region), runs K aggregation steps and — for N > 1 — the RCCL
+all-reduce of the integer edge table inside every step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG_DIR = ROOT / "anomod-a-dataset-for-anomaly-detection-and-root-cause-analysis-in-microservice-systems_amd"
+for _p in (str(PKG_DIR), str(ROOT)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+import anomod  # noqa: E402
+from anomod import _lib as L  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
+METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
+
+
+def algorithmic_bytes(n_spans: int, n_traces: int) -> int:
+    """Bytes the edge-aggregation kernel must read once: span_id 8 +
+    parent_span_id 8 + svc 2 + flags 2 + dur_us 4 = 24 B/span, plus the
+    8-B trace_ptr entries (trace_hash only picks the shard: not read)."""
+    return 24 * n_spans + 8 * (n_traces + 1)
+
+
+def cpu_baseline(spec, n_traces: int, threads: int, min_seconds: float) -> dict:
+    """The C oracle (oracle/liboracle.so) on host cores over a bounded
+    sample of the same synthetic workload, one trace range per thread."""
+    from oracle import native
+
+    sample = anomod.synth_generate_host(spec, n_traces)
+    S = len(sample.services)
+    native.lib()
+    bounds = np.linspace(0, sample.n_traces, threads + 1).astype(np.int64)
+
+    def work(i):
+        native.edge_aggregate(sample, S, int(bounds[i]), int(bounds[i + 1]))
+
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    return {"value": sample.n_spans * passes / el, "unit": "spans/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{sample.n_spans} synthetic SN spans ({n_traces} traces) x {passes} "
+                      f"passes in {el:.1f} s, C oracle, {threads} threads"}
+
+
+def load_traffic(n_spans: int) -> float | None:
+    """HBM bytes per launch from the committed PMC profile of this workload."""
+    p = ROOT / "profiles" / "edge_agg_pmc.json"
+    try:
+        d = json.loads(p.read_text())
+        if int(d["n_spans"]) == n_spans:
+            return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--traces-per-gpu", type=int, default=1 << 27)
+    ap.add_argument("--seed", type=int, default=20251103)
+    ap.add_argument("--cpu-traces", type=int, default=1 << 21)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip PageRank / EWMA legs")
+    ap.add_argument("--ppr-nodes", type=int, default=100_000)
+    ap.add_argument("--ppr-iters", type=int, default=100)
+    ap.add_argument("--ewma-series", type=int, default=100_000)
+    ap.add_argument("--ewma-steps", type=int, default=7680)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    tdist = None
+    if world > 1:
+        import torch.distributed as tdist  # host-side control plane only (gloo)
+
+        tdist.init_process_group("gloo")
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    def barrier():
+        if tdist is not None:
+            tdist.barrier()
+
+    def allmax(v: float) -> float:
+        if tdist is None:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allsum(v: float) -> float:
+        if tdist is None:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+        return float(t.item())
+
+    ctx = anomod.Context(local)
+    if world > 1:
+        from anomod import dist
+
+        dist.attach_rccl(ctx, dist.RankInfo(rank, world, local))
+
+    spec = anomod.SynthSpec("SN", seed=args.seed, p_orphan_ppm=100)
+    spans = ctx.generate(spec, args.traces_per_gpu, shard=rank)  # this rank's traces, in HBM
+
+    for _ in range(args.warmup):
+        ctx.edge_aggregate(spans, with_hist=False)
+    ctx.synchronize()
+    barrier()
+    ctx.synchronize()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        table = ctx.edge_aggregate(spans, with_hist=False)
+        kernel_ms.append(ctx.stage_ms(L.STAGE_EDGE_AGG))
+    ctx.synchronize()
+    barrier()
+    el = allmax(time.perf_counter() - t0)
+    total_spans = allsum(float(spans.n_spans))
+    assert int(table.count.sum()) == (int(total_spans) if world > 1 else spans.n_spans)
+
+    k_ms = float(np.mean(kernel_ms))
+    bytes_launch = algorithmic_bytes(spans.n_spans, spans.n_traces)
+    achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+    traffic = load_traffic(spans.n_spans)
+    result = {
+        "metric": METRIC,
+        "value": total_spans * args.steps / el,
+        "unit": "spans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (DeathStarBench SocialNetwork topology, generated in HBM)",
+        "config": {
+            "workload": "config 3 shape: synthetic SN spans grouped by trace, "
+                        f"{args.traces_per_gpu} traces (~{spans.n_spans / 1e9:.2f}e9 spans) "
+                        "per GPU, edge table + 896-bin histograms + p50/p99 per step",
+            "spans_per_gpu": spans.n_spans, "traces_per_gpu": spans.n_traces,
+            "services": len(spans.services), "hist_bins": L.HIST_BINS,
+            "parallelism": f"dp{world} (traceId shards)" + (" + RCCL all-reduce" if world > 1
+                                                            else ""),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+            "kernel": "edge_agg_kernel<18,true>", "kernel_ms": k_ms,
+            "bytes_per_launch": bytes_launch,
+        },
+    }
+    spans.free()
+
+    if not args.no_extras:
+        # --- PageRank RCA: replicas (one graph + personalization per GPU)
+        g = anomod.DeviceGraph(ctx, synthetic=(args.ppr_nodes, 10, 11 + rank))
+        p = np.random.default_rng(rank).random(g.N)
+        g.pagerank(p, iters=args.ppr_iters)  # capture + warm
+        reps = 10
+        barrier()
+        t0 = time.perf_counter()
+        pr_ms = []
+        for _ in range(reps):
+            g.pagerank(p, iters=args.ppr_iters)
+            pr_ms.append(ctx.stage_ms(L.STAGE_PAGERANK))
+        pel = allmax(time.perf_counter() - t0)
+        ppr_bytes = 4 * (g.N + 1) + 8 * g.nnz + 16 * g.N  # in_ptr + (col,w) + x gather/write
+        result["pagerank"] = {
+            "iters_per_s": world * reps * args.ppr_iters / pel,
+            "device_iters_per_s_per_gpu": args.ppr_iters / (np.mean(pr_ms) * 1e-3),
+            "nodes": g.N, "edges": g.nnz, "iters_per_solve": args.ppr_iters,
+            "mode": "replicas (independent personalization per GPU, no collective)",
+            "bytes_per_iter": ppr_bytes,
+            "achieved_GBps": ppr_bytes * args.ppr_iters / (np.mean(pr_ms) * 1e-3) / 1e9,
+        }
+        g.free()
+        # --- EWMA/z over a [T][S] f32 chunk resident in HBM (config 4 shape)
+        ser = anomod.DeviceSeries(ctx, args.ewma_steps, args.ewma_series)
+        ser.fill_synthetic(7 + rank)
+        ser.ewma_z(2 / 61, 60, download=False)
+        ew = []
+        for _ in range(5):
+            ser.reset_state()
+            ser.ewma_z(2 / 61, 60, download=False)
+            ew.append(ctx.stage_ms(L.STAGE_EWMA))
+        e_ms = float(np.mean(ew))
+        samples = args.ewma_steps * args.ewma_series
+        e_bytes = 4 * samples + 4 * samples // 60 + 20 * args.ewma_series
+        result["ewma"] = {
+            "samples_per_s": allsum(samples / (e_ms * 1e-3)),
+            "T": args.ewma_steps, "S": args.ewma_series, "W": 60, "kernel_ms": e_ms,
+            "achieved_GBps": e_bytes / (e_ms * 1e-3) / 1e9,
+            "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+        }
+        ser.free()
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        result["cpu_baseline"] = cpu_baseline(spec, args.cpu_traces, threads, args.cpu_seconds)
+
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if tdist is not None:
+        tdist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,234 @@
+/*
+ * anomod.h — C ABI of the MI355X-native AnoMod RCA-feature engine (libanomod.so).
+ *
+ * The reference (EvoTestOps/AnoMod, /root/reference) has no FFI: its hot path is
+ * a CLI + file boundary driven by bash.  Each entry point below
+ * names the reference code it replaces (path:line relative to the reference
+ * root).  Everything is `extern "C"`, plain pointers and sizes; no torch types.
+ *
+ * Conventions
+ *  - Every function returns an int status: ANOMOD_OK (0) or a negative code; a
+ *    human-readable message is available from anomod_last_error(ctx) (or
+ *    anomod_last_error(NULL) for errors raised before a ctx exists).
+ *  - Host buffers are caller-owned; no pointer is retained after a call
+ *    returns and inputs are never mutated (unlike trace_collector.py:415, which
+ *    mutates the span dicts it is handed).
+ *  - Empty input (n == 0) is not an error: outputs are zero/empty tables and
+ *    status is ANOMOD_OK (mirrors jaeger_to_csv.py:92-97, which writes a
+ *    header-only CSV and exits 0).
+ *  - One ctx per host thread; a ctx owns one HIP device, one stream and,
+ *    optionally, one RCCL communicator.
+ */
+#ifndef ANOMOD_H
+#define ANOMOD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ANOMOD_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+#define ANOMOD_OK 0
+#define ANOMOD_EINVAL (-1)  /* bad argument / shape                           */
+#define ANOMOD_EHIP (-2)    /* HIP runtime error (no device, launch failure)  */
+#define ANOMOD_ERCCL (-3)   /* RCCL error                                     */
+#define ANOMOD_ENOMEM (-4)  /* device or host allocation failed               */
+#define ANOMOD_ESTATE (-5)  /* call not valid in this state                   */
+
+/* ---- span flags (anomod_span_soa.flags) --------------------------------- */
+/* Error bit.  SN/Jaeger: tags["error"] == true or http.status_code >= 500
+ * (tags kept at jaeger_to_csv.py:55-67,88).  TT/SkyWalking: isError
+ * (trace_collector.py:471).                                                 */
+#define ANOMOD_FLAG_ERROR 0x1u
+
+/* ---- latency histogram (build-defined) ---------------
+ * Integer log-linear ("HDR") binning of a u32 microsecond latency v:
+ *   v <  64 : bin = v                                 (exact)
+ *   v >= 64 : e = floor(log2 v) - 5 ; bin = 32*e + (v >> e)
+ * 32 sub-buckets per octave (<= 3.1 % relative bin width), 896 bins cover the
+ * whole u32 range.                                                          */
+#define ANOMOD_HIST_SUB_BITS 5
+#define ANOMOD_HIST_BINS 896
+
+/* ---- edge table layout ---------------------------------------------------
+ * For S services the table has E = (S + 2) * S rows; row = p * S + c where c
+ * is the child span's service and p is the parent span's service, or
+ *   p == S     : ROOT   — the span carries no parent reference
+ *                (jaeger_to_csv.py:34-38 leaves parent_span_id = '';
+ *                 trace_collector.py:427-437 yields parent_node None)
+ *   p == S + 1 : ORPHAN — a parent reference that names no span of the same
+ *                trace (trace_collector.py:443 counts these among the roots). */
+#define ANOMOD_ROOT_ROWS 2
+
+typedef struct anomod_ctx anomod_ctx;       /* device + stream + comm      */
+typedef struct anomod_spans anomod_spans;   /* device-resident span set    */
+typedef struct anomod_series anomod_series; /* device-resident X[T][S]     */
+typedef struct anomod_graph anomod_graph;   /* device-resident CSR graph   */
+
+/* Span set in struct-of-arrays form, grouped by trace: the spans of trace t
+ * are [trace_ptr[t], trace_ptr[t+1]).  span_id 0 is reserved; a
+ * parent_span_id of 0 means "no parent reference".  Collectors already emit
+ * spans grouped by trace (jaeger_to_csv.py:21-32 iterates trace -> spans;
+ * trace_collector.py:539-546 emits per-trace span lists).                   */
+typedef struct {
+  const uint64_t* trace_hash;      /* [n] shard key (may be NULL)          */
+  const uint64_t* span_id;         /* [n]                                  */
+  const uint64_t* parent_span_id;  /* [n]                                  */
+  const uint16_t* svc;             /* [n] service index (< n_services)     */
+  const uint16_t* flags;           /* [n] ANOMOD_FLAG_*                    */
+  const uint32_t* dur_us;          /* [n] latency in microseconds          */
+} anomod_span_soa;
+
+/* Writable twin of anomod_span_soa (download / host generation targets). */
+typedef struct {
+  uint64_t* trace_hash;
+  uint64_t* span_id;
+  uint64_t* parent_span_id;
+  uint16_t* svc;
+  uint16_t* flags;
+  uint32_t* dur_us;
+} anomod_span_soa_out;
+
+/* Per-edge aggregate.  Every pointer may be NULL (that output is skipped).
+ * Arrays have E = (n_services + 2) * n_services rows; hist has E * n_bins. */
+typedef struct {
+  uint32_t n_services;  /* in : S                                         */
+  uint32_t n_bins;      /* in : must equal ANOMOD_HIST_BINS               */
+  uint64_t* count;      /* [E] spans on the edge                          */
+  uint64_t* errors;     /* [E] spans with ANOMOD_FLAG_ERROR               */
+  uint64_t* sum_us;     /* [E] sum of latencies                           */
+  uint32_t* min_us;     /* [E] UINT32_MAX when count == 0                 */
+  uint32_t* max_us;     /* [E] 0 when count == 0                          */
+  uint64_t* hist;       /* [E * n_bins] latency histogram                 */
+  double* p50_us;       /* [E] histogram quantile, rank (n*50)//100       */
+  double* p99_us;       /* [E] histogram quantile, rank (n*99)//100       */
+} anomod_edge_table;
+
+/* ---- library / context ---------------------------------------------------*/
+int anomod_abi_version(void);
+const char* anomod_last_error(const anomod_ctx* ctx);
+int anomod_device_count(int* out);
+int anomod_ctx_create(int device, anomod_ctx** out);
+int anomod_ctx_destroy(anomod_ctx* ctx);
+int anomod_ctx_synchronize(anomod_ctx* ctx);
+/* Milliseconds of the last launch of a stage, measured with hipEvents on the
+ * ctx stream.  stage: 0 = edge aggregation kernel, 1 = edge finalize kernel,
+ * 2 = edge all-reduce, 3 = ewma kernel, 4 = pagerank iterations.          */
+int anomod_ctx_stage_ms(const anomod_ctx* ctx, int stage, double* ms);
+
+/* ---- histogram helpers (host) ------------------------------------------- */
+uint32_t anomod_hist_bin(uint32_t v);
+int anomod_hist_bin_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi);
+
+/* ---- span sets -----------------------------------------------------------*/
+/* Copy a host span set to HBM.  Replaces the in-memory hand-off between
+ * json.load and the per-span loop of jaeger_to_csv.py:12-32 /
+ * trace_collector.py:519-531.                                              */
+int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                        const uint64_t* trace_ptr, uint64_t n_traces, anomod_spans** out);
+int anomod_spans_info(const anomod_spans* spans, uint64_t* n_spans, uint64_t* n_traces);
+int anomod_spans_download(anomod_ctx* ctx, const anomod_spans* spans,
+                          const anomod_span_soa_out* dst, uint64_t* trace_ptr);
+int anomod_spans_free(anomod_spans* spans);
+
+/* ---- synthetic workload ----------------------*/
+#define ANOMOD_TOPO_SN 0 /* DeathStarBench SocialNetwork, 12 services        */
+#define ANOMOD_TOPO_TT 1 /* TrainTicket, 46 services                         */
+
+typedef struct {
+  uint32_t topology;          /* ANOMOD_TOPO_*                               */
+  uint32_t fault_service;     /* service index with an injected fault, or
+                                 UINT32_MAX for a normal run                 */
+  uint64_t seed;              /* Philox4x32-10 key                           */
+  uint32_t fault_latency_mult;/* latency multiplier on the faulty service    */
+  uint32_t p_error_ppm;       /* base error probability (parts per million)  */
+  uint32_t p_fault_error_ppm; /* error probability on the faulty service     */
+  uint32_t p_orphan_ppm;      /* probability a non-root span loses its parent*/
+} anomod_synth_spec;
+
+int anomod_synth_n_services(uint32_t topology, uint32_t* out);
+/* Service name of index i (sorted-name order, cf. trace_collector.py:536). */
+const char* anomod_synth_service_name(uint32_t topology, uint32_t i);
+/* Host generation (same code path as the device generator): first count the
+ * spans of traces [0, n_traces) of shard `shard`, then fill caller buffers.
+ * dst arrays have n_spans entries, trace_ptr has n_traces + 1.             */
+int anomod_synth_count_host(const anomod_synth_spec* spec, uint64_t shard, uint64_t n_traces,
+                            uint64_t* n_spans);
+int anomod_synth_generate_host(const anomod_synth_spec* spec, uint64_t shard, uint64_t n_traces,
+                               const anomod_span_soa_out* dst, uint64_t* trace_ptr);
+/* Device generation straight into HBM (no PCIe), bit-identical to host.    */
+int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64_t shard,
+                          uint64_t n_traces, anomod_spans** out);
+
+/* ---- edge aggregation (the hot path) -------------------------------------
+ * Call-graph edge table with per-edge latency histogram, count, errors,
+ * sum/min/max and p50/p99.  Replaces and extends the per-span loops of
+ * jaeger_to_csv.py:21-90 (parent = first CHILD_OF ref, service from
+ * processID) and trace_collector.py:401-481 (_build_span_records parent
+ * resolution) + the per-service aggregation of
+ * enhanced_trace_collector.py:216-296.  Integer results are bit-exact and
+ * independent of launch geometry, shard count and span order within a trace
+ * set.  When a communicator is attached the table is summed over all ranks
+ * (RCCL all-reduce) before quantiles are taken.                            */
+int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
+                                anomod_edge_table* out);
+/* One-shot host convenience: upload + aggregate + download.               */
+int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                          const uint64_t* trace_ptr, uint64_t n_traces, anomod_edge_table* out);
+
+/* ---- windowed EWMA / z-score -------------------------
+ * X is time-major [T][S] f32 (NaN = missing sample).  Per series:
+ *   d_t = x_t - m_{t-1};  z_t = d_t / sqrt(v_{t-1} + eps)
+ *   m_t = m_{t-1} + alpha*d_t;  v_t = (1-alpha)*(v_{t-1} + alpha*d_t^2)
+ * with m = x, v = 0, z = 0 at the first valid sample; NaN samples leave the
+ * state untouched and score 0.  Z[w][s] = max |z_t| over t in window w of W
+ * steps (T must be a multiple of W).  m/v equal pandas
+ * Series.ewm(alpha, adjust=False).mean() / .var(bias=True).  The metric
+ * matrix replaces the long CSV rows of metric_collector.py:427-443 and
+ * fetch_prometheus_metrics.py:53-67.                                       */
+int anomod_ewma_z(anomod_ctx* ctx, const float* X, uint64_t T, uint64_t S, float alpha,
+                  uint32_t W, float eps, float* Z);
+/* Device-resident streaming variant: X stays in HBM, the (m, v, n) state is
+ * carried across calls so T can be processed in chunks.                   */
+int anomod_series_create(anomod_ctx* ctx, uint64_t T, uint64_t S, anomod_series** out);
+int anomod_series_upload(anomod_ctx* ctx, anomod_series* ser, const float* X);
+int anomod_series_fill_synthetic(anomod_ctx* ctx, anomod_series* ser, uint64_t seed,
+                                 uint64_t t0);
+int anomod_series_reset_state(anomod_ctx* ctx, anomod_series* ser);
+int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint32_t W,
+                         float eps, float* Z_host /* may be NULL */);
+int anomod_series_free(anomod_series* ser);
+
+/* ---- personalized PageRank RCA -----------------------
+ * networkx 3.4.2 pagerank convention: out-edge CSR (row = caller) with
+ * weights; rows are normalised by out-weight; dangling mass is sent along
+ * the personalization p; x0 = 1/N;
+ *   x <- alpha*(x A + sum_{dangling} x * p) + (1 - alpha)*p
+ * stop when ||x - x_last||_1 < N*tol (tol > 0) or after `iters` iterations.
+ * iters_done = iterations executed; status ANOMOD_OK even when tol was not
+ * reached (caller checks iters_done == iters).                            */
+int anomod_pagerank(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t* col,
+                    const float* w, uint32_t N, const double* p, double alpha, uint32_t iters,
+                    double tol, double* x_out, uint32_t* iters_done);
+int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t* col,
+                        const float* w, uint32_t N, anomod_graph** out);
+int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, uint64_t seed,
+                           anomod_graph** out);
+int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz);
+int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
+                          uint32_t iters, double tol, double* x_out, uint32_t* iters_done);
+int anomod_graph_free(anomod_graph* g);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------*/
+#define ANOMOD_UNIQUE_ID_BYTES 128
+int anomod_comm_unique_id(uint8_t* out /* ANOMOD_UNIQUE_ID_BYTES */);
+int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks, int rank);
+int anomod_ctx_comm_info(const anomod_ctx* ctx, int* nranks, int* rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ANOMOD_H */

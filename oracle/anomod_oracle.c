@@ -1,0 +1,191 @@
+/*
+ * anomod_oracle.c — CPU restatement of the AnoMod hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the
+ * checker / the timed CPU port — never as part of the product path.
+ *
+ * Written from scratch in plain C, one function per hot-path stage, each
+ * citing the reference code (paths relative to /root/reference) it restates:
+ *
+ *  - parent resolution: the parent of a span is the span of the SAME trace
+ *    whose id equals the span's parent reference — jaeger_to_csv.py:34-38
+ *    (first CHILD_OF ref, '' when none) and trace_collector.py:424-443
+ *    (same segment / refs[0]; a parent that is not in the trace makes the
+ *    span a root).  First match in trace order wins.
+ *  - edge table / histogram / quantiles: absent in the reference (SURVEY.md
+ *    §0.3, §8a a10-a11); nearest-rank index (n*q)//100 follows
+ *    monitor_http_responses.py:180-190.
+ *  - EWMA/z: absent in the reference (§8a a12); pinned by pandas
+ *    Series.ewm(alpha, adjust=False) in tests/golden.
+ *  - PageRank: absent in the reference (§8a a13); networkx 3.4.2
+ *    _pagerank_scipy convention, pinned by networkx in tests/golden.
+ *
+ * Parity status: the decode rules are pinned by golden vectors produced by
+ * the reference's own code (tests/golden/gen/make_goldens.py); the
+ * build-defined stages are pinned against pandas / networkx goldens.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define OR_SUB_BITS 5u
+#define OR_BINS 896u
+
+uint32_t oracle_hist_bin(uint32_t v) {
+  if (v < 64u) return v;
+  uint32_t lg = 31u - (uint32_t)__builtin_clz(v);
+  uint32_t e = lg - OR_SUB_BITS;
+  return (e << OR_SUB_BITS) + (v >> e);
+}
+
+void oracle_hist_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi) {
+  if (bin < 64u) {
+    *lo = *hi = bin;
+    return;
+  }
+  uint32_t e = (bin >> OR_SUB_BITS) - 1u;
+  uint64_t m = (uint64_t)(bin & ((1u << OR_SUB_BITS) - 1u)) + (1u << OR_SUB_BITS);
+  *lo = (uint32_t)(m << e);
+  *hi = (uint32_t)(((m + 1) << e) - 1);
+}
+
+/* Accumulate traces [t0, t1) into the caller's tables (E = (S+2)*S rows:
+ * row = p*S + c, p = S for ROOT, S+1 for ORPHAN).  The caller zeroes
+ * count/err/sum/hist/mx and sets mn to UINT32_MAX. */
+void oracle_edge_aggregate(uint32_t S, const uint64_t* span_id, const uint64_t* parent,
+                           const uint16_t* svc, const uint16_t* flags, const uint32_t* dur,
+                           const uint64_t* trace_ptr, uint64_t t0, uint64_t t1, uint64_t* count,
+                           uint64_t* err, uint64_t* sum, uint32_t* mn, uint32_t* mx,
+                           uint64_t* hist) {
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t a = trace_ptr[t], b = trace_ptr[t + 1];
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t pid = parent[i];
+      uint32_t p = S;
+      if (pid != 0) {
+        p = S + 1;
+        for (uint64_t q = a; q < b; ++q) {
+          if (span_id[q] == pid) {
+            p = svc[q];
+            break;
+          }
+        }
+      }
+      const uint64_t e = (uint64_t)p * S + svc[i];
+      const uint32_t d = dur[i];
+      count[e] += 1;
+      if (flags[i] & 1u) err[e] += 1;
+      sum[e] += d;
+      if (d < mn[e]) mn[e] = d;
+      if (d > mx[e]) mx[e] = d;
+      hist[e * OR_BINS + oracle_hist_bin(d)] += 1;
+    }
+  }
+}
+
+/* Nearest-rank quantile from a histogram row: rank r = (n*q_pct)//100
+ * (monitor_http_responses.py:187-189), value = midpoint of the bin that
+ * holds the r-th (0-based) sample; NaN when the row is empty. */
+void oracle_quantiles(const uint64_t* hist, uint64_t E, uint32_t q_pct, double* out) {
+  for (uint64_t e = 0; e < E; ++e) {
+    const uint64_t* h = hist + e * OR_BINS;
+    uint64_t n = 0;
+    for (uint32_t b = 0; b < OR_BINS; ++b) n += h[b];
+    if (n == 0) {
+      out[e] = NAN;
+      continue;
+    }
+    const uint64_t r = n * q_pct / 100u;
+    uint64_t c = 0;
+    for (uint32_t b = 0; b < OR_BINS; ++b) {
+      c += h[b];
+      if (r < c) {
+        uint32_t lo, hi;
+        oracle_hist_bounds(b, &lo, &hi);
+        out[e] = 0.5 * ((double)lo + (double)hi);
+        break;
+      }
+    }
+  }
+}
+
+/* Windowed EWMA/z-score (f64 state and f64 z).  X is [T][S]; Z is [T/W][S]. */
+void oracle_ewma_z(const float* X, uint64_t T, uint64_t S, double alpha, uint32_t W, double eps,
+                   float* Z) {
+  const double beta = 1.0 - alpha;
+  for (uint64_t s = 0; s < S; ++s) {
+    double m = 0.0, v = 0.0;
+    uint64_t n = 0;
+    double wmax = 0.0;
+    uint32_t wpos = 0;
+    uint64_t w = 0;
+    for (uint64_t t = 0; t < T; ++t) {
+      const float x = X[t * S + s];
+      double z = 0.0;
+      if (x == x) {
+        if (n == 0) {
+          m = x;
+          v = 0.0;
+        } else {
+          const double d = (double)x - m;
+          z = d / sqrt(v + eps);
+          m = m + alpha * d;
+          v = beta * (v + alpha * d * d);
+        }
+        ++n;
+      }
+      if (fabs(z) > wmax) wmax = fabs(z);
+      if (++wpos == W) {
+        Z[w * S + s] = (float)wmax;
+        ++w;
+        wpos = 0;
+        wmax = 0.0;
+      }
+    }
+  }
+}
+
+/* Personalized PageRank, networkx 3.4.2 _pagerank_scipy convention, push
+ * form over the out-edge CSR.  p must already sum to 1.  Returns iterations
+ * executed; stops when ||x - xlast||_1 < N*tol (tol > 0) or after iters. */
+uint32_t oracle_pagerank(const uint32_t* row_ptr, const uint32_t* col, const float* w, uint32_t N,
+                         const double* p, double alpha, uint32_t iters, double tol,
+                         double* x_out) {
+  double* outw = (double*)calloc(N, sizeof(double));
+  double* x = (double*)malloc(N * sizeof(double));
+  double* y = (double*)malloc(N * sizeof(double));
+  for (uint32_t u = 0; u < N; ++u) {
+    for (uint32_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) outw[u] += (double)w[k];
+    x[u] = 1.0 / N;
+  }
+  uint32_t it = 0;
+  for (; it < iters;) {
+    double dsum = 0.0;
+    for (uint32_t u = 0; u < N; ++u) {
+      y[u] = 0.0;
+      if (outw[u] == 0.0) dsum += x[u];
+    }
+    for (uint32_t u = 0; u < N; ++u) {
+      if (outw[u] == 0.0) continue;
+      for (uint32_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k)
+        y[col[k]] += x[u] * ((double)w[k] / outw[u]);
+    }
+    double err = 0.0;
+    for (uint32_t u = 0; u < N; ++u) {
+      y[u] = alpha * (y[u] + dsum * p[u]) + (1.0 - alpha) * p[u];
+      err += fabs(y[u] - x[u]);
+    }
+    double* tmp = x;
+    x = y;
+    y = tmp;
+    ++it;
+    if (tol > 0.0 && err < (double)N * tol) break;
+  }
+  memcpy(x_out, x, N * sizeof(double));
+  free(outw);
+  free(x);
+  free(y);
+  return it;
+}

@@ -1,0 +1,103 @@
+"""ctypes binding of oracle/liboracle.so (test infrastructure only)."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+BINS = 896
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        _lib = C.CDLL(str(LIB))
+        P = C.POINTER
+        _lib.oracle_hist_bin.restype = C.c_uint32
+        _lib.oracle_hist_bin.argtypes = [C.c_uint32]
+        _lib.oracle_hist_bounds.argtypes = [C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
+        _lib.oracle_edge_aggregate.argtypes = [C.c_uint32] + [C.c_void_p] * 6 + [
+            C.c_uint64, C.c_uint64] + [C.c_void_p] * 6
+        _lib.oracle_quantiles.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
+        _lib.oracle_ewma_z.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_double,
+                                       C.c_uint32, C.c_double, C.c_void_p]
+        _lib.oracle_pagerank.restype = C.c_uint32
+        _lib.oracle_pagerank.argtypes = [C.c_void_p] * 3 + [C.c_uint32, C.c_void_p, C.c_double,
+                                                            C.c_uint32, C.c_double, C.c_void_p]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def hist_bin(v: int) -> int:
+    return lib().oracle_hist_bin(v)
+
+
+def new_tables(S: int) -> dict:
+    E = (S + 2) * S
+    return {"count": np.zeros(E, np.uint64), "errors": np.zeros(E, np.uint64),
+            "sum_us": np.zeros(E, np.uint64), "min_us": np.full(E, 0xFFFFFFFF, np.uint32),
+            "max_us": np.zeros(E, np.uint32), "hist": np.zeros((E, BINS), np.uint64)}
+
+
+def edge_aggregate(spans, S: int | None = None, t0: int = 0, t1: int | None = None,
+                   tables: dict | None = None) -> dict:
+    """Accumulate traces [t0, t1) of a SpanSet-like object into tables."""
+    S = len(spans.services) if S is None else S
+    t1 = spans.n_traces if t1 is None else t1
+    tab = new_tables(S) if tables is None else tables
+    arrs = [np.ascontiguousarray(getattr(spans, k)) for k in
+            ("span_id", "parent_span_id", "svc", "flags", "dur_us", "trace_ptr")]
+    lib().oracle_edge_aggregate(S, *[_p(a) for a in arrs], t0, t1, _p(tab["count"]),
+                                _p(tab["errors"]), _p(tab["sum_us"]), _p(tab["min_us"]),
+                                _p(tab["max_us"]), _p(tab["hist"]))
+    return tab
+
+
+def quantiles(hist: np.ndarray, q_pct: int) -> np.ndarray:
+    hist = np.ascontiguousarray(hist, np.uint64)
+    out = np.empty(hist.shape[0])
+    lib().oracle_quantiles(_p(hist), hist.shape[0], q_pct, _p(out))
+    return out
+
+
+def finalize(tab: dict) -> dict:
+    tab["p50_us"] = quantiles(tab["hist"], 50)
+    tab["p99_us"] = quantiles(tab["hist"], 99)
+    return tab
+
+
+def ewma_z(X: np.ndarray, alpha: float, W: int, eps: float = 1e-12) -> np.ndarray:
+    X = np.ascontiguousarray(X, np.float32)
+    T, S = X.shape
+    Z = np.empty((T // W, S), np.float32)
+    lib().oracle_ewma_z(_p(X), T, S, alpha, W, eps, _p(Z))
+    return Z
+
+
+def pagerank(row_ptr, col, w, p, alpha=0.85, iters=100, tol=1e-10):
+    row_ptr = np.ascontiguousarray(row_ptr, np.uint32)
+    col = np.ascontiguousarray(col, np.uint32)
+    w = np.ascontiguousarray(w, np.float32)
+    p = np.asarray(p, np.float64)
+    p = np.ascontiguousarray(p / p.sum())
+    N = row_ptr.shape[0] - 1
+    x = np.empty(N)
+    if col.size == 0:
+        col, w = np.zeros(1, np.uint32), np.zeros(1, np.float32)
+    it = lib().oracle_pagerank(_p(row_ptr), _p(col), _p(w), N, _p(p), alpha, iters, tol, _p(x))
+    return x, it

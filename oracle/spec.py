@@ -1,0 +1,200 @@
+"""Pure-Python / numpy restatement of the reference's per-span rules
+(TEST INFRASTRUCTURE ONLY — see oracle/__init__.py).
+
+Written independently of the product decoders in anomod/decode.py so the two
+can be checked against each other and against the reference goldens.
+"""
+from __future__ import annotations
+
+import math
+from collections import deque
+
+import numpy as np
+
+
+# ---- SN / Jaeger: jaeger_to_csv.py:21-90 ---------------------------------
+def jaeger_rows(doc: dict) -> list[dict]:
+    rows = []
+    for trace in doc.get("data", []):                                   # :21
+        tid = trace.get("traceID", "")                                   # :22
+        p2s = {k: v.get("serviceName", "") for k, v in trace.get("processes", {}).items()}
+        for span in trace.get("spans", []):                              # :32
+            parent = ""
+            for ref in span.get("references", []):                       # :35-38
+                if ref.get("refType") == "CHILD_OF":
+                    parent = ref.get("spanID", "")
+                    break
+            tags = {}
+            for tag in span.get("tags", []):                             # :55-58
+                tags[tag.get("key", "")] = tag.get("value", "")
+            rows.append({"trace_id": tid, "span_id": span.get("spanID", ""),
+                         "parent_span_id": parent,
+                         "service": p2s.get(span.get("processID", ""), ""),  # :45-46
+                         "duration_us": span.get("duration", 0), "tags": tags})  # :83
+    return rows
+
+
+# ---- TT / SkyWalking: trace_collector.py:401-481 ---------------------------
+def build_span_records(spans: list[dict]):
+    """node ids, parent node ids, children, depth (BFS from roots), roots."""
+    nodes, parents, children, order = {}, {}, {}, []
+    for span in spans:                                                   # :409-417
+        seg, sid = span.get("segmentId"), span.get("spanId")
+        if seg is None or sid is None:
+            order.append(None)
+            continue
+        nid = f"{seg}:{sid}"
+        order.append(nid)
+        nodes[nid] = span
+        children.setdefault(nid, [])
+    for span, nid in zip(spans, order):                                  # :420-439
+        if nid is None:
+            continue
+        pn = None
+        psid = span.get("parentSpanId", -1)
+        if isinstance(psid, int) and psid >= 0:
+            pn = f"{span.get('segmentId')}:{psid}"
+        else:
+            refs = span.get("refs") or []
+            if refs:
+                ps, pp = refs[0].get("parentSegmentId"), refs[0].get("parentSpanId")
+                if ps is not None and pp is not None:
+                    pn = f"{ps}:{pp}"
+        parents[nid] = pn
+        if pn and pn in children:
+            children[pn].append(nid)
+    depth = {}
+    roots = [n for n, p in parents.items() if p not in nodes]            # :443
+    q = deque((n, 0) for n in roots)
+    while q:                                                             # :445-449
+        cur, d = q.popleft()
+        depth[cur] = d
+        for ch in children.get(cur, []):
+            q.append((ch, d + 1))
+    recs = []
+    for span, nid in zip(spans, order):                                  # :452-479
+        if nid is None:
+            continue
+        recs.append({"node_id": nid, "parent_node_id": parents.get(nid),
+                     "children": list(children.get(nid, [])), "depth": depth.get(nid, 0),
+                     "duration_ms": max(0, span.get("endTime", 0) - span.get("startTime", 0)),
+                     "is_error": bool(span.get("isError", False)),
+                     "service_code": span.get("serviceCode")})
+    return recs, roots
+
+
+# ---- enhanced_trace_collector.py:216-296 ----------------------------------
+def analyze_trace_patterns(traces: list[dict]) -> dict:
+    if not traces:
+        return {"total_traces": 0, "unique_services": [], "unique_endpoints": [],
+                "error_traces": 0, "service_call_counts": {}, "endpoint_call_counts": {},
+                "latency_stats": None, "time_range": {"earliest": None, "latest": None}}
+    svc_c, ep_c, lat, err = {}, {}, [], 0
+    lo = hi = None
+    for t in traces:
+        s = t.get("service_name", "unknown")
+        svc_c[s] = svc_c.get(s, 0) + 1
+        e = t.get("endpoint_name", "unknown")
+        ep_c[e] = ep_c.get(e, 0) + 1
+        if t.get("is_error", 0) == 1:
+            err += 1
+        if t.get("latency", 0) > 0:
+            lat.append(t["latency"])
+        st = t.get("start_time", 0)
+        if st:
+            lo = st if lo is None or st < lo else lo
+            hi = st if hi is None or st > hi else hi
+    stats = ({"min": min(lat), "max": max(lat), "avg": sum(lat) / len(lat), "count": len(lat)}
+             if lat else [])
+    return {"total_traces": len(traces), "unique_services": sorted(svc_c),
+            "unique_endpoints": sorted(ep_c), "error_traces": err,
+            "service_call_counts": svc_c, "endpoint_call_counts": ep_c, "latency_stats": stats,
+            "time_range": {"earliest": lo, "latest": hi}}
+
+
+# ---- monitor_http_responses.py:180-190 ------------------------------------
+def nearest_rank(values, q_pct: int):
+    v = sorted(values)
+    return v[len(v) * q_pct // 100]
+
+
+# ---- histogram binning (build-defined, include/anomod.h) ------------------
+def hist_bin(v: int) -> int:
+    if v < 64:
+        return v
+    e = v.bit_length() - 1 - 5
+    return (e << 5) + (v >> e)
+
+
+def hist_bounds(b: int) -> tuple[int, int]:
+    if b < 64:
+        return b, b
+    e = (b >> 5) - 1
+    m = (b & 31) + 32
+    return m << e, ((m + 1) << e) - 1
+
+
+def edge_table_py(spans, S: int) -> dict:
+    """Pure-Python edge table for tiny span sets (first match in trace order)."""
+    E = (S + 2) * S
+    out = {"count": [0] * E, "errors": [0] * E, "sum_us": [0] * E,
+           "min_us": [0xFFFFFFFF] * E, "max_us": [0] * E, "hist": {}}
+    for t in range(spans.n_traces):
+        a, b = int(spans.trace_ptr[t]), int(spans.trace_ptr[t + 1])
+        for i in range(a, b):
+            pid = int(spans.parent_span_id[i])
+            p = S
+            if pid:
+                p = S + 1
+                for q in range(a, b):
+                    if int(spans.span_id[q]) == pid:
+                        p = int(spans.svc[q])
+                        break
+            e = p * S + int(spans.svc[i])
+            d = int(spans.dur_us[i])
+            out["count"][e] += 1
+            out["errors"][e] += int(spans.flags[i]) & 1
+            out["sum_us"][e] += d
+            out["min_us"][e] = min(out["min_us"][e], d)
+            out["max_us"][e] = max(out["max_us"][e], d)
+            k = (e, hist_bin(d))
+            out["hist"][k] = out["hist"].get(k, 0) + 1
+    return out
+
+
+# ---- EWMA / z-score (build-defined; pandas ewm adjust=False) --------------
+def ewma_state(x: np.ndarray, alpha: float):
+    """Per-step (m, v) of one series, NaN samples skipped (ignore_na=True)."""
+    m = np.full(x.shape[0], np.nan)
+    v = np.full(x.shape[0], np.nan)
+    cm = cv = None
+    for t, xv in enumerate(x.astype(np.float64)):
+        if not math.isnan(xv):
+            if cm is None:
+                cm, cv = xv, 0.0
+            else:
+                d = xv - cm
+                cm = cm + alpha * d
+                cv = (1 - alpha) * (cv + alpha * d * d)
+        if cm is not None:
+            m[t], v[t] = cm, cv
+    return m, v
+
+
+def window_scores_from_state(X: np.ndarray, M: np.ndarray, V: np.ndarray, W: int,
+                             eps: float) -> np.ndarray:
+    """Z[w, s] = max |z_t| over window w, z_t = (x_t - m_{t-1})/sqrt(v_{t-1}+eps)."""
+    T, S = X.shape
+    Z = np.zeros((T // W, S))
+    for s in range(S):
+        seen = False
+        for t in range(T):
+            x = float(X[t, s])
+            z = 0.0
+            if not math.isnan(x):
+                if seen:
+                    z = (x - M[t - 1, s]) / math.sqrt(V[t - 1, s] + eps)
+                seen = True
+            # carry state across NaNs: M/V at t-1 already hold the last state
+            Z[t // W, s] = max(Z[t // W, s], abs(z))
+    return Z

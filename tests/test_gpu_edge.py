@@ -1,0 +1,158 @@
+"""GPU parity: HIP edge aggregation (libanomod) vs the CPU oracle, bit-exact."""
+import json
+
+import numpy as np
+import pytest
+
+import anomod
+from oracle import native
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("count", "errors", "sum_us", "min_us", "max_us")
+
+
+def assert_table_equal(gpu: anomod.EdgeTable, ref: dict):
+    for k in FIELDS:
+        np.testing.assert_array_equal(getattr(gpu, k), ref[k], err_msg=k)
+    if gpu.hist is not None:
+        np.testing.assert_array_equal(gpu.hist, ref["hist"], err_msg="hist")
+    ref = native.finalize(ref)
+    np.testing.assert_array_equal(gpu.p50_us, ref["p50_us"])  # NaN == NaN here
+    np.testing.assert_array_equal(gpu.p99_us, ref["p99_us"])
+
+
+def _random_spanset(rng, S, n_traces, max_len, orphan=0.05, dup=0.0, wide_dur=True):
+    lens = rng.integers(0, max_len + 1, n_traces)
+    ptr = np.zeros(n_traces + 1, np.uint64)
+    np.cumsum(lens, out=ptr[1:])
+    n = int(ptr[-1])
+    sid = rng.integers(1, 2**63, n, dtype=np.uint64)
+    pid = np.zeros(n, np.uint64)
+    t_of = np.repeat(np.arange(n_traces), lens)
+    starts = ptr[:-1].astype(np.int64)[t_of]
+    pos = np.arange(n) - starts
+    has_parent = pos > 0
+    pick = starts + (rng.random(n) * np.maximum(pos, 1)).astype(np.int64)
+    pid[has_parent] = sid[pick[has_parent]]
+    orph = has_parent & (rng.random(n) < orphan)
+    pid[orph] = rng.integers(1, 2**63, int(orph.sum()), dtype=np.uint64)
+    if dup:
+        d = has_parent & (rng.random(n) < dup)
+        sid[d] = sid[pick[d]]  # duplicate span ids inside a trace
+    svc = rng.integers(0, S, n).astype(np.uint16)
+    flg = (rng.random(n) < 0.1).astype(np.uint16)
+    if wide_dur:
+        dur = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        dur[rng.random(n) < 0.7] %= 20000
+    else:
+        dur = rng.integers(50, 5000, n).astype(np.uint32)
+    return anomod.SpanSet([f"svc{i:03d}" for i in range(S)], ptr, sid.copy(), sid, pid, svc, flg,
+                          dur)
+
+
+def test_native_library_is_loaded(ctx):
+    assert anomod.LIB_PATH.exists()
+    assert anomod.device_count() >= 1
+
+
+@pytest.mark.parametrize("S,n_traces,max_len", [
+    (1, 100, 5), (3, 2000, 12), (12, 20000, 24), (20, 5000, 30),  # LDS-stat variants
+    (46, 5000, 60),   # TrainTicket width: 22-bit keys, HBM stats
+    (100, 2000, 40),  # beyond LDS keys: all-HBM path
+])
+def test_random_sets_bit_exact(ctx, S, n_traces, max_len):
+    rng = np.random.default_rng(S * 1000 + n_traces)
+    sp = _random_spanset(rng, S, n_traces, max_len, dup=0.02)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_big_traces(ctx):
+    rng = np.random.default_rng(7)
+    parts = [_random_spanset(rng, 12, 50, 10), _random_spanset(rng, 12, 3, 3000),
+             _random_spanset(rng, 12, 200, 20), _random_spanset(rng, 12, 1, 257)]
+    sp = anomod.SpanSet.concat(parts)
+    assert np.diff(sp.trace_ptr).max() > 256
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_empty_and_degenerate(ctx):
+    svcs = ["a", "b"]
+    empty = anomod.SpanSet(svcs, np.zeros(1, np.uint64), *(np.zeros(0, t) for t in
+                           (np.uint64, np.uint64, np.uint64, np.uint16, np.uint16, np.uint32)))
+    t = ctx.edge_aggregate(empty)
+    assert t.count.sum() == 0 and np.isnan(t.p50_us).all()
+    assert (t.min_us == 0xFFFFFFFF).all()
+    # traces with zero spans between real ones, self-parent, parent == 0
+    sp = anomod.SpanSet(svcs, np.array([0, 0, 3, 3, 4], np.uint64),
+                        np.zeros(4, np.uint64), np.array([5, 6, 7, 9], np.uint64),
+                        np.array([0, 5, 6, 9], np.uint64), np.array([0, 1, 1, 0], np.uint16),
+                        np.array([1, 0, 0, 0], np.uint16),
+                        np.array([0, 2**32 - 1, 64, 7], np.uint32))
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_counter_wrap_and_table_saturation(ctx):
+    # one (edge, bin) hit millions of times: exercises the packed-count wrap
+    n = 3_000_000
+    ptr = np.arange(0, n + 1, 2, dtype=np.uint64)
+    sid = np.arange(1, n + 1, dtype=np.uint64)
+    pid = np.where(np.arange(n) % 2 == 1, sid - 1, 0).astype(np.uint64)
+    sp = anomod.SpanSet(["x", "y"], ptr, sid, sid, pid, (np.arange(n) % 2).astype(np.uint16),
+                        np.zeros(n, np.uint16), np.full(n, 1234, np.uint32))
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+    # every bin of many edges: more distinct keys than LDS slots
+    rng = np.random.default_rng(11)
+    sp = _random_spanset(rng, 16, 60000, 30)
+    sp.dur_us[:] = rng.integers(0, 2**32, sp.n_spans, dtype=np.uint64).astype(np.uint32)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_device_generation_matches_host(ctx):
+    for topo, n in (("SN", 50000), ("TT", 5000)):
+        spec = anomod.SynthSpec(topo, seed=99, p_orphan_ppm=3000,
+                                fault_service=3)
+        dev = ctx.generate(spec, n)
+        host = anomod.synth_generate_host(spec, n)
+        got = dev.download()
+        for k in ("trace_ptr", "trace_hash", "span_id", "parent_span_id", "svc", "flags",
+                  "dur_us"):
+            np.testing.assert_array_equal(getattr(got, k), getattr(host, k), err_msg=k)
+        assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(host))
+
+
+def test_jaeger_golden_edge_table(ctx, golden):
+    doc = json.loads((golden / "jaeger_small.json").read_text())
+    sp = anomod.decode_jaeger(doc)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_skywalking_golden_edge_table(ctx, golden):
+    g = json.loads((golden / "skywalking_small.json").read_text())
+    sp = anomod.decode_skywalking_raw(g["inputs"])
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+def test_shards_sum_to_whole(ctx):
+    sp = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=5, p_orphan_ppm=1000), 40000)
+    whole = ctx.edge_aggregate(sp)
+    parts = [ctx.edge_aggregate(sp.shard(3, r)) for r in range(3)]
+    np.testing.assert_array_equal(sum(p.count for p in parts), whole.count)
+    np.testing.assert_array_equal(sum(p.hist for p in parts), whole.hist)
+    np.testing.assert_array_equal(np.minimum.reduce([p.min_us for p in parts]), whole.min_us)
+    np.testing.assert_array_equal(np.maximum.reduce([p.max_us for p in parts]), whole.max_us)
+
+
+@pytest.mark.slow
+def test_large_synthetic_full_parity(ctx):
+    """~72 M spans generated in HBM: full oracle parity + conservation."""
+    spec = anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=500)
+    dev = ctx.generate(spec, 1 << 23)
+    t1 = ctx.edge_aggregate(dev)
+    t2 = ctx.edge_aggregate(dev)
+    for k in FIELDS:
+        np.testing.assert_array_equal(getattr(t1, k), getattr(t2, k))  # deterministic
+    assert int(t1.count.sum()) == dev.n_spans
+    np.testing.assert_array_equal(t1.hist.sum(axis=1), t1.count)
+    host = dev.download()
+    assert_table_equal(t1, native.edge_aggregate(host))

@@ -1,0 +1,95 @@
+"""GPU parity: EWMA/z kernel vs pandas golden + C oracle; PageRank vs
+networkx golden + C oracle; the load -> features -> rank surface."""
+import numpy as np
+import pytest
+
+import anomod
+from oracle import native, spec
+
+pytestmark = pytest.mark.gpu
+
+# z is computed in f32 from f64 state on the GPU (f64 in the oracle): 1e-5 rel.
+Z_RTOL, Z_ATOL = 1e-5, 1e-5
+
+
+def test_ewma_matches_pandas_golden(ctx, golden):
+    g = np.load(golden / "ewma_pandas.npz")
+    X, M, V, a = g["X"], g["mean"], g["var"], float(g["alpha"])
+    W, eps = 60, 1e-12
+    Z = ctx.ewma_z(X, a, W, eps)
+    np.testing.assert_allclose(Z, spec.window_scores_from_state(X, M, V, W, eps),
+                               rtol=Z_RTOL, atol=Z_ATOL)
+
+
+@pytest.mark.parametrize("T,S,W", [(60, 1, 60), (600, 1000, 60), (4800, 77, 16), (256, 5000, 1)])
+def test_ewma_matches_oracle(ctx, T, S, W):
+    rng = np.random.default_rng(T + S)
+    X = (rng.uniform(0, 1e4, S) + rng.uniform(0.1, 10, S) * rng.standard_normal((T, S)))
+    X = X.astype(np.float32)
+    X[rng.random((T, S)) < 0.01] = np.nan
+    a = 2.0 / (W + 1) if W > 1 else 0.3
+    np.testing.assert_allclose(ctx.ewma_z(X, a, W), native.ewma_z(X, a, W),
+                               rtol=Z_RTOL, atol=Z_ATOL)
+
+
+def test_ewma_streaming_chunks_equal_one_pass(ctx):
+    rng = np.random.default_rng(1)
+    T, S, W = 1200, 300, 60
+    X = (100 + rng.standard_normal((T, S))).astype(np.float32)
+    one = ctx.ewma_z(X, 2 / 61, W)
+    ser = anomod.DeviceSeries(ctx, T // 2, S)
+    ser.upload(X[: T // 2])
+    z1 = ser.ewma_z(2 / 61, W)
+    ser.upload(X[T // 2:])
+    z2 = ser.ewma_z(2 / 61, W)
+    np.testing.assert_array_equal(np.concatenate([z1, z2]), one)
+    ser.free()
+
+
+def test_pagerank_matches_networkx_golden(ctx, golden):
+    g = np.load(golden / "pagerank_networkx.npz")
+    x, it = ctx.pagerank(g["row_ptr"], g["col"], g["w"], g["p"], float(g["alpha"]),
+                         iters=1000, tol=1e-12)
+    assert it < 1000
+    assert np.abs(x - g["x"]).sum() < 1e-5
+
+
+def test_pagerank_fixed_iters_matches_oracle(ctx):
+    rng = np.random.default_rng(4)
+    N = 20000
+    deg = rng.integers(0, 20, N)
+    deg[rng.random(N) < 0.05] = 0
+    row_ptr = np.zeros(N + 1, np.uint32)
+    np.cumsum(deg, out=row_ptr[1:])
+    col = rng.integers(0, N, int(row_ptr[-1])).astype(np.uint32)
+    w = rng.integers(1, 1000, col.size).astype(np.float32)
+    p = rng.random(N)
+    for iters in (1, 2, 37, 100):
+        x, it = ctx.pagerank(row_ptr, col, w, p, 0.85, iters=iters, tol=0.0)
+        xr, itr = native.pagerank(row_ptr, col, w, p, 0.85, iters=iters, tol=0.0)
+        assert it == itr == iters
+        assert np.abs(x - xr).sum() < 1e-5
+
+
+def test_device_graph_replay(ctx):
+    g = anomod.DeviceGraph(ctx, synthetic=(100000, 10, 11))
+    assert g.N == 100000 and g.nnz > 500000
+    p = np.random.default_rng(0).random(g.N)
+    x1, _ = g.pagerank(p, iters=100)
+    x2, _ = g.pagerank(p, iters=100)
+    np.testing.assert_array_equal(x1, x2)
+    assert abs(x1.sum() - 1.0) < 1e-6
+    g.free()
+
+
+def test_features_and_rank_find_injected_fault(ctx):
+    fault = "post-storage-service"
+    base = anomod.load_experiment(anomod.SynthSpec("SN", seed=21), n_traces=20000)
+    exp = anomod.load_experiment(anomod.SynthSpec("SN", seed=22, fault_service=fault),
+                                 n_traces=20000)
+    fb = anomod.features(base, ctx)
+    fe = anomod.features(exp, ctx, baseline=fb)
+    assert fe.edges.count.sum() == exp.spans.n_spans
+    assert fe.window_scores is not None and fe.window_scores.shape[0] == 480 // 60
+    ranking = anomod.rank(fe, ctx=ctx)
+    assert anomod.hit_at(ranking, fault, 3) == 1.0
