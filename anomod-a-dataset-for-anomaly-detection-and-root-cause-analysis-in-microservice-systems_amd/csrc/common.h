@@ -46,11 +46,9 @@ struct anomod_spans {
   uint64_t* trace_hash = nullptr;
   uint64_t* span_id = nullptr;
   uint64_t* parent_span_id = nullptr;
-  uint16_t* svc = nullptr;
-  uint16_t* flags = nullptr;
+  uint32_t* svc_flags = nullptr;  // svc | flags << 16 (one 4-B load per span)
   uint32_t* dur_us = nullptr;
   uint64_t* trace_ptr = nullptr;  // [n_traces + 1]
-  void* base = nullptr;           // single allocation backing every array
 };
 
 #define ANOMOD_HIP(ctx, expr)                                                               \

@@ -41,24 +41,28 @@ constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWave * kWavesPerWG;
 constexpr int kStage = 256;  // spans staged per wave chunk
 constexpr int kPer = kStage / kWave;
-constexpr int kHtLog2 = 14;
+constexpr int kHtLog2 = 13;
 constexpr uint32_t kHtSlots = 1u << kHtLog2;
-constexpr int kMaxProbe = 64;
+constexpr int kMaxProbe = 48;
 constexpr uint32_t kLdsEdges = 512;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
+// Experiment-only ablations (never set in the shipped build): 1 = no stats,
+// 2 = no histogram, 4 = no parent scan.
+#ifndef ANOMOD_ABL
+#define ANOMOD_ABL 0
+#endif
 
 // LDS carve (bytes, every offset a multiple of 16).
-constexpr int kOffHt = 0;
-constexpr int kOffSum = kOffHt + (int)kHtSlots * 4;
+constexpr int kOffHt = 0;                                // u64 slots (count<<32 | key)
+constexpr int kOffSum = kOffHt + (int)kHtSlots * 8;
 constexpr int kOffErr = kOffSum + (int)kLdsEdges * 8;
 constexpr int kOffMin = kOffErr + (int)kLdsEdges * 4;
 constexpr int kOffMax = kOffMin + (int)kLdsEdges * 4;
 constexpr int kOffWave = kOffMax + (int)kLdsEdges * 4;
-constexpr int kWSid = 0;
-constexpr int kWSvc = kWSid + kStage * 8;
-constexpr int kWTix = kWSvc + kStage * 2;
-constexpr int kWTs = kWTix + kStage;
-constexpr int kWBytes = kWTs + 144;
+constexpr int kWSid = 0;                        // u64 span ids [kStage + 8]
+constexpr int kWSvc = kWSid + (kStage + 8) * 8;  // u16 services [kStage + 8]
+constexpr int kWFlag = kWSvc + (kStage + 8) * 2; // u8 trace-start flags [kStage]
+constexpr int kWBytes = kWFlag + kStage;
 constexpr int kLdsBytes = kOffWave + kWavesPerWG * kWBytes;
 static_assert(kWBytes % 16 == 0, "wave staging must stay 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
@@ -71,35 +75,42 @@ struct Table {
   unsigned int* mx;          // [E]
 };
 
+struct Cols {
+  const uint64_t* __restrict__ span_id;
+  const uint64_t* __restrict__ parent;
+  const uint32_t* __restrict__ svcfl;  // svc | flags << 16
+  const uint32_t* __restrict__ dur;
+};
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Packed LDS hash-table increment of histogram key `kidx` (edge*kBins+bin).
-// Slot word = (count << KEYBITS) | (kidx + 1); 0 = empty.
-template <int KEYBITS>
-__device__ __forceinline__ void ht_add(uint32_t* ht, uint32_t kidx,
+// Histogram increment of key kidx = edge*kBins + bin in the workgroup's LDS
+// hash table.  Slot = (count << 32) | (kidx + 1); 0 = empty.  A resident key
+// costs one LDS read + one fire-and-forget ds_add_u64; a workgroup sees
+// < 2^32 spans so the count half never carries into the key half.
+template <bool LDS_HIST>
+__device__ __forceinline__ void ht_add(unsigned long long* ht, uint32_t kidx,
                                        unsigned long long* __restrict__ ghist) {
-  if constexpr (KEYBITS == 0) {
+  if constexpr (!LDS_HIST) {
     atomicAdd(&ghist[kidx], 1ull);
   } else {
-    constexpr uint32_t kKeyMask = (1u << KEYBITS) - 1u;
-    constexpr uint32_t kInc = 1u << KEYBITS;
-    constexpr uint32_t kCntMax = (1u << (32 - KEYBITS)) - 1u;
     const uint32_t key = kidx + 1u;
     uint32_t h = (key * 0x9E3779B1u) >> (32 - kHtLog2);
     for (int probe = 0; probe < kMaxProbe; ++probe) {
-      uint32_t cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (cur == 0u) {
-        const uint32_t prev = atomicCAS(&ht[h], 0u, key | kInc);
-        if (prev == 0u) return;
+      unsigned long long cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (cur == 0ull) {
+        const unsigned long long ins = (1ull << 32) | key;
+        const unsigned long long prev = atomicCAS(&ht[h], 0ull, ins);
+        if (prev == 0ull) return;
         cur = prev;
       }
-      if ((cur & kKeyMask) == key) {
-        const uint32_t old = atomicAdd(&ht[h], kInc);
-        if ((old >> KEYBITS) == kCntMax) atomicAdd(&ghist[kidx], (unsigned long long)kCntMax + 1ull);
+      if ((uint32_t)cur == key) {
+        atomicAdd(&ht[h], 1ull << 32);
         return;
       }
       h = (h + 1u) & (kHtSlots - 1u);
@@ -108,11 +119,13 @@ __device__ __forceinline__ void ht_add(uint32_t* ht, uint32_t kidx,
   }
 }
 
-template <int KEYBITS, bool LDS_STATS>
+template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
                                        const Table& tab) {
-  ht_add<KEYBITS>(reinterpret_cast<uint32_t*>(smem + kOffHt), edge * kBins + hist_bin(d),
-                  tab.hist);
+  if constexpr (!(ANOMOD_ABL & 2))
+    ht_add<LDS_HIST>(reinterpret_cast<unsigned long long*>(smem + kOffHt),
+                     edge * kBins + hist_bin(d), tab.hist);
+  if constexpr (ANOMOD_ABL & 1) return;
   if constexpr (LDS_STATS) {
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
@@ -133,12 +146,9 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
 // A trace longer than kStage: wave-cooperative scan of the trace's span ids,
 // staged kStage at a time through the wave's LDS area (O(L^2 / 64) per trace;
 // rare — real traces are tens of spans).
-template <int KEYBITS, bool LDS_STATS>
+template <bool LDS_HIST, bool LDS_STATS>
 __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uint64_t lo,
-                          uint64_t hi, const uint64_t* __restrict__ span_id,
-                          const uint64_t* __restrict__ parent, const uint16_t* __restrict__ svc,
-                          const uint16_t* __restrict__ flags, const uint32_t* __restrict__ dur,
-                          uint32_t S, const Table& tab) {
+                          uint64_t hi, const Cols& col, uint32_t S, const Table& tab) {
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
   for (uint64_t i0 = lo; i0 < hi; i0 += kWave) {
@@ -147,10 +157,11 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
     uint64_t pid = 0;
     uint32_t d = 0, fl = 0, c = 0;
     if (active) {
-      pid = parent[i];
-      d = dur[i];
-      fl = flags[i];
-      c = svc[i];
+      pid = col.parent[i];
+      d = col.dur[i];
+      const uint32_t sf = col.svcfl[i];
+      c = sf & 0xFFFFu;
+      fl = sf >> 16;
     }
     uint32_t p = (pid == 0) ? S : S + 1u;
     bool done = !active || pid == 0;
@@ -158,8 +169,8 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
       if (__all(done)) break;
       const uint32_t m = (uint32_t)((hi - q0) < (uint64_t)kStage ? (hi - q0) : (uint64_t)kStage);
       for (uint32_t q = lane; q < m; q += kWave) {
-        lsid[q] = span_id[q0 + q];
-        lsvc[q] = svc[q0 + q];
+        lsid[q] = col.span_id[q0 + q];
+        lsvc[q] = (uint16_t)col.svcfl[q0 + q];
       }
       wave_sync();
       if (!done) {
@@ -173,25 +184,178 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
       }
       wave_sync();
     }
-    if (active) record<KEYBITS, LDS_STATS>(smem, p * S + c, d, fl, tab);
+    if (active) record<LDS_HIST, LDS_STATS>(smem, p * S + c, d, fl, tab);
   }
 }
 
-template <int KEYBITS, bool LDS_STATS>
+// One wave's chunk: up to 64 consecutive traces holding <= kStage spans, or a
+// single trace longer than kStage (k == 0).
+struct Chunk {
+  uint64_t base;   // first span
+  uint32_t k;      // traces in the chunk (0 = one big trace)
+  uint32_t n;      // spans in the chunk
+  uint32_t start;  // this lane's trace start relative to base (lanes < k)
+};
+
+// Span columns of a chunk held in registers while the previous chunk is
+// processed (software pipeline, one chunk ahead).
+struct Regs {
+  uint64_t sid[kPer], pid[kPer];
+  uint32_t dur[kPer], sf[kPer];  // sf = svc | flags << 16
+};
+
+__device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane, uint64_t lo,
+                                            uint64_t hi) {
+  Chunk c;
+  const bool valid = t + lane < t_end;
+  const uint64_t b = __shfl(lo, 0);
+  c.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
+  c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
+  const uint32_t n = c.k ? (uint32_t)(__shfl(hi, (int)c.k - 1) - c.base)
+                         : (uint32_t)(__shfl(hi, 0) - c.base);
+  c.n = (uint32_t)__builtin_amdgcn_readfirstlane(n);
+  c.start = (uint32_t)(lo - c.base);
+  return c;
+}
+
+__device__ __forceinline__ void load_bounds(const uint64_t* __restrict__ trace_ptr, uint64_t t,
+                                            uint64_t t_end, int lane, uint64_t& lo, uint64_t& hi) {
+  lo = hi = 0;
+  if (t + lane < t_end) {
+    lo = trace_ptr[t + lane];
+    hi = trace_ptr[t + lane + 1];
+  }
+}
+
+__device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int lane, Regs& R) {
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    R.sid[r] = R.pid[r] = 0;
+    R.dur[r] = R.sf[r] = 0;
+    if (c.k && i < c.n) {
+      R.sid[r] = col.span_id[c.base + i];
+      R.pid[r] = col.parent[c.base + i];
+      R.sf[r] = col.svcfl[c.base + i];
+      R.dur[r] = col.dur[c.base + i];
+    }
+  }
+}
+
+// Bounds [a, b) of the trace holding chunk position i = 64*r + lane, from the
+// four 64-bit trace-start masks (wave-uniform).
+__device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, int lane,
+                                             uint32_t n, uint32_t& a, uint32_t& b) {
+  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+  uint64_t m = Sm[r] & le;
+  a = 0;
+  if (m) {
+    a = 64u * r + 63u - (uint32_t)__clzll((long long)m);
+  } else {
+    for (int q = r - 1; q >= 0; --q) {
+      if (Sm[q]) {
+        a = 64u * q + 63u - (uint32_t)__clzll((long long)Sm[q]);
+        break;
+      }
+    }
+  }
+  m = Sm[r] & ~le;
+  b = n;
+  if (m) {
+    b = 64u * r + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+  } else {
+    for (int q = r + 1; q < kPer; ++q) {
+      if (Sm[q]) {
+        b = 64u * q + (uint32_t)__ffsll((unsigned long long)Sm[q]) - 1u;
+        break;
+      }
+    }
+  }
+  if (b > n) b = n;
+}
+
+// First span of [a, b) whose id equals pid (4 ids per step via ds_read_b128).
+__device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
+                                           uint64_t pid) {
+  for (uint32_t q0 = a & ~1u; q0 < b; q0 += 4) {
+    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
+    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
+    int hit = -1;
+    if (q0 + 3 >= a && q0 + 3 < b && v1.y == pid) hit = (int)q0 + 3;
+    if (q0 + 2 >= a && q0 + 2 < b && v1.x == pid) hit = (int)q0 + 2;
+    if (q0 + 1 >= a && q0 + 1 < b && v0.y == pid) hit = (int)q0 + 1;
+    if (q0 >= a && v0.x == pid) hit = (int)q0;
+    if (hit >= 0) return hit;
+  }
+  return -1;
+}
+
+template <bool LDS_HIST, bool LDS_STATS>
+__device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
+                                              const Chunk& c, const Regs& R, const Cols& col,
+                                              uint32_t S, const Table& tab) {
+  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
+  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
+  auto* lflag = reinterpret_cast<uint8_t*>(wsm + kWFlag);
+  // Stage ids / services; mark trace starts.
+  reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    if (i < c.n) {
+      lsid[i] = R.sid[r];
+      lsvc[i] = (uint16_t)R.sf[r];
+    }
+  }
+  if ((uint32_t)lane < c.k && c.start < c.n) lflag[c.start] = 1;
+  wave_sync();
+  uint64_t Sm[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) Sm[r] = __ballot(lflag[lane + r * kWave] != 0);
+  uint32_t pidx[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    pidx[r] = S;  // ROOT
+    if (i < c.n && R.pid[r] != 0ull) {
+      pidx[r] = S + 1u;  // ORPHAN unless found in the trace
+      if constexpr (!(ANOMOD_ABL & 4)) {
+        uint32_t a, b;
+        trace_bounds(Sm, r, lane, c.n, a, b);
+        const int q = find_parent(lsid, a, b, R.pid[r]);
+        if (q >= 0) pidx[r] = 0x80000000u | (uint32_t)q;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    if (i < c.n) {
+      const uint32_t p = (pidx[r] & 0x80000000u) ? (uint32_t)lsvc[pidx[r] & 0xFFFFu] : pidx[r];
+      record<LDS_HIST, LDS_STATS>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r], R.sf[r] >> 16,
+                                  tab);
+    }
+  }
+  wave_sync();
+}
+
+template <bool LDS_HIST, bool LDS_STATS>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
-    const uint16_t* __restrict__ svc, const uint16_t* __restrict__ flags,
-    const uint32_t* __restrict__ dur, const uint64_t* __restrict__ trace_ptr, uint64_t n_traces,
-    uint32_t S, uint32_t E, Table tab) {
+    const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+    const uint64_t* __restrict__ trace_ptr, uint64_t n_traces, uint32_t S, uint32_t E, Table tab) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wid = tid / kWave;
+  const Cols col{span_id, parent, svcfl, dur};
 
   // ---- init LDS tables
   {
-    auto* ht = reinterpret_cast<uint32_t*>(smem + kOffHt);
-    for (uint32_t s = tid; s < kHtSlots; s += kThreads) ht[s] = 0u;
+    auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
+    for (uint32_t s = tid; s < kHtSlots; s += kThreads) ht[s] = 0ull;
     if constexpr (LDS_STATS) {
       auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
       auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
@@ -208,101 +372,50 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   __syncthreads();
 
   unsigned char* wsm = smem + kOffWave + wid * kWBytes;
-  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
-  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
-  auto* ltix = reinterpret_cast<uint8_t*>(wsm + kWTix);
-  auto* lts = reinterpret_cast<uint16_t*>(wsm + kWTs);
-
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-  uint64_t t = n_traces * gw / nw;
+  const uint64_t t_begin = n_traces * gw / nw;
   const uint64_t t_end = n_traces * (gw + 1) / nw;
 
-  while (t < t_end) {
-    // Trace boundaries of up to 64 traces: lane j holds trace t + j.
-    const uint64_t ti = t + lane;
-    const bool valid = ti < t_end;
-    uint64_t lo = 0, hi = 0;
-    if (valid) {
-      lo = trace_ptr[ti];
-      hi = trace_ptr[ti + 1];
-    }
-    const uint64_t base = __shfl(lo, 0);
-    const bool fits = valid && (hi - base) <= (uint64_t)kStage;
-    const int k = __popcll(__ballot(fits));  // traces that fit: a prefix of the lanes
-    if (k == 0) {
-      big_trace<KEYBITS, LDS_STATS>(smem, wsm, lane, base, __shfl(hi, 0), span_id, parent, svc,
-                                    flags, dur, S, tab);
-      t += 1;
-      continue;
-    }
-    const uint32_t n = (uint32_t)(__shfl(hi, k - 1) - base);
-
-    // Issue every global load of the chunk before touching LDS.
-    uint64_t rs[kPer], rp[kPer];
-    uint32_t rd[kPer], rv[kPer], rf[kPer];
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const uint32_t i = lane + r * kWave;
-      rs[r] = rp[r] = 0;
-      rd[r] = rv[r] = rf[r] = 0;
-      if (i < n) {
-        rs[r] = span_id[base + i];
-        rp[r] = parent[base + i];
-        rv[r] = svc[base + i];
-        rf[r] = flags[base + i];
-        rd[r] = dur[base + i];
+  if (t_begin < t_end) {
+    // Pipeline: the bounds of chunk c+2 and the span columns of chunk c+1 are
+    // in flight while chunk c is resolved and recorded.
+    uint64_t lo, hi;
+    load_bounds(trace_ptr, t_begin, t_end, lane, lo, hi);
+    Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi);
+    Regs R;
+    load_regs(col, cur, lane, R);
+    uint64_t t_next = t_begin + (cur.k ? cur.k : 1u);
+    load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
+    while (true) {
+      const bool has_next = t_next < t_end;
+      Chunk nxt{};
+      Regs Rn;
+      if (has_next) {
+        nxt = make_chunk(t_next, t_end, lane, lo, hi);
+        load_regs(col, nxt, lane, Rn);
+        t_next += nxt.k ? nxt.k : 1u;
+        load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
       }
-    }
-    // Local trace table: starts, and a per-span trace index.
-    if (lane < k) {
-      const uint32_t a = (uint32_t)(lo - base), b = (uint32_t)(hi - base);
-      lts[lane] = (uint16_t)a;
-      if (lane == k - 1) lts[k] = (uint16_t)b;
-      for (uint32_t i = a; i < b; ++i) ltix[i] = (uint8_t)lane;
-    }
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const uint32_t i = lane + r * kWave;
-      if (i < n) {
-        lsid[i] = rs[r];
-        lsvc[i] = (uint16_t)rv[r];
+      if (cur.k == 0) {
+        big_trace<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur.base, cur.base + cur.n, col, S, tab);
+      } else {
+        process_chunk<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur, R, col, S, tab);
       }
+      if (!has_next) break;
+      cur = nxt;
+      R = Rn;
     }
-    wave_sync();
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      const uint32_t i = lane + r * kWave;
-      if (i < n) {
-        const uint32_t j = ltix[i];
-        const uint32_t a = lts[j], b = lts[j + 1];
-        const uint64_t pid = rp[r];
-        uint32_t p = S;  // ROOT: no parent reference
-        if (pid != 0ull) {
-          p = S + 1u;  // ORPHAN unless found in the trace
-          for (uint32_t q = a; q < b; ++q) {
-            if (lsid[q] == pid) {
-              p = lsvc[q];
-              break;
-            }
-          }
-        }
-        record<KEYBITS, LDS_STATS>(smem, p * S + rv[r], rd[r], rf[r], tab);
-      }
-    }
-    wave_sync();
-    t += (uint64_t)k;
   }
   __syncthreads();
 
   // ---- flush the workgroup's private tables (integer atomics, order-free)
-  if constexpr (KEYBITS != 0) {
-    constexpr uint32_t kKeyMask = (1u << KEYBITS) - 1u;
-    auto* ht = reinterpret_cast<uint32_t*>(smem + kOffHt);
+  if constexpr (LDS_HIST) {
+    auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
     for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
-      const uint32_t v = ht[s];
-      const uint32_t cnt = v >> KEYBITS;
-      if (cnt) atomicAdd(&tab.hist[(v & kKeyMask) - 1u], (unsigned long long)cnt);
+      const unsigned long long v = ht[s];
+      const uint32_t cnt = (uint32_t)(v >> 32);
+      if (cnt) atomicAdd(&tab.hist[(uint32_t)v - 1u], (unsigned long long)cnt);
     }
   }
   if constexpr (LDS_STATS) {
@@ -376,26 +489,23 @@ __global__ __launch_bounds__(kWave) void edge_finalize_kernel(Table tab,
   if (r99 >= excl && r99 < incl) p99[e] = quantile_from(r99, excl, incl, v, lane);
 }
 
-using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint16_t*, const uint16_t*,
-                          const uint32_t*, const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
+using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                          const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
 
-KernelFn pick_kernel(uint32_t E, int* keybits) {
+KernelFn pick_kernel(uint32_t E, const char** name) {
   const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
+  const bool lds_hist = keys < (1ull << 32);
   const bool lds_stats = E <= kLdsEdges;
-  if (keys < (1ull << 18) && lds_stats) {
-    *keybits = 18;
-    return edge_agg_kernel<18, true>;
+  if (lds_hist && lds_stats) {
+    *name = "edge_agg_kernel<lds_hist,lds_stats>";
+    return edge_agg_kernel<true, true>;
   }
-  if (keys < (1ull << 20)) {
-    *keybits = 20;
-    return lds_stats ? edge_agg_kernel<20, true> : edge_agg_kernel<20, false>;
+  if (lds_hist) {
+    *name = "edge_agg_kernel<lds_hist,hbm_stats>";
+    return edge_agg_kernel<true, false>;
   }
-  if (keys < (1ull << 22)) {
-    *keybits = 22;
-    return edge_agg_kernel<22, false>;
-  }
-  *keybits = 0;
-  return edge_agg_kernel<0, false>;
+  *name = "edge_agg_kernel<hbm_hist,hbm_stats>";
+  return edge_agg_kernel<false, false>;
 }
 
 // Device table layout inside ctx->d_table.
@@ -454,16 +564,16 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
-    int keybits = 0;
-    KernelFn fn = pick_kernel(E, &keybits);
+    const char* kname = nullptr;
+    KernelFn fn = pick_kernel(E, &kname);
     // One workgroup per CU; more only to keep a workgroup's u32 LDS counters
     // (errors, min, max) far from 2^32 spans.
     uint64_t grid = (uint64_t)ctx->num_cus;
     const uint64_t per_wg_cap = 1ull << 30;
     if (spans->n_spans / grid > per_wg_cap) grid = (spans->n_spans + per_wg_cap - 1) / per_wg_cap;
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
-                       spans->parent_span_id, spans->svc, spans->flags, spans->dur_us,
-                       spans->trace_ptr, spans->n_traces, S, E, tab);
+                       spans->parent_span_id, spans->svc_flags, spans->dur_us, spans->trace_ptr,
+                       spans->n_traces, S, E, tab);
     ANOMOD_HIP(ctx, hipGetLastError());
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;

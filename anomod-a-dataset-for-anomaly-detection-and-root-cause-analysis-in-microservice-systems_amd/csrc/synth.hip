@@ -332,8 +332,8 @@ __global__ void synth_sizes_kernel(TopoView tp, SynthParams sp, uint64_t shard, 
 
 __global__ void synth_fill_kernel(TopoView tp, SynthParams sp, uint64_t shard, uint64_t n_traces,
                                   const uint64_t* __restrict__ trace_ptr, uint64_t* trace_hash,
-                                  uint64_t* span_id, uint64_t* parent, uint16_t* svc,
-                                  uint16_t* flags, uint32_t* dur) {
+                                  uint64_t* span_id, uint64_t* parent, uint32_t* svc_flags,
+                                  uint32_t* dur) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_traces;
        t += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h;
@@ -345,8 +345,7 @@ __global__ void synth_fill_kernel(TopoView tp, SynthParams sp, uint64_t shard, u
       trace_hash[base + j] = h;
       span_id[base + j] = s.span_id;
       parent[base + j] = s.parent_span_id;
-      svc[base + j] = s.svc;
-      flags[base + j] = s.flags;
+      svc_flags[base + j] = (uint32_t)s.svc | ((uint32_t)s.flags << 16);
       dur[base + j] = s.dur_us;
     }
   }
@@ -355,8 +354,8 @@ __global__ void synth_fill_kernel(TopoView tp, SynthParams sp, uint64_t shard, u
 void free_spans(anomod_spans* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
-  void* ptrs[] = {s->trace_hash, s->span_id, s->parent_span_id, s->svc,
-                  s->flags,      s->dur_us,  s->trace_ptr};
+  void* ptrs[] = {s->trace_hash, s->span_id, s->parent_span_id, s->svc_flags, s->dur_us,
+                  s->trace_ptr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete s;
@@ -374,8 +373,7 @@ int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_
   if (ok && with_hash) ok = hipMalloc(&s->trace_hash, ns * 8) == hipSuccess;
   ok = ok && hipMalloc(&s->span_id, ns * 8) == hipSuccess;
   ok = ok && hipMalloc(&s->parent_span_id, ns * 8) == hipSuccess;
-  ok = ok && hipMalloc(&s->svc, ns * 2) == hipSuccess;
-  ok = ok && hipMalloc(&s->flags, ns * 2) == hipSuccess;
+  ok = ok && hipMalloc(&s->svc_flags, ns * 4) == hipSuccess;
   ok = ok && hipMalloc(&s->dur_us, ns * 4) == hipSuccess;
   if (!ok) {
     free_spans(s);
@@ -551,7 +549,7 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
     s->trace_ptr = tptr;
     hipLaunchKernelGGL(synth_fill_kernel, dim3(blocks), dim3(threads), 0, ctx->stream, tp, sp,
                        shard, n_traces, s->trace_ptr, s->trace_hash, s->span_id,
-                       s->parent_span_id, s->svc, s->flags, s->dur_us);
+                       s->parent_span_id, s->svc_flags, s->dur_us);
     hipError_t e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) {
@@ -609,8 +607,10 @@ int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_
   if (soa->trace_hash) cp(s->trace_hash, soa->trace_hash, n_spans * 8);
   cp(s->span_id, soa->span_id, n_spans * 8);
   cp(s->parent_span_id, soa->parent_span_id, n_spans * 8);
-  cp(s->svc, soa->svc, n_spans * 2);
-  cp(s->flags, soa->flags, n_spans * 2);
+  std::vector<uint32_t> packed(n_spans);
+  for (uint64_t i = 0; i < n_spans; ++i)
+    packed[i] = (uint32_t)soa->svc[i] | ((uint32_t)soa->flags[i] << 16);
+  cp(s->svc_flags, packed.data(), n_spans * 4);
   cp(s->dur_us, soa->dur_us, n_spans * 4);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
@@ -645,11 +645,15 @@ int anomod_spans_download(anomod_ctx* ctx, const anomod_spans* s, const anomod_s
   cp(dst->trace_hash, s->trace_hash, n * 8);
   cp(dst->span_id, s->span_id, n * 8);
   cp(dst->parent_span_id, s->parent_span_id, n * 8);
-  cp(dst->svc, s->svc, n * 2);
-  cp(dst->flags, s->flags, n * 2);
+  std::vector<uint32_t> packed((dst->svc || dst->flags) ? n : 0);
+  if (!packed.empty()) cp(packed.data(), s->svc_flags, n * 4);
   cp(dst->dur_us, s->dur_us, n * 4);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   ANOMOD_HIP(ctx, e);
+  for (uint64_t i = 0; i < packed.size(); ++i) {
+    if (dst->svc) dst->svc[i] = (uint16_t)(packed[i] & 0xFFFFu);
+    if (dst->flags) dst->flags[i] = (uint16_t)(packed[i] >> 16);
+  }
   return ANOMOD_OK;
 }
 
