@@ -37,13 +37,19 @@ namespace anomod {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerWG = 16;
+#ifndef ANOMOD_WAVES
+#define ANOMOD_WAVES 16
+#endif
+constexpr int kWavesPerWG = ANOMOD_WAVES;
 constexpr int kThreads = kWave * kWavesPerWG;
 constexpr int kStage = 256;  // spans staged per wave chunk
 constexpr int kPer = kStage / kWave;
 constexpr int kHtLog2 = 13;
 constexpr uint32_t kHtSlots = 1u << kHtLog2;
-constexpr int kMaxProbe = 48;
+#ifndef ANOMOD_MAXPROBE
+#define ANOMOD_MAXPROBE 48
+#endif
+constexpr int kMaxProbe = ANOMOD_MAXPROBE;
 constexpr uint32_t kLdsEdges = 512;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
@@ -92,6 +98,14 @@ __device__ __forceinline__ void wave_sync() {
 // hash table.  Slot = (count << 32) | (kidx + 1); 0 = empty.  A resident key
 // costs one LDS read + one fire-and-forget ds_add_u64; a workgroup sees
 // < 2^32 spans so the count half never carries into the key half.
+#ifndef ANOMOD_PROBE
+#define ANOMOD_PROBE 0
+#endif
+
+// Histogram increment of key kidx = edge*kBins + bin in the workgroup's LDS
+// hash table.  Slot = (count << 32) | (kidx + 1); 0 = empty.  A resident key
+// costs one LDS read + one fire-and-forget ds_add_u64 (new keys: ds_cmpst);
+// a workgroup sees < 2^32 spans so the count half never carries into the key.
 template <bool LDS_HIST>
 __device__ __forceinline__ void ht_add(unsigned long long* ht, uint32_t kidx,
                                        unsigned long long* __restrict__ ghist) {
@@ -100,12 +114,22 @@ __device__ __forceinline__ void ht_add(unsigned long long* ht, uint32_t kidx,
   } else {
     const uint32_t key = kidx + 1u;
     uint32_t h = (key * 0x9E3779B1u) >> (32 - kHtLog2);
+#if ANOMOD_PROBE == 1
+    {
+      const unsigned long long cur0 = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((uint32_t)cur0 == key) {
+        atomicAdd(&ht[h], 1ull << 32);
+        return;
+      }
+    }
+#pragma unroll 1
+#endif
     for (int probe = 0; probe < kMaxProbe; ++probe) {
       unsigned long long cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
       if (cur == 0ull) {
-        const unsigned long long ins = (1ull << 32) | key;
-        const unsigned long long prev = atomicCAS(&ht[h], 0ull, ins);
+        const unsigned long long prev = atomicCAS(&ht[h], 0ull, (1ull << 32) | key);
         if (prev == 0ull) return;
         cur = prev;
       }
@@ -276,6 +300,7 @@ __device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, 
   if (b > n) b = n;
 }
 
+#if defined(ANOMOD_SCAN4)
 // First span of [a, b) whose id equals pid (4 ids per step via ds_read_b128).
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
@@ -291,6 +316,28 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   }
   return -1;
 }
+#else
+// First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read_b128
+// from a 16-B aligned start), matches folded into a bit mask.
+__device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
+                                           uint64_t pid) {
+  for (uint32_t q0 = a & ~3u; q0 < b; q0 += 8) {
+    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
+    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
+    const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 4);
+    const ulonglong2 v3 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 6);
+    uint32_t m = (v0.x == pid ? 1u : 0u) | (v0.y == pid ? 2u : 0u) | (v1.x == pid ? 4u : 0u) |
+                 (v1.y == pid ? 8u : 0u) | (v2.x == pid ? 16u : 0u) | (v2.y == pid ? 32u : 0u) |
+                 (v3.x == pid ? 64u : 0u) | (v3.y == pid ? 128u : 0u);
+    const uint32_t lo = a > q0 ? a - q0 : 0u;             // < 4
+    const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;    // >= 1
+    m &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    if (m) return (int)(q0 + __ffs(m) - 1u);
+  }
+  return -1;
+}
+
+#endif
 
 template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,

@@ -8,7 +8,7 @@
 // series per lane.  The state (m, v in f64, sample count) lives in HBM
 // between calls so an arbitrarily long T is streamed in chunks (400 GB at
 // 10^6 x 10^5 does not fit 288 GB of HBM).  HBM-bound: 4 B/sample read +
-// 4/W B/sample written.  Loads are double-buffered 16 steps deep per lane to
+// 4/W B/sample written.  Loads are double-buffered 32 steps deep per lane to
 // keep enough bytes in flight with only S/64 waves on the chip.
 #include <cmath>
 
@@ -29,7 +29,10 @@ struct anomod_series {
 namespace anomod {
 namespace {
 
-constexpr int kU = 16;  // time steps per load block
+#ifndef ANOMOD_EWMA_U
+#define ANOMOD_EWMA_U 32
+#endif
+constexpr int kU = ANOMOD_EWMA_U;  // time steps per load block (x2 buffers in flight)
 
 struct EwmaState {
   double m, v;
@@ -53,7 +56,7 @@ __device__ __forceinline__ float ewma_step(EwmaState& st, float x, double alpha,
   return z;
 }
 
-__global__ __launch_bounds__(256) void ewma_z_kernel(const float* __restrict__ X, uint64_t T,
+__global__ __launch_bounds__(64) void ewma_z_kernel(const float* __restrict__ X, uint64_t T,
                                                      uint64_t S, double alpha, uint32_t W,
                                                      float eps, float* __restrict__ Z,
                                                      double* __restrict__ gm,
@@ -221,8 +224,9 @@ int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint3
     ser->z_cap = zbytes;
   }
   if (int rc = stage_begin(ctx, kStageEwma)) return rc;
-  const unsigned blocks = (unsigned)((ser->S + 255) / 256);
-  hipLaunchKernelGGL(ewma_z_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ser->X, ser->T,
+  // One wave per block so the S/64 waves spread evenly over the CUs.
+  const unsigned blocks = (unsigned)((ser->S + 63) / 64);
+  hipLaunchKernelGGL(ewma_z_kernel, dim3(blocks), dim3(64), 0, ctx->stream, ser->X, ser->T,
                      ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);
   ANOMOD_HIP(ctx, hipGetLastError());
   if (int rc = stage_end(ctx, kStageEwma)) return rc;

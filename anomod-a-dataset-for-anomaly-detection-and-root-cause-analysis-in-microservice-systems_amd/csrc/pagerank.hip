@@ -4,12 +4,13 @@
 // redistributed along the personalization vector, L1 stopping rule N*tol.
 //
 // GPU form: pull SpMV over the in-edge CSR (transpose of the caller ->
-// callee graph, weights pre-divided by the caller's out-weight), eight lanes
-// per row with a shuffle reduction.  One launch per iteration; the launch
-// also emits per-block partial sums of the new vector's dangling mass (read
-// by the next launch's prologue) and of |x_new - x_old| (the stopping test),
-// so an iteration needs no extra reduction kernel.  The fixed-iteration loop
-// is captured once into a hipGraph and replayed.
+// callee graph, weights pre-divided by the caller's out-weight), one lane per
+// row with the row's in-edge loads batched 8 at a time (no grid-stride
+// passes; every row in flight in one round).  One launch per iteration: each block adds its share of the new
+// vector's dangling mass and of |x_new - x_old| (the stopping test) to 64-bit
+// fixed-point accumulators with integer atomics (order-free, so the result is
+// bit-reproducible), and the next launch reads one scalar.  The
+// fixed-iteration loop is captured once into a hipGraph and replayed.
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -27,9 +28,13 @@ struct anomod_graph {
   float* in_w = nullptr;       // [nnz] w / outweight(src)
   uint8_t* dangling = nullptr; // [N]
   double* p = nullptr;         // [N]
+  uint32_t n_dangling = 0;
   double* x[2] = {nullptr, nullptr};
-  double* dpart[2] = {nullptr, nullptr};  // [grid] dangling-mass partials
-  double* epart = nullptr;     // [grid] L1-change partials
+  // Fixed-point accumulators, kAccSlots-way spread, triple-buffered by
+  // iteration (k reads buffer k%3, adds into (k+1)%3, zeroes (k+2)%3):
+  // buffers 0..2 dangling mass (2^-62 units), 3..5 L1 change (2^-61 units).
+  unsigned long long* acc = nullptr;
+  std::vector<unsigned long long> host_acc;
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
   uint32_t exec_iters = 0;
@@ -40,8 +45,13 @@ namespace anomod {
 namespace {
 
 constexpr int kPprThreads = 256;
-constexpr int kRowLanes = 8;
+constexpr int kRowsPerBlock = kPprThreads;  // one row per lane
+constexpr int kEdgeBatch = 8;              // in-edge loads issued together per lane
+constexpr double kDScale = 4611686018427387904.0;  // 2^62: dangling mass <= 1
+constexpr double kEScale = 2305843009213693952.0;  // 2^61: L1 change <= 2
+constexpr int kAccSlots = 64;  // atomics spread over 64 words: no single-address queue
 
+// Block-wide sum, fixed reduction tree (deterministic); result valid in thread 0.
 __device__ __forceinline__ double block_sum(double v, double* red) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -55,61 +65,71 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 __global__ __launch_bounds__(kPprThreads) void ppr_init_kernel(uint32_t N, double x0,
-                                                               const uint8_t* __restrict__ dangling,
-                                                               double* __restrict__ x,
-                                                               double* __restrict__ dpart) {
-  __shared__ double red[kPprThreads / 64];
-  double acc = 0.0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+                                                               double* __restrict__ x) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
     x[i] = x0;
-    if (dangling[i]) acc += x0;
-  }
-  const double s = block_sum(acc, red);
-  if (threadIdx.x == 0) dpart[blockIdx.x] = s;
 }
 
+// One power iteration x_in -> x_out.  Eight lanes per row pull the in-edges.
+// The block's share of the new vector's dangling mass and of |x_out - x_in|
+// is rounded to 64-bit fixed point and added with one integer atomic each:
+// integer adds commute, so the next launch reads a bit-reproducible scalar
+// without a reduction kernel or an inter-block hand-off.
 __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
     const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
     const double* __restrict__ p, double alpha, const double* __restrict__ x_in,
-    double* __restrict__ x_out, const double* __restrict__ dpart_in, double* __restrict__ dpart_out,
-    double* __restrict__ epart) {
+    double* __restrict__ x_out, const unsigned long long* __restrict__ d_in,
+    unsigned long long* d_out, unsigned long long* d_zero, unsigned long long* e_out,
+    unsigned long long* e_zero) {
   __shared__ double red[kPprThreads / 64];
   __shared__ double s_dsum;
-  // Prologue: dangling mass of x_in from the previous launch's partials.
-  {
-    double a = 0.0;
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) a += dpart_in[i];
-    const double s = block_sum(a, red);
-    if (threadIdx.x == 0) s_dsum = s;
-    __syncthreads();
-  }
-  const double dsum = s_dsum;
-  const int sub = threadIdx.x & (kRowLanes - 1);
-  const uint32_t rows_per_pass = gridDim.x * (blockDim.x / kRowLanes);
-  double dacc = 0.0, eacc = 0.0;
-  for (uint32_t r0 = blockIdx.x * (blockDim.x / kRowLanes); r0 < N; r0 += rows_per_pass) {
-    const uint32_t r = r0 + threadIdx.x / kRowLanes;
-    double acc = 0.0;
-    if (r < N) {
-      const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
-      for (uint32_t k = b + sub; k < e; k += kRowLanes) acc += x_in[in_col[k]] * (double)in_w[k];
-    }
+  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  double acc = 0.0;
+  if (r < N) {
+    const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
+    // In-degrees are short (uniform callees): one lane per row, kEdgeBatch
+    // (col, w) pairs loaded together, then the x gathers together.
+    for (uint32_t k0 = b; k0 < e; k0 += kEdgeBatch) {
+      uint32_t c[kEdgeBatch];
+      float wv[kEdgeBatch];
 #pragma unroll
-    for (int off = kRowLanes / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kRowLanes);
-    if (r < N && sub == 0) {
-      const double pr = p[r];
-      const double y = alpha * (acc + dsum * pr) + (1.0 - alpha) * pr;
-      x_out[r] = y;
-      if (dangling[r]) dacc += y;
-      eacc += fabs(y - x_in[r]);
+      for (int j = 0; j < kEdgeBatch; ++j) {
+        const bool ok = k0 + j < e;
+        c[j] = ok ? in_col[k0 + j] : 0u;
+        wv[j] = ok ? in_w[k0 + j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kEdgeBatch; ++j)
+        if (k0 + j < e) acc += x_in[c[j]] * (double)wv[j];
     }
+  }
+  // Dangling mass of x_in: wave 0 folds the fixed-point slots (exact).
+  if (threadIdx.x < 64) {
+    unsigned long long v = d_in[threadIdx.x];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (threadIdx.x == 0) s_dsum = (double)v * (1.0 / kDScale);
+  }
+  __syncthreads();
+  const double dsum = s_dsum;
+  double dacc = 0.0, eacc = 0.0;
+  if (r < N) {
+    const double pr = p[r];
+    const double y = alpha * (acc + dsum * pr) + (1.0 - alpha) * pr;
+    x_out[r] = y;
+    if (dangling[r]) dacc = y;
+    eacc = fabs(y - x_in[r]);
   }
   const double ds = block_sum(dacc, red);
   const double es = block_sum(eacc, red);
   if (threadIdx.x == 0) {
-    dpart_out[blockIdx.x] = ds;
-    epart[blockIdx.x] = es;
+    const int slot = blockIdx.x & (kAccSlots - 1);
+    atomicAdd(&d_out[slot], __double2ull_rn(ds * kDScale));
+    atomicAdd(&e_out[slot], __double2ull_rn(es * kEScale));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < kAccSlots) {
+    d_zero[threadIdx.x] = 0ull;
+    e_zero[threadIdx.x] = 0ull;
   }
 }
 
@@ -117,8 +137,7 @@ void free_graph(anomod_graph* g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,
-                g->x[0],   g->x[1],   g->dpart[0], g->dpart[1], g->epart};
+  void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, g->x[0], g->x[1], g->acc};
   for (void* q : ps)
     if (q) (void)hipFree(q);
   delete g;
@@ -127,9 +146,12 @@ void free_graph(anomod_graph* g) {
 // Launch iteration `it` (x[it&1] -> x[(it+1)&1]).
 void launch_iter(anomod_ctx* ctx, anomod_graph* g, double alpha, uint32_t it) {
   const int a = it & 1, b = a ^ 1;
+  const int r = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
+  unsigned long long* A = g->acc;
+  const int S = kAccSlots;
   hipLaunchKernelGGL(ppr_iter_kernel, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream, g->N,
                      g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, g->x[a], g->x[b],
-                     g->dpart[a], g->dpart[b], g->epart);
+                     A + r * S, A + w * S, A + z * S, A + (3 + w) * S, A + (3 + z) * S);
 }
 
 }  // namespace
@@ -176,19 +198,16 @@ int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t
   g->device = ctx->device;
   g->N = N;
   g->nnz = nnz;
-  g->grid = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>((N + kPprThreads / kRowLanes - 1) / (kPprThreads / kRowLanes),
-                            (uint64_t)ctx->num_cus * 4));
+  g->grid = (N + kRowsPerBlock - 1) / kRowsPerBlock;
+  for (uint32_t u = 0; u < N; ++u) g->n_dangling += dang[u];
   bool ok = hipMalloc(&g->in_ptr, (N + 1) * 4ull) == hipSuccess;
   ok = ok && hipMalloc(&g->in_col, in_col.size() * 4) == hipSuccess;
   ok = ok && hipMalloc(&g->in_w, in_w.size() * 4) == hipSuccess;
   ok = ok && hipMalloc(&g->dangling, N) == hipSuccess;
   ok = ok && hipMalloc(&g->p, N * 8ull) == hipSuccess;
-  for (int i = 0; i < 2; ++i) {
-    ok = ok && hipMalloc(&g->x[i], N * 8ull) == hipSuccess;
-    ok = ok && hipMalloc(&g->dpart[i], g->grid * 8ull) == hipSuccess;
-  }
-  ok = ok && hipMalloc(&g->epart, g->grid * 8ull) == hipSuccess;
+  for (int i = 0; i < 2; ++i) ok = ok && hipMalloc(&g->x[i], N * 8ull) == hipSuccess;
+  ok = ok && hipMalloc(&g->acc, 6 * kAccSlots * 8) == hipSuccess;
+  g->host_acc.assign(6 * kAccSlots, 0ull);
   if (!ok) {
     free_graph(g);
     set_error(ctx, "hipMalloc failed for a graph of %u nodes / %llu edges", N,
@@ -265,25 +284,31 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   for (double& v : pn) v /= psum;
   if (int rc = bind(ctx)) return rc;
   ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, pn.data(), N * 8ull, hipMemcpyHostToDevice, ctx->stream));
-  const dim3 grid(g->grid), block(kPprThreads);
-  hipLaunchKernelGGL(ppr_init_kernel, grid, block, 0, ctx->stream, N, 1.0 / N, g->dangling,
-                     g->x[0], g->dpart[0]);
+  // x0 = 1/N; its dangling mass n_dangling/N seeds iteration 0 (slot 0); the
+  // slots iteration 0 adds into must start at zero.
+  for (unsigned long long& v : g->host_acc) v = 0ull;
+  g->host_acc[0] = (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->acc, g->host_acc.data(), g->host_acc.size() * 8,
+                                 hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(ppr_init_kernel, dim3(std::min<uint32_t>(g->grid, 1024)), dim3(kPprThreads),
+                     0, ctx->stream, N, 1.0 / N, g->x[0]);
   ANOMOD_HIP(ctx, hipGetLastError());
   uint32_t done = 0;
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
   if (tol > 0.0) {
     // Convergence mode: host reads the L1 change after every iteration.
-    std::vector<double> ep(g->grid);
     for (uint32_t it = 0; it < iters; ++it) {
       launch_iter(ctx, g, alpha, it);
       ANOMOD_HIP(ctx, hipGetLastError());
-      ANOMOD_HIP(ctx, hipMemcpyAsync(ep.data(), g->epart, g->grid * 8ull, hipMemcpyDeviceToHost,
-                                     ctx->stream));
+      const int w = (it + 1) % 3;
+      unsigned long long* eh = g->host_acc.data() + (3 + w) * kAccSlots;
+      ANOMOD_HIP(ctx, hipMemcpyAsync(eh, g->acc + (3 + w) * kAccSlots, kAccSlots * 8,
+                                     hipMemcpyDeviceToHost, ctx->stream));
       ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
       done = it + 1;
-      double err = 0.0;
-      for (double v : ep) err += v;
-      if (err < (double)N * tol) break;
+      unsigned long long et = 0;
+      for (int i = 0; i < kAccSlots; ++i) et += eh[i];
+      if ((double)et * (1.0 / kEScale) < (double)N * tol) break;
     }
   } else {
     // Fixed-iteration mode: replay a captured graph of `iters` launches.

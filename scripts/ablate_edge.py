@@ -40,12 +40,14 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--one":
         one(traces, 7)
         return
-    libs = [None] + sorted(str(p) for p in (PKG / "csrc/build/variants").glob("libanomod_abl*.so"))
+    libs = [None] + sorted(str(p) for p in (PKG / "csrc/build/variants").glob("libanomod_*.so"))
+    print("libs:", [Path(l).name if l else "main" for l in libs], flush=True)
     for lib in libs:
         env = dict(os.environ)
         if lib:
             env["ANOMOD_LIB"] = lib
         r = subprocess.run([sys.executable, __file__, "--one"], env=env, timeout=300)
+        print(f"rc={r.returncode} lib={Path(lib).name if lib else 'main'}", flush=True)
         if r.returncode != 0:
             sys.exit(r.returncode)
 
