@@ -190,7 +190,7 @@ def main() -> int:
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-            "kernel": "edge_agg_kernel<18,true>", "kernel_ms": k_ms,
+            "kernel": "edge_agg_kernel<lds_hist,lds_stats>", "kernel_ms": k_ms,
             "bytes_per_launch": bytes_launch,
         },
     }
