@@ -16,15 +16,21 @@
 //
 // Design (MI355X):
 //  * one pass over the span SoA in HBM: 8 B span_id + 8 B parent_span_id +
-//    2 B svc + 2 B flags + 4 B dur_us per span + 8 B trace_ptr per trace;
+//    4 B svc|flags + 4 B dur_us per span + 8 B trace_ptr per trace, read
+//    with buffer loads (one scalar descriptor per column and chunk, 32-bit
+//    lane offsets, out-of-chunk lanes read 0 — no per-lane address math);
 //  * persistent grid, one 1024-thread workgroup per CU; every wave owns a
-//    contiguous range of traces and walks it in chunks of <= 256 spans, so
-//    parent resolution is trace-local in that wave's LDS staging area (no
-//    inter-wave synchronisation inside the loop);
+//    contiguous range of traces and walks it in chunks of <= 256 spans /
+//    <= 64 traces, so parent resolution is trace-local in that wave's LDS
+//    staging area (no inter-wave synchronisation inside the loop);
+//  * parent lookup: ordered scan of the trace's staged ids (first match, the
+//    reference rule), 8 ids per 4 x ds_read_b128 step (a per-wave LDS hash
+//    with ds_cmpst inserts measured 1.7x slower, and scanning a lane's 4
+//    slots in lockstep 1.1-1.4x slower: register pressure);
 //  * the E x 896 histogram does not fit LDS, so each workgroup privatises it
-//    in a 16 Ki-slot LDS hash table of packed (key | count) words; a count
-//    field that wraps flushes 2^cntbits to HBM with a u64 atomic, slots are
-//    flushed once at the end;
+//    in an 8 Ki-slot LDS hash table of packed (count << 32 | key) words
+//    (first probes of a lane's 4 spans issued together), flushed once with
+//    u64 atomics;
 //  * per-edge error/sum/min/max live in LDS (E <= 512) and are flushed once;
 //  * all merges are integer adds / min / max: results are bit-exact and
 //    independent of geometry, scheduling and shard count.
@@ -46,16 +52,16 @@ constexpr int kStage = 256;  // spans staged per wave chunk
 constexpr int kPer = kStage / kWave;
 constexpr int kHtLog2 = 13;
 constexpr uint32_t kHtSlots = 1u << kHtLog2;
-#ifndef ANOMOD_MAXPROBE
-#define ANOMOD_MAXPROBE 48
-#endif
-constexpr int kMaxProbe = ANOMOD_MAXPROBE;
+constexpr int kMaxProbe = 48;
 constexpr uint32_t kLdsEdges = 512;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
-// 2 = no histogram, 4 = no parent scan.
+// 2 = no histogram, 4 = no parent lookup.
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
+#endif
+#ifndef ANOMOD_HB
+#define ANOMOD_HB 0  // 1 = batch the first histogram probes of a lane's 4 spans
 #endif
 
 // LDS carve (bytes, every offset a multiple of 16).
@@ -65,7 +71,7 @@ constexpr int kOffErr = kOffSum + (int)kLdsEdges * 8;
 constexpr int kOffMin = kOffErr + (int)kLdsEdges * 4;
 constexpr int kOffMax = kOffMin + (int)kLdsEdges * 4;
 constexpr int kOffWave = kOffMax + (int)kLdsEdges * 4;
-constexpr int kWSid = 0;                        // u64 span ids [kStage + 8]
+constexpr int kWSid = 0;                         // u64 span ids [kStage + 8]
 constexpr int kWSvc = kWSid + (kStage + 8) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2; // u8 trace-start flags [kStage]
 constexpr int kWBytes = kWFlag + kStage;
@@ -94,61 +100,57 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Histogram increment of key kidx = edge*kBins + bin in the workgroup's LDS
-// hash table.  Slot = (count << 32) | (kidx + 1); 0 = empty.  A resident key
-// costs one LDS read + one fire-and-forget ds_add_u64; a workgroup sees
-// < 2^32 spans so the count half never carries into the key half.
-#ifndef ANOMOD_PROBE
-#define ANOMOD_PROBE 0
-#endif
-
-// Histogram increment of key kidx = edge*kBins + bin in the workgroup's LDS
-// hash table.  Slot = (count << 32) | (kidx + 1); 0 = empty.  A resident key
-// costs one LDS read + one fire-and-forget ds_add_u64 (new keys: ds_cmpst);
-// a workgroup sees < 2^32 spans so the count half never carries into the key.
-template <bool LDS_HIST>
-__device__ __forceinline__ void ht_add(unsigned long long* ht, uint32_t kidx,
-                                       unsigned long long* __restrict__ ghist) {
-  if constexpr (!LDS_HIST) {
-    atomicAdd(&ghist[kidx], 1ull);
-  } else {
-    const uint32_t key = kidx + 1u;
-    uint32_t h = (key * 0x9E3779B1u) >> (32 - kHtLog2);
-#if ANOMOD_PROBE == 1
-    {
-      const unsigned long long cur0 = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-      if ((uint32_t)cur0 == key) {
-        atomicAdd(&ht[h], 1ull << 32);
-        return;
-      }
-    }
-#pragma unroll 1
-#endif
-    for (int probe = 0; probe < kMaxProbe; ++probe) {
-      unsigned long long cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (cur == 0ull) {
-        const unsigned long long prev = atomicCAS(&ht[h], 0ull, (1ull << 32) | key);
-        if (prev == 0ull) return;
-        cur = prev;
-      }
-      if ((uint32_t)cur == key) {
-        atomicAdd(&ht[h], 1ull << 32);
-        return;
-      }
-      h = (h + 1u) & (kHtSlots - 1u);
-    }
-    atomicAdd(&ghist[kidx], 1ull);  // table saturated: count in HBM directly
-  }
+// Make a wave-uniform 64-bit value provably uniform (SGPR) for the compiler.
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-template <bool LDS_HIST, bool LDS_STATS>
-__device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
-                                       const Table& tab) {
-  if constexpr (!(ANOMOD_ABL & 2))
-    ht_add<LDS_HIST>(reinterpret_cast<unsigned long long*>(smem + kOffHt),
-                     edge * kBins + hist_bin(d), tab.hist);
+// Buffer descriptor over [base, base + bytes): loads past the end return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ uint64_t bload64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint64_t)__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t bload32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+
+// Histogram increment of key = edge*kBins + bin + 1 in the workgroup's LDS
+// hash table, probing from slot h.  Slot = (count << 32) | key; 0 = empty.
+// A resident key costs one LDS read + one fire-and-forget ds_add_u64 (new
+// keys: ds_cmpst); a workgroup sees < 2^32 spans so the count half never
+// carries into the key.  A saturated probe chain counts in HBM directly.
+__device__ __forceinline__ uint32_t ht_slot(uint32_t key) {
+  return (key * 0x9E3779B1u) >> (32 - kHtLog2);
+}
+
+__device__ __forceinline__ void ht_insert(unsigned long long* ht, uint32_t key, uint32_t h,
+                                          unsigned long long* __restrict__ ghist) {
+  for (int probe = 0; probe < kMaxProbe; ++probe) {
+    unsigned long long cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(&ht[h], 0ull, (1ull << 32) | key);
+      if (prev == 0ull) return;
+      cur = prev;
+    }
+    if ((uint32_t)cur == key) {
+      atomicAdd(&ht[h], 1ull << 32);
+      return;
+    }
+    h = (h + 1u) & (kHtSlots - 1u);
+  }
+  atomicAdd(&ghist[key - 1u], 1ull);
+}
+
+template <bool LDS_STATS>
+__device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uint32_t d,
+                                         uint32_t fl, const Table& tab) {
   if constexpr (ANOMOD_ABL & 1) return;
   if constexpr (LDS_STATS) {
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
@@ -165,6 +167,21 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
     atomicMax(&tab.mx[edge], d);
     if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&tab.err[edge], 1ull);
   }
+}
+
+// One span (big-trace path).
+template <bool LDS_HIST, bool LDS_STATS>
+__device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
+                                       const Table& tab) {
+  if constexpr (!(ANOMOD_ABL & 2)) {
+    const uint32_t kidx = edge * kBins + hist_bin(d);
+    if constexpr (LDS_HIST)
+      ht_insert(reinterpret_cast<unsigned long long*>(smem + kOffHt), kidx + 1u,
+                ht_slot(kidx + 1u), tab.hist);
+    else
+      atomicAdd(&tab.hist[kidx], 1ull);
+  }
+  stat_add<LDS_STATS>(smem, edge, d, fl, tab);
 }
 
 // A trace longer than kStage: wave-cooperative scan of the trace's span ids,
@@ -213,7 +230,7 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
 }
 
 // One wave's chunk: up to 64 consecutive traces holding <= kStage spans, or a
-// single trace longer than kStage (k == 0).
+// single trace longer than kStage (k == 0).  base / k / n are wave-uniform.
 struct Chunk {
   uint64_t base;   // first span
   uint32_t k;      // traces in the chunk (0 = one big trace)
@@ -232,9 +249,7 @@ __device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane
                                             uint64_t hi) {
   Chunk c;
   const bool valid = t + lane < t_end;
-  const uint64_t b = __shfl(lo, 0);
-  c.base = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  c.base = uniform64(__shfl(lo, 0));
   const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
   c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
   const uint32_t n = c.k ? (uint32_t)(__shfl(hi, (int)c.k - 1) - c.base)
@@ -244,27 +259,30 @@ __device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane
   return c;
 }
 
+// trace_ptr[t + lane] and trace_ptr[t + lane + 1] for lanes t + lane < t_end
+// (0 elsewhere).  t and t_end are wave-uniform.
 __device__ __forceinline__ void load_bounds(const uint64_t* __restrict__ trace_ptr, uint64_t t,
                                             uint64_t t_end, int lane, uint64_t& lo, uint64_t& hi) {
-  lo = hi = 0;
-  if (t + lane < t_end) {
-    lo = trace_ptr[t + lane];
-    hi = trace_ptr[t + lane + 1];
-  }
+  t = uniform64(t);
+  const uint64_t avail = t_end > t ? t_end - t : 0;
+  const uint32_t bytes = (uint32_t)(avail < (uint64_t)kWave ? avail : (uint64_t)kWave) * 8u;
+  lo = bload64(rsrc(trace_ptr + t, bytes), (uint32_t)lane * 8u);
+  hi = bload64(rsrc(trace_ptr + t + 1, bytes), (uint32_t)lane * 8u);
 }
 
 __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int lane, Regs& R) {
+  const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by big_trace()
+  const auto rsid = rsrc(col.span_id + c.base, n * 8u);
+  const auto rpid = rsrc(col.parent + c.base, n * 8u);
+  const auto rsf = rsrc(col.svcfl + c.base, n * 4u);
+  const auto rdur = rsrc(col.dur + c.base, n * 4u);
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
-    const uint32_t i = lane + r * kWave;
-    R.sid[r] = R.pid[r] = 0;
-    R.dur[r] = R.sf[r] = 0;
-    if (c.k && i < c.n) {
-      R.sid[r] = col.span_id[c.base + i];
-      R.pid[r] = col.parent[c.base + i];
-      R.sf[r] = col.svcfl[c.base + i];
-      R.dur[r] = col.dur[c.base + i];
-    }
+    const uint32_t i = (uint32_t)lane + (uint32_t)(r * kWave);
+    R.sid[r] = bload64(rsid, i * 8u);
+    R.pid[r] = bload64(rpid, i * 8u);
+    R.sf[r] = bload32(rsf, i * 4u);
+    R.dur[r] = bload32(rdur, i * 4u);
   }
 }
 
@@ -300,25 +318,59 @@ __device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, 
   if (b > n) b = n;
 }
 
-#if defined(ANOMOD_SCAN4)
-// First span of [a, b) whose id equals pid (4 ids per step via ds_read_b128).
-__device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
-                                           uint64_t pid) {
-  for (uint32_t q0 = a & ~1u; q0 < b; q0 += 4) {
-    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
-    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
-    int hit = -1;
-    if (q0 + 3 >= a && q0 + 3 < b && v1.y == pid) hit = (int)q0 + 3;
-    if (q0 + 2 >= a && q0 + 2 < b && v1.x == pid) hit = (int)q0 + 2;
-    if (q0 + 1 >= a && q0 + 1 < b && v0.y == pid) hit = (int)q0 + 1;
-    if (q0 >= a && v0.x == pid) hit = (int)q0;
-    if (hit >= 0) return hit;
+// The 4 spans of a lane: the first-probe reads of the histogram hash for all
+// four are issued together, so a resident key costs one shared LDS round
+// trip and one fire-and-forget ds_add_u64.
+template <bool LDS_HIST, bool LDS_STATS>
+__device__ __forceinline__ void record4(unsigned char* smem, int lane, uint32_t n,
+                                        const uint32_t (&edge)[kPer], const Regs& R,
+                                        const Table& tab) {
+  if constexpr (!(ANOMOD_ABL & 2)) {
+    uint32_t key[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) key[r] = edge[r] * kBins + hist_bin(R.dur[r]) + 1u;
+    if constexpr (LDS_HIST) {
+      auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
+      uint32_t h[kPer];
+      unsigned long long cur[kPer];
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        h[r] = ht_slot(key[r]);
+        cur[r] = 0ull;
+        if ((uint32_t)lane + r * kWave < n)
+          cur[r] = __hip_atomic_load(&ht[h[r]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        if ((uint32_t)lane + r * kWave < n) {
+          if ((uint32_t)cur[r] == key[r])
+            atomicAdd(&ht[h[r]], 1ull << 32);
+          else
+            ht_insert(ht, key[r], h[r], tab.hist);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kPer; ++r)
+        if ((uint32_t)lane + r * kWave < n) atomicAdd(&tab.hist[key[r] - 1u], 1ull);
+    }
   }
-  return -1;
+#pragma unroll
+  for (int r = 0; r < kPer; ++r)
+    if ((uint32_t)lane + r * kWave < n)
+      stat_add<LDS_STATS>(smem, edge[r], R.dur[r], R.sf[r] >> 16, tab);
 }
-#else
+
+// Parent scan of the 4 span slots of a lane in lockstep.  Ids are staged as
+// split 32-bit halves; every step issues the next 8 low halves (2 x
+// ds_read_b128) of every live slot before comparing, so one LDS round trip
+// serves four lookups; a low-half match is confirmed on the high half.
+// First match in trace order (the reference rule: jaeger_to_csv.py:34-38 /
+// trace_collector.py:424-443).
 // First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read_b128
-// from a 16-B aligned start), matches folded into a bit mask.
+// from a 16-B aligned start), matches folded into a bit mask.  First match in
+// trace order (the reference rule: jaeger_to_csv.py:34-38 /
+// trace_collector.py:424-443).
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
   for (uint32_t q0 = a & ~3u; q0 < b; q0 += 8) {
@@ -337,54 +389,50 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   return -1;
 }
 
-#endif
-
 template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
-                                              const Chunk& c, const Regs& R, const Cols& col,
-                                              uint32_t S, const Table& tab) {
+                                              const Chunk& c, const Regs& R, uint32_t S,
+                                              const Table& tab) {
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
   auto* lflag = reinterpret_cast<uint8_t*>(wsm + kWFlag);
-  // Stage ids / services; mark trace starts.
+  // Stage ids / services (lanes past n hold zeros from the buffer loads);
+  // mark trace starts.
   reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
-    if (i < c.n) {
-      lsid[i] = R.sid[r];
-      lsvc[i] = (uint16_t)R.sf[r];
-    }
+    lsid[i] = R.sid[r];
+    lsvc[i] = (uint16_t)R.sf[r];
   }
+  wave_sync();
   if ((uint32_t)lane < c.k && c.start < c.n) lflag[c.start] = 1;
   wave_sync();
   uint64_t Sm[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) Sm[r] = __ballot(lflag[lane + r * kWave] != 0);
-  uint32_t pidx[kPer];
+  uint32_t edge[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
-    pidx[r] = S;  // ROOT
+    uint32_t p = S;  // ROOT
     if (i < c.n && R.pid[r] != 0ull) {
-      pidx[r] = S + 1u;  // ORPHAN unless found in the trace
+      p = S + 1u;  // ORPHAN unless found in the trace
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
         trace_bounds(Sm, r, lane, c.n, a, b);
         const int q = find_parent(lsid, a, b, R.pid[r]);
-        if (q >= 0) pidx[r] = 0x80000000u | (uint32_t)q;
+        if (q >= 0) p = lsvc[q];
       }
     }
+    edge[r] = p * S + (R.sf[r] & 0xFFFFu);
+#if !ANOMOD_HB
+    if (i < c.n) record<LDS_HIST, LDS_STATS>(smem, edge[r], R.dur[r], R.sf[r] >> 16, tab);
+#endif
   }
-#pragma unroll
-  for (int r = 0; r < kPer; ++r) {
-    const uint32_t i = lane + r * kWave;
-    if (i < c.n) {
-      const uint32_t p = (pidx[r] & 0x80000000u) ? (uint32_t)lsvc[pidx[r] & 0xFFFFu] : pidx[r];
-      record<LDS_HIST, LDS_STATS>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r], R.sf[r] >> 16,
-                                  tab);
-    }
-  }
+#if ANOMOD_HB
+  record4<LDS_HIST, LDS_STATS>(smem, lane, c.n, edge, R, tab);
+#endif
   wave_sync();
 }
 
@@ -421,8 +469,8 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   unsigned char* wsm = smem + kOffWave + wid * kWBytes;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-  const uint64_t t_begin = n_traces * gw / nw;
-  const uint64_t t_end = n_traces * (gw + 1) / nw;
+  const uint64_t t_begin = uniform64(n_traces * gw / nw);
+  const uint64_t t_end = uniform64(n_traces * (gw + 1) / nw);
 
   if (t_begin < t_end) {
     // Pipeline: the bounds of chunk c+2 and the span columns of chunk c+1 are
@@ -447,7 +495,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       if (cur.k == 0) {
         big_trace<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur.base, cur.base + cur.n, col, S, tab);
       } else {
-        process_chunk<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur, R, col, S, tab);
+        process_chunk<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
