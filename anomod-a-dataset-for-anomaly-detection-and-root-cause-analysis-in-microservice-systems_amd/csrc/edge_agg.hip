@@ -56,9 +56,12 @@ constexpr int kMaxProbe = 48;
 constexpr uint32_t kLdsEdges = 512;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
-// 2 = no histogram, 4 = no parent lookup.
+// 2 = no histogram, 4 = no parent lookup, 16 = stream the columns only.
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
+#endif
+#ifndef ANOMOD_CASCADE
+#define ANOMOD_CASCADE 0  // 1 = descending-select parent scan from the trace start
 #endif
 #ifndef ANOMOD_HB
 #define ANOMOD_HB 0  // 1 = batch the first histogram probes of a lane's 4 spans
@@ -175,10 +178,17 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
                                        const Table& tab) {
   if constexpr (!(ANOMOD_ABL & 2)) {
     const uint32_t kidx = edge * kBins + hist_bin(d);
-    if constexpr (LDS_HIST)
-      ht_insert(reinterpret_cast<unsigned long long*>(smem + kOffHt), kidx + 1u,
-                ht_slot(kidx + 1u), tab.hist);
-    else
+    if constexpr (LDS_HIST) {
+      // fast path: the key is resident in its home slot -> one read and an
+      // unconditional add (0 for lanes that miss, so no branch around it)
+      auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
+      const uint32_t key = kidx + 1u, h = ht_slot(key);
+      const unsigned long long cur =
+          __hip_atomic_load(&ht[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const bool hit = (uint32_t)cur == key;
+      atomicAdd(&ht[h], hit ? (1ull << 32) : 0ull);
+      if (!hit) ht_insert(ht, key, h, tab.hist);
+    } else
       atomicAdd(&tab.hist[kidx], 1ull);
   }
   stat_add<LDS_STATS>(smem, edge, d, fl, tab);
@@ -287,33 +297,25 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
 }
 
 // Bounds [a, b) of the trace holding chunk position i = 64*r + lane, from the
-// four 64-bit trace-start masks (wave-uniform).
+// four 64-bit trace-start masks (wave-uniform); branch-free (selects only).
 __device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, int lane,
                                              uint32_t n, uint32_t& a, uint32_t& b) {
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-  uint64_t m = Sm[r] & le;
   a = 0;
-  if (m) {
-    a = 64u * r + 63u - (uint32_t)__clzll((long long)m);
-  } else {
-    for (int q = r - 1; q >= 0; --q) {
-      if (Sm[q]) {
-        a = 64u * q + 63u - (uint32_t)__clzll((long long)Sm[q]);
-        break;
-      }
-    }
-  }
-  m = Sm[r] & ~le;
   b = n;
-  if (m) {
-    b = 64u * r + (uint32_t)__ffsll((unsigned long long)m) - 1u;
-  } else {
-    for (int q = r + 1; q < kPer; ++q) {
-      if (Sm[q]) {
-        b = 64u * q + (uint32_t)__ffsll((unsigned long long)Sm[q]) - 1u;
-        break;
-      }
-    }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (q > r) break;
+    const uint64_t m = (q == r) ? (Sm[q] & le) : Sm[q];
+    const uint32_t pos = 64u * q + 63u - (uint32_t)__clzll((long long)m);
+    a = m ? pos : a;
+  }
+#pragma unroll
+  for (int q = kPer - 1; q >= 0; --q) {
+    if (q < r) break;
+    const uint64_t m = (q == r) ? (Sm[q] & ~le) : Sm[q];
+    const uint32_t pos = 64u * q + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    b = m ? pos : b;
   }
   if (b > n) b = n;
 }
@@ -367,6 +369,27 @@ __device__ __forceinline__ void record4(unsigned char* smem, int lane, uint32_t 
 // serves four lookups; a low-half match is confirmed on the high half.
 // First match in trace order (the reference rule: jaeger_to_csv.py:34-38 /
 // trace_collector.py:424-443).
+#if ANOMOD_CASCADE
+// Cascade form: 8 ids per step read from the trace start on (ds_read_b64,
+// any 8-B alignment, so no position below a is ever compared); the lowest
+// matching position of a step comes from a descending select chain.  A
+// match at or past b means no in-trace match (every in-trace position of the
+// step is lower).  First match in trace order (jaeger_to_csv.py:34-38 /
+// trace_collector.py:424-443).
+__device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
+                                           uint64_t pid) {
+  for (uint32_t q0 = a; q0 < b; q0 += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];
+    uint32_t idx = 8u;
+#pragma unroll
+    for (int j = 7; j >= 0; --j) idx = (v[j] == pid) ? (uint32_t)j : idx;
+    if (idx < 8u) return (q0 + idx < b) ? (int)(q0 + idx) : -1;
+  }
+  return -1;
+}
+#else
 // First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read_b128
 // from a 16-B aligned start), matches folded into a bit mask.  First match in
 // trace order (the reference rule: jaeger_to_csv.py:34-38 /
@@ -388,6 +411,7 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   }
   return -1;
 }
+#endif
 
 template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
@@ -396,6 +420,13 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
   auto* lflag = reinterpret_cast<uint8_t*>(wsm + kWFlag);
+  if constexpr (ANOMOD_ABL & 16) {  // stream only: keep the loads, do nothing
+    uint64_t x = 0;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) x ^= R.sid[r] ^ R.pid[r] ^ R.sf[r] ^ ((uint64_t)R.dur[r] << 7);
+    if (x == 0x0123456789ABCDEFull) tab.err[0] = x;
+    return;
+  }
   // Stage ids / services (lanes past n hold zeros from the buffer loads);
   // mark trace starts.
   reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
@@ -661,9 +692,13 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   if (spans->n_traces > 0) {
     const char* kname = nullptr;
     KernelFn fn = pick_kernel(E, &kname);
-    // One workgroup per CU; more only to keep a workgroup's u32 LDS counters
+    // As many workgroups as are resident at once (LDS / registers decide:
+    // one or two per CU); more only to keep a workgroup's u32 LDS counters
     // (errors, min, max) far from 2^32 spans.
-    uint64_t grid = (uint64_t)ctx->num_cus;
+    int per_cu = 0;
+    ANOMOD_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per_cu, reinterpret_cast<const void*>(fn), kThreads, 0));
+    uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
     const uint64_t per_wg_cap = 1ull << 30;
     if (spans->n_spans / grid > per_wg_cap) grid = (spans->n_spans + per_wg_cap - 1) / per_wg_cap;
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
