@@ -19,7 +19,7 @@ from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec,
                      synth_generate_host, synth_services)
 from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
                      load_experiment, rank)
-from .spans import EdgeTable, SpanSet, edge_rows
+from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
 
 __all__ = [
     "AnomodError", "Context", "DeviceGraph", "DeviceSeries", "DeviceSpans", "EdgeTable",
@@ -28,5 +28,5 @@ __all__ = [
     "decode_metric_long_csv", "decode_prometheus_csv_dir", "decode_skywalking_payload",
     "decode_skywalking_raw", "default_context", "device_count", "device_count_safe", "edge_rows", "fault_target",
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
-    "rank", "skywalking_parents", "synth_generate_host", "synth_services",
+    "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
 ]

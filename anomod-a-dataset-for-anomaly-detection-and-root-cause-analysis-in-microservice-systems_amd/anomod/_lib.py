@@ -26,7 +26,10 @@ TOPO_TT = 1
 OK, EINVAL, EHIP, ERCCL, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
 _STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", ESTATE: "ESTATE"}
 
-STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK = range(5)
+(STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK,
+ STAGE_TRACE_STRUCT, STAGE_SEGMENTS) = range(7)
+NO_PARENT = 0xFFFFFFFF
+SPAN_ROOT, SPAN_FIRST = 0x1, 0x2
 
 
 class AnomodError(RuntimeError):
@@ -60,6 +63,18 @@ class EdgeTableC(C.Structure):
         ("hist", C.POINTER(C.c_uint64)),
         ("p50_us", C.POINTER(C.c_double)),
         ("p99_us", C.POINTER(C.c_double)),
+    ]
+
+
+class TraceStructC(C.Structure):
+    _fields_ = [
+        ("n_services", C.c_uint32),
+        ("parent_pos", C.POINTER(C.c_uint32)),
+        ("depth", C.POINTER(C.c_uint32)),
+        ("n_children", C.POINTER(C.c_uint32)),
+        ("span_flags", C.POINTER(C.c_uint8)),
+        ("n_roots", C.POINTER(C.c_uint32)),
+        ("svc_mask", C.POINTER(C.c_uint64)),
     ]
 
 
@@ -102,6 +117,8 @@ _SIGS = {
     "anomod_spans_generate": (_i32, [_vp, _P(SynthSpec), _u64, _u64, _P(_vp)]),
     "anomod_edge_aggregate_spans": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
     "anomod_edge_aggregate": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(EdgeTableC)]),
+    "anomod_trace_structure_spans": (_i32, [_vp, _vp, _P(TraceStructC)]),
+    "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),
     "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),
     "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),

@@ -11,7 +11,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib as L
-from .spans import EdgeTable, SpanSet, edge_rows
+from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
 
 
 @dataclass
@@ -195,6 +195,22 @@ class Context:
             if table.hist is not None:
                 table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
             return table
+        finally:
+            if tmp is not None:
+                tmp.free()
+
+    def trace_structure(self, spans: DeviceSpans | SpanSet) -> TraceStructure:
+        """Per-span parent/depth/children and per-trace roots/services
+        (the trace-structure HIP kernel)."""
+        tmp = None
+        if isinstance(spans, SpanSet):
+            tmp = spans = self.upload(spans)
+        try:
+            ts = TraceStructure.empty(spans.services, spans.n_spans, spans.n_traces)
+            cs = ts.c_struct()
+            self._check(self._lib.anomod_trace_structure_spans(self.handle, spans.handle,
+                                                               C.byref(cs)))
+            return ts
         finally:
             if tmp is not None:
                 tmp.free()

@@ -185,3 +185,43 @@ class EdgeTable:
             ws.extend(cnt[p, nz].tolist())
             row_ptr[p + 1] = len(cols)
         return row_ptr, np.asarray(cols, dtype=np.uint32), np.asarray(ws, dtype=np.float32)
+
+
+@dataclass
+class TraceStructure:
+    """Per-span / per-trace structure of a span set (trace_collector.py:401-481,
+    536-547; see anomod_trace_structure in include/anomod.h)."""
+
+    services: list[str]
+    parent_pos: np.ndarray   # u32 [n_spans] position of the node's parent in its trace
+    depth: np.ndarray        # u32 [n_spans]
+    n_children: np.ndarray   # u32 [n_spans]
+    span_flags: np.ndarray   # u8  [n_spans] SPAN_ROOT | SPAN_FIRST
+    n_roots: np.ndarray      # u32 [n_traces]
+    svc_mask: np.ndarray     # u64 [n_traces, ceil(S/64)]
+
+    @staticmethod
+    def empty(services: list[str], n_spans: int, n_traces: int) -> "TraceStructure":
+        w = (len(services) + 63) // 64
+        return TraceStructure(list(services), np.zeros(n_spans, np.uint32),
+                              np.zeros(n_spans, np.uint32), np.zeros(n_spans, np.uint32),
+                              np.zeros(n_spans, np.uint8), np.zeros(n_traces, np.uint32),
+                              np.zeros((n_traces, w), np.uint64))
+
+    def c_struct(self) -> L.TraceStructC:
+        return L.TraceStructC(len(self.services), L.ptr(self.parent_pos, C.c_uint32),
+                              L.ptr(self.depth, C.c_uint32), L.ptr(self.n_children, C.c_uint32),
+                              L.ptr(self.span_flags, C.c_uint8), L.ptr(self.n_roots, C.c_uint32),
+                              L.ptr(self.svc_mask, C.c_uint64))
+
+    def services_involved(self, t: int) -> list[str]:
+        """Sorted service names of trace t (trace_collector.py:536)."""
+        m = self.svc_mask[t]
+        return [s for i, s in enumerate(self.services) if (int(m[i // 64]) >> (i % 64)) & 1]
+
+    def root_positions(self, trace_ptr: np.ndarray, t: int) -> list[int]:
+        """Trace-local positions of the root nodes of trace t, in first-seen
+        order (root_span_node_ids, trace_collector.py:443, 544)."""
+        a, b = int(trace_ptr[t]), int(trace_ptr[t + 1])
+        fl = self.span_flags[a:b]
+        return [k for k in range(b - a) if fl[k] == (L.SPAN_ROOT | L.SPAN_FIRST)]

@@ -1,0 +1,127 @@
+// Trace-chunk walking shared by the span kernels (edge aggregation, trace
+// structure).  A wave owns a contiguous range of traces and walks it in
+// chunks of up to 64 whole traces holding <= kStage spans (or one trace longer
+// than kStage), so every per-trace question is answered inside the wave's own
+// LDS staging area.  Internal header (not part of the ABI).
+#pragma once
+
+#include "common.h"
+
+namespace anomod {
+namespace chunk {
+
+constexpr int kWave = 64;
+constexpr int kStage = 256;  // spans staged per wave chunk
+constexpr int kPer = kStage / kWave;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Make a wave-uniform 64-bit value provably uniform (SGPR) for the compiler.
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+// Buffer descriptor over [base, base + bytes): loads past the end return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ uint64_t bload64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint64_t)__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t bload32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+
+// One wave's chunk: up to 64 consecutive traces holding <= kStage spans, or a
+// single trace longer than kStage (k == 0).  base / k / n are wave-uniform.
+struct Chunk {
+  uint64_t base;   // first span
+  uint32_t k;      // traces in the chunk (0 = one big trace)
+  uint32_t n;      // spans in the chunk
+  uint32_t start;  // this lane's trace start relative to base (lanes < k)
+};
+
+// lo/hi = trace_ptr[t + lane], trace_ptr[t + lane + 1] (see load_bounds).
+__device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane, uint64_t lo,
+                                            uint64_t hi) {
+  Chunk c;
+  const bool valid = t + lane < t_end;
+  c.base = uniform64(__shfl(lo, 0));
+  const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
+  c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
+  const uint32_t n = c.k ? (uint32_t)(__shfl(hi, (int)c.k - 1) - c.base)
+                         : (uint32_t)(__shfl(hi, 0) - c.base);
+  c.n = (uint32_t)__builtin_amdgcn_readfirstlane(n);
+  c.start = (uint32_t)(lo - c.base);
+  return c;
+}
+
+// trace_ptr[t + lane] and trace_ptr[t + lane + 1] for lanes t + lane < t_end
+// (0 elsewhere).  t and t_end are wave-uniform.
+__device__ __forceinline__ void load_bounds(const uint64_t* __restrict__ trace_ptr, uint64_t t,
+                                            uint64_t t_end, int lane, uint64_t& lo, uint64_t& hi) {
+  t = uniform64(t);
+  const uint64_t avail = t_end > t ? t_end - t : 0;
+  const uint32_t bytes = (uint32_t)(avail < (uint64_t)kWave ? avail : (uint64_t)kWave) * 8u;
+  lo = bload64(rsrc(trace_ptr + t, bytes), (uint32_t)lane * 8u);
+  hi = bload64(rsrc(trace_ptr + t + 1, bytes), (uint32_t)lane * 8u);
+}
+
+// Trace-start masks of a chunk: bit l of Sm[r] is set when chunk position
+// 64*r + l starts a trace.  lflag is the wave's u8[kStage] LDS scratch.
+__device__ __forceinline__ void start_masks(uint8_t* lflag, const Chunk& c, int lane,
+                                            uint64_t (&Sm)[kPer]) {
+  reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
+  wave_sync();
+  if ((uint32_t)lane < c.k && c.start < c.n) lflag[c.start] = 1;
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) Sm[r] = __ballot(lflag[lane + r * kWave] != 0);
+}
+
+// Bounds [a, b) of the trace holding chunk position i = 64*r + lane, from the
+// four 64-bit trace-start masks (wave-uniform); branch-free (selects only).
+__device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, int lane,
+                                             uint32_t n, uint32_t& a, uint32_t& b) {
+  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+  a = 0;
+  b = n;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (q > r) break;
+    const uint64_t m = (q == r) ? (Sm[q] & le) : Sm[q];
+    const uint32_t pos = 64u * q + 63u - (uint32_t)__clzll((long long)m);
+    a = m ? pos : a;
+  }
+#pragma unroll
+  for (int q = kPer - 1; q >= 0; --q) {
+    if (q < r) break;
+    const uint64_t m = (q == r) ? (Sm[q] & ~le) : Sm[q];
+    const uint32_t pos = 64u * q + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    b = m ? pos : b;
+  }
+  if (b > n) b = n;
+}
+
+// Index of the trace (within the chunk) holding chunk position 64*r + lane.
+__device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], int r, int lane) {
+  uint32_t before = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (q < r) before += (uint32_t)__popcll(Sm[q]);
+  const uint64_t m = Sm[r];
+  const uint32_t below =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  return before + below + (uint32_t)((m >> lane) & 1ull) - 1u;
+}
+
+}  // namespace chunk
+}  // namespace anomod

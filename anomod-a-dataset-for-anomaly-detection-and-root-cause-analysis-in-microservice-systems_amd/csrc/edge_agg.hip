@@ -37,19 +37,18 @@
 #include <cmath>
 #include <limits>
 
+#include "chunk.h"
 #include "common.h"
 
 namespace anomod {
 namespace {
 
-constexpr int kWave = 64;
+using namespace chunk;
 #ifndef ANOMOD_WAVES
 #define ANOMOD_WAVES 16
 #endif
 constexpr int kWavesPerWG = ANOMOD_WAVES;
 constexpr int kThreads = kWave * kWavesPerWG;
-constexpr int kStage = 256;  // spans staged per wave chunk
-constexpr int kPer = kStage / kWave;
 constexpr int kHtLog2 = 13;
 constexpr uint32_t kHtSlots = 1u << kHtLog2;
 constexpr int kMaxProbe = 48;
@@ -96,32 +95,6 @@ struct Cols {
   const uint32_t* __restrict__ svcfl;  // svc | flags << 16
   const uint32_t* __restrict__ dur;
 };
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Make a wave-uniform 64-bit value provably uniform (SGPR) for the compiler.
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
-}
-
-// Buffer descriptor over [base, base + bytes): loads past the end return 0.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-
-__device__ __forceinline__ uint64_t bload64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return (uint64_t)__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
-}
-
-__device__ __forceinline__ uint32_t bload32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
-}
 
 // Histogram increment of key = edge*kBins + bin + 1 in the workgroup's LDS
 // hash table, probing from slot h.  Slot = (count << 32) | key; 0 = empty.
@@ -239,46 +212,12 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
   }
 }
 
-// One wave's chunk: up to 64 consecutive traces holding <= kStage spans, or a
-// single trace longer than kStage (k == 0).  base / k / n are wave-uniform.
-struct Chunk {
-  uint64_t base;   // first span
-  uint32_t k;      // traces in the chunk (0 = one big trace)
-  uint32_t n;      // spans in the chunk
-  uint32_t start;  // this lane's trace start relative to base (lanes < k)
-};
-
 // Span columns of a chunk held in registers while the previous chunk is
 // processed (software pipeline, one chunk ahead).
 struct Regs {
   uint64_t sid[kPer], pid[kPer];
   uint32_t dur[kPer], sf[kPer];  // sf = svc | flags << 16
 };
-
-__device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane, uint64_t lo,
-                                            uint64_t hi) {
-  Chunk c;
-  const bool valid = t + lane < t_end;
-  c.base = uniform64(__shfl(lo, 0));
-  const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
-  c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
-  const uint32_t n = c.k ? (uint32_t)(__shfl(hi, (int)c.k - 1) - c.base)
-                         : (uint32_t)(__shfl(hi, 0) - c.base);
-  c.n = (uint32_t)__builtin_amdgcn_readfirstlane(n);
-  c.start = (uint32_t)(lo - c.base);
-  return c;
-}
-
-// trace_ptr[t + lane] and trace_ptr[t + lane + 1] for lanes t + lane < t_end
-// (0 elsewhere).  t and t_end are wave-uniform.
-__device__ __forceinline__ void load_bounds(const uint64_t* __restrict__ trace_ptr, uint64_t t,
-                                            uint64_t t_end, int lane, uint64_t& lo, uint64_t& hi) {
-  t = uniform64(t);
-  const uint64_t avail = t_end > t ? t_end - t : 0;
-  const uint32_t bytes = (uint32_t)(avail < (uint64_t)kWave ? avail : (uint64_t)kWave) * 8u;
-  lo = bload64(rsrc(trace_ptr + t, bytes), (uint32_t)lane * 8u);
-  hi = bload64(rsrc(trace_ptr + t + 1, bytes), (uint32_t)lane * 8u);
-}
 
 __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int lane, Regs& R) {
   const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by big_trace()
@@ -296,79 +235,6 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
   }
 }
 
-// Bounds [a, b) of the trace holding chunk position i = 64*r + lane, from the
-// four 64-bit trace-start masks (wave-uniform); branch-free (selects only).
-__device__ __forceinline__ void trace_bounds(const uint64_t (&Sm)[kPer], int r, int lane,
-                                             uint32_t n, uint32_t& a, uint32_t& b) {
-  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-  a = 0;
-  b = n;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    if (q > r) break;
-    const uint64_t m = (q == r) ? (Sm[q] & le) : Sm[q];
-    const uint32_t pos = 64u * q + 63u - (uint32_t)__clzll((long long)m);
-    a = m ? pos : a;
-  }
-#pragma unroll
-  for (int q = kPer - 1; q >= 0; --q) {
-    if (q < r) break;
-    const uint64_t m = (q == r) ? (Sm[q] & ~le) : Sm[q];
-    const uint32_t pos = 64u * q + (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    b = m ? pos : b;
-  }
-  if (b > n) b = n;
-}
-
-// The 4 spans of a lane: the first-probe reads of the histogram hash for all
-// four are issued together, so a resident key costs one shared LDS round
-// trip and one fire-and-forget ds_add_u64.
-template <bool LDS_HIST, bool LDS_STATS>
-__device__ __forceinline__ void record4(unsigned char* smem, int lane, uint32_t n,
-                                        const uint32_t (&edge)[kPer], const Regs& R,
-                                        const Table& tab) {
-  if constexpr (!(ANOMOD_ABL & 2)) {
-    uint32_t key[kPer];
-#pragma unroll
-    for (int r = 0; r < kPer; ++r) key[r] = edge[r] * kBins + hist_bin(R.dur[r]) + 1u;
-    if constexpr (LDS_HIST) {
-      auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
-      uint32_t h[kPer];
-      unsigned long long cur[kPer];
-#pragma unroll
-      for (int r = 0; r < kPer; ++r) {
-        h[r] = ht_slot(key[r]);
-        cur[r] = 0ull;
-        if ((uint32_t)lane + r * kWave < n)
-          cur[r] = __hip_atomic_load(&ht[h[r]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#pragma unroll
-      for (int r = 0; r < kPer; ++r) {
-        if ((uint32_t)lane + r * kWave < n) {
-          if ((uint32_t)cur[r] == key[r])
-            atomicAdd(&ht[h[r]], 1ull << 32);
-          else
-            ht_insert(ht, key[r], h[r], tab.hist);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < kPer; ++r)
-        if ((uint32_t)lane + r * kWave < n) atomicAdd(&tab.hist[key[r] - 1u], 1ull);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < kPer; ++r)
-    if ((uint32_t)lane + r * kWave < n)
-      stat_add<LDS_STATS>(smem, edge[r], R.dur[r], R.sf[r] >> 16, tab);
-}
-
-// Parent scan of the 4 span slots of a lane in lockstep.  Ids are staged as
-// split 32-bit halves; every step issues the next 8 low halves (2 x
-// ds_read_b128) of every live slot before comparing, so one LDS round trip
-// serves four lookups; a low-half match is confirmed on the high half.
-// First match in trace order (the reference rule: jaeger_to_csv.py:34-38 /
-// trace_collector.py:424-443).
 #if ANOMOD_CASCADE
 // Cascade form: 8 ids per step read from the trace start on (ds_read_b64,
 // any 8-B alignment, so no position below a is ever compared); the lowest
@@ -429,19 +295,14 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   }
   // Stage ids / services (lanes past n hold zeros from the buffer loads);
   // mark trace starts.
-  reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
     lsid[i] = R.sid[r];
     lsvc[i] = (uint16_t)R.sf[r];
   }
-  wave_sync();
-  if ((uint32_t)lane < c.k && c.start < c.n) lflag[c.start] = 1;
-  wave_sync();
   uint64_t Sm[kPer];
-#pragma unroll
-  for (int r = 0; r < kPer; ++r) Sm[r] = __ballot(lflag[lane + r * kWave] != 0);
+  start_masks(lflag, c, lane, Sm);
   uint32_t edge[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {

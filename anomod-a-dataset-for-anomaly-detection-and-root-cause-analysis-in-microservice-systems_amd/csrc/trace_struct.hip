@@ -1,0 +1,401 @@
+// Trace-structure features: per span the parent's
+// position in its trace, the BFS depth and the child count; per trace the
+// number of roots and the set of services involved.
+//
+// Restates on the GPU what TT_collection-scripts/T-Dataset/trace_collector.py
+// computes per trace, one Python dict at a time, in _build_span_records
+// (:401-481) and collect_traces (:536-547).  Spans are nodes keyed by their
+// id (node_id = segmentId:spanId, :414); with duplicated ids the reference's
+// dicts keep the LAST span's parent (parents[node_id] = ..., :437) while every
+// span appends itself to its own parent's child list (:438-439):
+//   parent_pos  position of the node's parent: the first span of the trace
+//               whose id equals the parent reference of the LAST span with
+//               this node's id; ANOMOD_NO_PARENT when that reference is 0 or
+//               names no span of the trace (:427-437)
+//   depth       distance from the node's root along those parents (the BFS
+//               of :441-449); 0 when the chain never reaches a root (a parent
+//               cycle: unreachable from the roots, :477 default)
+//   n_children  spans whose own parent reference names this node (:438-439),
+//               shared by every span carrying the node's id (:476)
+//   span_flags  ANOMOD_SPAN_ROOT (node parent not in the trace, :443) |
+//               ANOMOD_SPAN_FIRST (first span of the trace with this id)
+//   n_roots     distinct root nodes of the trace (len(root_span_node_ids))
+//   svc_mask    services_involved (:536) as a bit set of service indices
+//
+// GPU form: the chunk walk of the edge kernel (chunk.h) — whole traces in a
+// wave's LDS, ordered scans for the id questions, parent pointer-jumping in
+// LDS for the depth (<= 8 rounds for a 256-span chunk), per-trace counters in
+// LDS.  A trace longer than 256 spans is resolved by the whole wave against
+// HBM (O(L^2 / 64) compares; rare).
+#include "chunk.h"
+#include "common.h"
+
+namespace anomod {
+namespace {
+
+using namespace chunk;
+
+constexpr int kTsWaves = 8;
+constexpr int kTsThreads = kTsWaves * kWave;
+constexpr uint32_t kDone = 0x80000000u;  // pointer-jumping: chain reached a root
+
+// Per-wave LDS carve (bytes; 16-B aligned offsets).
+constexpr int kTSid = 0;                          // u64 span ids   [kStage + 8]
+constexpr int kTPid = kTSid + (kStage + 8) * 8;   // u64 parent refs [kStage + 8]
+constexpr int kTNxt = kTPid + (kStage + 8) * 8;   // u32 jump target | kDone [kStage]
+constexpr int kTDst = kTNxt + kStage * 4;         // u32 distance to the target [kStage]
+constexpr int kTCnt = kTDst + kStage * 4;         // u32 child counts [kStage]
+constexpr int kTSvc = kTCnt + kStage * 4;         // u16 services [kStage]
+constexpr int kTRf = kTSvc + kStage * 2;          // u8 root-node flag of first spans [kStage]
+constexpr int kTFlag = kTRf + kStage;             // u8 trace-start flags [kStage]
+constexpr int kTBytes = kTFlag + kStage;
+static_assert(kTBytes % 16 == 0, "wave area must stay 16-B aligned");
+static_assert(kTBytes * kTsWaves <= 160 * 1024, "LDS budget");
+
+struct TsOut {
+  uint32_t* parent_pos;
+  uint32_t* depth;
+  uint32_t* n_children;
+  uint8_t* flags;
+  uint32_t* n_roots;
+  unsigned long long* svc_mask;  // [n_traces * words]
+  uint32_t words;                // ceil(S / 64)
+};
+
+// First / last position in [a, b) whose id equals x (-1 when none).  The
+// scan covers the whole range (the last match is wanted too).
+__device__ __forceinline__ void first_last(const uint64_t* lsid, uint32_t a, uint32_t b,
+                                           uint64_t x, int& f, int& l) {
+  f = -1;
+  l = -1;
+  for (uint32_t q = a; q < b; ++q) {
+    if (lsid[q] == x) {
+      if (f < 0) f = (int)q;
+      l = (int)q;
+    }
+  }
+}
+
+// First position in [a, b) whose id equals x (-1 when none or x == 0).
+__device__ __forceinline__ int first_of(const uint64_t* lsid, uint32_t a, uint32_t b, uint64_t x) {
+  if (x == 0ull) return -1;
+  for (uint32_t q = a; q < b; ++q)
+    if (lsid[q] == x) return (int)q;
+  return -1;
+}
+
+__device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t t0,
+                         const uint64_t (&sid)[kPer], const uint64_t (&pid)[kPer],
+                         const uint32_t (&svc)[kPer], const TsOut& o) {
+  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kTSid);
+  auto* lpid = reinterpret_cast<uint64_t*>(wsm + kTPid);
+  auto* lnxt = reinterpret_cast<uint32_t*>(wsm + kTNxt);
+  auto* ldst = reinterpret_cast<uint32_t*>(wsm + kTDst);
+  auto* lcnt = reinterpret_cast<uint32_t*>(wsm + kTCnt);
+  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kTSvc);
+  auto* lrf = reinterpret_cast<uint8_t*>(wsm + kTRf);
+  auto* lflag = reinterpret_cast<uint8_t*>(wsm + kTFlag);
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    lsid[i] = sid[r];
+    lpid[i] = pid[r];
+    lcnt[i] = 0u;
+    lsvc[i] = (uint16_t)svc[r];
+  }
+  uint64_t Sm[kPer];
+  start_masks(lflag, c, lane, Sm);
+
+  int f[kPer], np[kPer];
+  uint32_t a[kPer], nxt[kPer], dst[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    f[r] = np[r] = -1;
+    a[r] = 0;
+    if (i < c.n) {
+      uint32_t b;
+      trace_bounds(Sm, r, lane, c.n, a[r], b);
+      int l;
+      first_last(lsid, a[r], b, sid[r], f[r], l);
+      const int pf = first_of(lsid, a[r], b, pid[r]);  // own parent: child lists
+      np[r] = (l == (int)i) ? pf : first_of(lsid, a[r], b, lpid[l]);  // node parent
+      if (pf >= 0) atomicAdd(&lcnt[pf], 1u);
+    }
+    lrf[i] = (uint8_t)(i < c.n && np[r] < 0 && f[r] == (int)i);
+    nxt[r] = np[r] >= 0 ? (uint32_t)np[r] : (i | kDone);
+    dst[r] = np[r] >= 0 ? 1u : 0u;
+    lnxt[i] = nxt[r];
+    ldst[i] = dst[r];
+  }
+  wave_sync();
+  // Pointer jumping: after round k every span points 2^k ancestors up (or at
+  // its root, flagged kDone) and knows the distance; 8 rounds cover 256.
+  for (int round = 0; round < 8; ++round) {
+    bool live = false;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) live |= !(nxt[r] & kDone);
+    if (__ballot(live) == 0ull) break;
+    uint32_t nn[kPer], nd[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      nn[r] = nxt[r];
+      nd[r] = 0u;
+      if (!(nxt[r] & kDone)) {
+        nn[r] = lnxt[nxt[r]];
+        nd[r] = ldst[nxt[r]];
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      if (!(nxt[r] & kDone)) {
+        const uint32_t i = lane + r * kWave;
+        dst[r] += nd[r];
+        nxt[r] = nn[r];  // the target's target; a root target carries kDone
+        lnxt[i] = nxt[r];
+        ldst[i] = dst[r];
+      }
+    }
+    wave_sync();
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const uint32_t i = lane + r * kWave;
+    if (i < c.n) {
+      const uint64_t g = c.base + i;
+      o.parent_pos[g] = np[r] >= 0 ? (uint32_t)np[r] - a[r] : ANOMOD_NO_PARENT;
+      o.depth[g] = (nxt[r] & kDone) ? dst[r] : 0u;
+      o.n_children[g] = lcnt[f[r]];
+      o.flags[g] = (uint8_t)((np[r] < 0 ? ANOMOD_SPAN_ROOT : 0u) |
+                             (f[r] == (int)i ? ANOMOD_SPAN_FIRST : 0u));
+    }
+  }
+  // Per trace: lane l < k owns trace t0 + l = chunk positions [s, e).
+  const uint32_t next_start = (uint32_t)__shfl((int)c.start, (lane + 1) & (kWave - 1));
+  if ((uint32_t)lane < c.k) {
+    const uint32_t s = c.start;
+    const uint32_t e = (lane + 1 < (int)c.k) ? next_start : c.n;
+    const uint64_t t = t0 + lane;
+    uint32_t roots = 0;
+    unsigned long long mask = 0;
+    for (uint32_t q = s; q < e; ++q) {
+      roots += lrf[q];
+      const uint32_t sv = lsvc[q];
+      if (o.words == 1u) mask |= 1ull << sv;
+      else
+        atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
+    }
+    o.n_roots[t] = roots;
+    if (o.words == 1u) o.svc_mask[t] = mask;
+  }
+  wave_sync();
+}
+
+// A trace longer than kStage, resolved against HBM by the whole wave.
+__device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
+                       const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+                       const uint32_t* __restrict__ svcfl, const TsOut& o) {
+  const uint32_t L = (uint32_t)(hi - lo);
+  auto first_last_g = [&](uint64_t x, int& f, int& l) {
+    f = l = -1;
+    for (uint32_t q = 0; q < L; ++q)
+      if (span_id[lo + q] == x) {
+        if (f < 0) f = (int)q;
+        l = (int)q;
+      }
+  };
+  auto first_g = [&](uint64_t x) -> int {
+    if (x == 0ull) return -1;
+    for (uint32_t q = 0; q < L; ++q)
+      if (span_id[lo + q] == x) return (int)q;
+    return -1;
+  };
+  uint32_t roots = 0;
+  unsigned long long mask = 0;
+  // pass 1: node parents, flags, child counts (atomics on n_children)
+  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    if (i < L) {
+      int f, l;
+      first_last_g(span_id[lo + i], f, l);
+      const int pf = first_g(parent[lo + i]);
+      const int np = (l == (int)i) ? pf : first_g(parent[lo + l]);
+      if (pf >= 0) atomicAdd(&o.n_children[lo + pf], 1u);
+      o.parent_pos[lo + i] = np >= 0 ? (uint32_t)np : ANOMOD_NO_PARENT;
+      o.flags[lo + i] = (uint8_t)((np < 0 ? ANOMOD_SPAN_ROOT : 0u) |
+                                    (f == (int)i ? ANOMOD_SPAN_FIRST : 0u));
+      if (np < 0 && f == (int)i) ++roots;
+      const uint32_t sv = svcfl[lo + i] & 0xFFFFu;
+      if (o.words == 1u) mask |= 1ull << sv;
+      else
+        atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_wave_barrier();
+  // pass 2: depth by walking the node parents (<= L steps: longer = cycle);
+  // a duplicate id takes its first span's child count
+  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    if (i < L) {
+      uint32_t j = i, d = 0;
+      while (d <= L) {
+        const uint32_t p = __hip_atomic_load(&o.parent_pos[lo + j], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (p == ANOMOD_NO_PARENT) break;
+        j = p;
+        ++d;
+      }
+      o.depth[lo + i] = d <= L ? d : 0u;
+      int f, l;
+      first_last_g(span_id[lo + i], f, l);
+      if (f != (int)i)
+        o.n_children[lo + i] = __hip_atomic_load(&o.n_children[lo + f], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_wave_barrier();
+  // per-trace outputs
+  for (int off = 32; off > 0; off >>= 1) {
+    roots += (uint32_t)__shfl_xor((int)roots, off);
+    mask |= (unsigned long long)__shfl_xor((long long)mask, off);
+  }
+  if (lane == 0) {
+    o.n_roots[t] = roots;
+    if (o.words == 1u) o.svc_mask[t] = mask;
+  }
+}
+
+__global__ __launch_bounds__(kTsThreads) void trace_struct_kernel(
+    const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+    const uint32_t* __restrict__ svcfl, const uint64_t* __restrict__ trace_ptr, uint64_t n_traces,
+    TsOut o) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kTBytes * kTsWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  unsigned char* wsm = smem + wid * kTBytes;
+  const uint64_t gw = (uint64_t)blockIdx.x * kTsWaves + wid;
+  const uint64_t nw = (uint64_t)gridDim.x * kTsWaves;
+  const uint64_t t_end = uniform64(n_traces * (gw + 1) / nw);
+  uint64_t t = uniform64(n_traces * gw / nw);
+  while (t < t_end) {
+    uint64_t lo, hi;
+    load_bounds(trace_ptr, t, t_end, lane, lo, hi);
+    const Chunk c = make_chunk(t, t_end, lane, lo, hi);
+    if (c.k == 0) {
+      ts_big(lane, c.base, c.base + c.n, t, span_id, parent, svcfl, o);
+      t += 1;
+      continue;
+    }
+    const auto rsid = rsrc(span_id + c.base, c.n * 8u);
+    const auto rpid = rsrc(parent + c.base, c.n * 8u);
+    const auto rsf = rsrc(svcfl + c.base, c.n * 4u);
+    uint64_t sid[kPer], pid[kPer];
+    uint32_t svc[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const uint32_t i = (uint32_t)lane + (uint32_t)(r * kWave);
+      sid[r] = bload64(rsid, i * 8u);
+      pid[r] = bload64(rpid, i * 8u);
+      svc[r] = bload32(rsf, i * 4u) & 0xFFFFu;
+    }
+    ts_chunk(wsm, lane, c, t, sid, pid, svc, o);
+    t += c.k;
+  }
+}
+
+}  // namespace
+}  // namespace anomod
+
+using namespace anomod;
+
+extern "C" {
+
+int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
+                                 anomod_trace_struct_out* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && spans && out, "anomod_trace_structure_spans: NULL argument");
+  ANOMOD_REQUIRE(ctx, out->n_services >= 1 && out->n_services <= 4096,
+                 "n_services=%u out of range [1, 4096]", out->n_services);
+  ANOMOD_REQUIRE(ctx, spans->device == ctx->device, "span set lives on another device");
+  ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < out->n_services,
+                 "span service index %u >= n_services %u", spans->max_svc, out->n_services);
+  if (int rc = bind(ctx)) return rc;
+  const uint64_t n = spans->n_spans, nt = spans->n_traces;
+  const uint32_t words = (out->n_services + 63u) / 64u;
+  // device outputs: parent_pos | depth | n_children (u32 x n), flags (u8 x n),
+  // n_roots (u32 x nt), svc_mask (u64 x nt x words)
+  const size_t off_depth = n * 4, off_cnt = 2 * n * 4, off_flags = 3 * n * 4;
+  const size_t off_roots = (off_flags + n + 7) & ~(size_t)7;
+  const size_t off_mask = (off_roots + nt * 4 + 7) & ~(size_t)7;
+  const size_t bytes = off_mask + nt * words * 8 + 8;
+  char* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) {
+    set_error(ctx, "hipMalloc(%zu) for trace-structure outputs failed", bytes);
+    return ANOMOD_ENOMEM;
+  }
+  auto fail = [&](hipError_t e, const char* what) {
+    (void)hipFree(d);
+    set_error(ctx, "%s failed: %s", what, hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  };
+  hipError_t e = hipMemsetAsync(d + off_cnt, 0, n * 4, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d + off_mask, 0, nt * words * 8, ctx->stream);
+  if (e != hipSuccess) return fail(e, "hipMemsetAsync");
+  TsOut o;
+  o.parent_pos = reinterpret_cast<uint32_t*>(d);
+  o.depth = reinterpret_cast<uint32_t*>(d + off_depth);
+  o.n_children = reinterpret_cast<uint32_t*>(d + off_cnt);
+  o.flags = reinterpret_cast<uint8_t*>(d + off_flags);
+  o.n_roots = reinterpret_cast<uint32_t*>(d + off_roots);
+  o.svc_mask = reinterpret_cast<unsigned long long*>(d + off_mask);
+  o.words = words;
+  if (int rc = stage_begin(ctx, kStageTraceStruct)) {
+    (void)hipFree(d);
+    return rc;
+  }
+  if (nt > 0) {
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(trace_struct_kernel), kTsThreads, 0);
+    if (e != hipSuccess) return fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
+    hipLaunchKernelGGL(trace_struct_kernel, dim3((unsigned)grid), dim3(kTsThreads), 0, ctx->stream,
+                       spans->span_id, spans->parent_span_id, spans->svc_flags, spans->trace_ptr,
+                       nt, o);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(e, "trace_struct_kernel launch");
+  }
+  if (int rc = stage_end(ctx, kStageTraceStruct)) {
+    (void)hipFree(d);
+    return rc;
+  }
+  auto d2h = [&](void* dst, const void* src, size_t nbytes) -> hipError_t {
+    if (!dst || nbytes == 0) return hipSuccess;
+    return hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToHost, ctx->stream);
+  };
+  e = d2h(out->parent_pos, o.parent_pos, n * 4);
+  if (e == hipSuccess) e = d2h(out->depth, o.depth, n * 4);
+  if (e == hipSuccess) e = d2h(out->n_children, o.n_children, n * 4);
+  if (e == hipSuccess) e = d2h(out->span_flags, o.flags, n);
+  if (e == hipSuccess) e = d2h(out->n_roots, o.n_roots, nt * 4);
+  if (e == hipSuccess) e = d2h(out->svc_mask, o.svc_mask, nt * words * 8);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return fail(e, "trace-structure download");
+  (void)hipFree(d);
+  return ANOMOD_OK;
+}
+
+int anomod_trace_structure(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                           const uint64_t* trace_ptr, uint64_t n_traces,
+                           anomod_trace_struct_out* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && soa && out, "anomod_trace_structure: NULL argument");
+  anomod_spans* s = nullptr;
+  if (int rc = anomod_spans_upload(ctx, soa, n_spans, trace_ptr, n_traces, &s)) return rc;
+  const int rc = anomod_trace_structure_spans(ctx, s, out);
+  anomod_spans_free(s);
+  return rc;
+}
+
+}  // extern "C"

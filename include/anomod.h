@@ -116,7 +116,8 @@ int anomod_ctx_destroy(anomod_ctx* ctx);
 int anomod_ctx_synchronize(anomod_ctx* ctx);
 /* Milliseconds of the last launch of a stage, measured with hipEvents on the
  * ctx stream.  stage: 0 = edge aggregation kernel, 1 = edge finalize kernel,
- * 2 = edge all-reduce, 3 = ewma kernel, 4 = pagerank iterations.          */
+ * 2 = edge all-reduce, 3 = ewma kernel, 4 = pagerank iterations,
+ * 5 = trace-structure kernel, 6 = segment-summary kernel.                 */
 int anomod_ctx_stage_ms(const anomod_ctx* ctx, int stage, double* ms);
 
 /* ---- histogram helpers (host) ------------------------------------------- */
@@ -178,6 +179,40 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
 /* One-shot host convenience: upload + aggregate + download.               */
 int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
                           const uint64_t* trace_ptr, uint64_t n_traces, anomod_edge_table* out);
+
+/* ---- trace structure -------------------------------
+ * Per span and per trace, what _build_span_records / collect_traces compute
+ * one dict at a time (trace_collector.py:401-481, 536-547).  Spans are nodes
+ * keyed by their id; with duplicated ids the reference keeps the LAST span's
+ * parent (:437) while every span joins its own parent's child list (:438-439).
+ *   parent_pos  position in the trace of the node's parent (first span whose
+ *               id equals the parent reference of the LAST span carrying the
+ *               node's id), ANOMOD_NO_PARENT when the reference is 0 or names
+ *               no span of the trace (:427-437, :443)
+ *   depth       distance from the node's root along those parents (the BFS of
+ *               :441-449); 0 when no root reaches the node (parent cycle, :477)
+ *   n_children  spans whose own parent reference names the node (:438-439)
+ *   span_flags  ANOMOD_SPAN_ROOT | ANOMOD_SPAN_FIRST (first span with its id)
+ *   n_roots     distinct root nodes of the trace (len(root_span_node_ids))
+ *   svc_mask    services_involved (:536): bit s of word s/64, ceil(S/64) words
+ * Every pointer may be NULL (that output is skipped).                      */
+#define ANOMOD_NO_PARENT 0xFFFFFFFFu
+#define ANOMOD_SPAN_ROOT 0x1u
+#define ANOMOD_SPAN_FIRST 0x2u
+typedef struct {
+  uint32_t n_services;  /* in : S (sizes svc_mask)                          */
+  uint32_t* parent_pos; /* [n_spans]                                        */
+  uint32_t* depth;      /* [n_spans]                                        */
+  uint32_t* n_children; /* [n_spans]                                        */
+  uint8_t* span_flags;  /* [n_spans]                                        */
+  uint32_t* n_roots;    /* [n_traces]                                       */
+  uint64_t* svc_mask;   /* [n_traces * ceil(S / 64)]                        */
+} anomod_trace_struct_out;
+int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
+                                 anomod_trace_struct_out* out);
+int anomod_trace_structure(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                           const uint64_t* trace_ptr, uint64_t n_traces,
+                           anomod_trace_struct_out* out);
 
 /* ---- windowed EWMA / z-score -------------------------
  * X is time-major [T][S] f32 (NaN = missing sample).  Per series:

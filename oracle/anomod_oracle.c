@@ -189,3 +189,59 @@ uint32_t oracle_pagerank(const uint32_t* row_ptr, const uint32_t* col, const flo
   free(y);
   return it;
 }
+
+/* Trace structure of traces [t0, t1): restatement of _build_span_records
+ * (trace_collector.py:401-481) on id columns.  Per trace of L spans:
+ *   first/last(i) : first / last span of the trace with span i's id
+ *   own parent    : first span whose id equals parent[i] (0 = no reference),
+ *                   every such span counts as a child of that node (:438-439)
+ *   node parent   : own parent of last(i) — parents[node_id] keeps the last
+ *                   span's value (:437)
+ *   depth         : walk node parents to a root; > L steps = cycle -> 0 (:477)
+ *   roots         : first spans whose node parent is missing (:443)
+ * parent_pos is trace-local; 0xFFFFFFFF = no parent.  n_children, svc_mask
+ * must be zeroed by the caller. */
+static long or_first(const uint64_t* id, uint64_t a, uint64_t b, uint64_t x) {
+  if (x == 0) return -1;
+  for (uint64_t q = a; q < b; ++q)
+    if (id[q] == x) return (long)(q - a);
+  return -1;
+}
+
+void oracle_trace_structure(const uint64_t* span_id, const uint64_t* parent, const uint16_t* svc,
+                            const uint64_t* trace_ptr, uint64_t t0, uint64_t t1, uint32_t words,
+                            uint32_t* parent_pos, uint32_t* depth, uint32_t* n_children,
+                            uint8_t* flags, uint32_t* n_roots, uint64_t* svc_mask) {
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t a = trace_ptr[t], b = trace_ptr[t + 1], L = b - a;
+    uint32_t roots = 0;
+    for (uint64_t i = a; i < b; ++i) {
+      long f = -1, l = -1;
+      for (uint64_t q = a; q < b; ++q)
+        if (span_id[q] == span_id[i]) {
+          if (f < 0) f = (long)(q - a);
+          l = (long)(q - a);
+        }
+      const long pf = or_first(span_id, a, b, parent[i]);
+      const long np = (l == (long)(i - a)) ? pf : or_first(span_id, a, b, parent[a + l]);
+      if (pf >= 0) n_children[a + pf] += 1;
+      parent_pos[i] = np >= 0 ? (uint32_t)np : 0xFFFFFFFFu;
+      flags[i] = (uint8_t)((np < 0 ? 1u : 0u) | (f == (long)(i - a) ? 2u : 0u));
+      if (np < 0 && f == (long)(i - a)) ++roots;
+      svc_mask[t * words + (svc[i] >> 6)] |= 1ull << (svc[i] & 63u);
+    }
+    for (uint64_t i = a; i < b; ++i) {
+      long f = -1;
+      for (uint64_t q = a; q < b && f < 0; ++q)
+        if (span_id[q] == span_id[i]) f = (long)(q - a);
+      if (f != (long)(i - a)) n_children[i] = n_children[a + f];
+      uint64_t j = i - a, d = 0;
+      while (d <= L && parent_pos[a + j] != 0xFFFFFFFFu) {
+        j = parent_pos[a + j];
+        ++d;
+      }
+      depth[i] = d <= L ? (uint32_t)d : 0u;
+    }
+    n_roots[t] = roots;
+  }
+}

@@ -33,6 +33,8 @@ def lib():
         _lib.oracle_quantiles.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
         _lib.oracle_ewma_z.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_double,
                                        C.c_uint32, C.c_double, C.c_void_p]
+        _lib.oracle_trace_structure.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_uint64,
+                                                                    C.c_uint32] + [C.c_void_p] * 6
         _lib.oracle_pagerank.restype = C.c_uint32
         _lib.oracle_pagerank.argtypes = [C.c_void_p] * 3 + [C.c_uint32, C.c_void_p, C.c_double,
                                                             C.c_uint32, C.c_double, C.c_void_p]
@@ -66,6 +68,23 @@ def edge_aggregate(spans, S: int | None = None, t0: int = 0, t1: int | None = No
                                 _p(tab["errors"]), _p(tab["sum_us"]), _p(tab["min_us"]),
                                 _p(tab["max_us"]), _p(tab["hist"]))
     return tab
+
+
+def trace_structure(spans, S: int | None = None) -> dict:
+    """Per-span parent_pos / depth / n_children / flags and per-trace n_roots /
+    svc_mask of a SpanSet-like object (oracle_trace_structure)."""
+    S = len(spans.services) if S is None else S
+    words = (S + 63) // 64
+    n, nt = spans.n_spans, spans.n_traces
+    out = {"parent_pos": np.zeros(n, np.uint32), "depth": np.zeros(n, np.uint32),
+           "n_children": np.zeros(n, np.uint32), "span_flags": np.zeros(n, np.uint8),
+           "n_roots": np.zeros(nt, np.uint32), "svc_mask": np.zeros((nt, words), np.uint64)}
+    arrs = [np.ascontiguousarray(getattr(spans, k)) for k in
+            ("span_id", "parent_span_id", "svc", "trace_ptr")]
+    lib().oracle_trace_structure(*[_p(a) for a in arrs], 0, nt, words,
+                                 *[_p(out[k]) for k in ("parent_pos", "depth", "n_children",
+                                                        "span_flags", "n_roots", "svc_mask")])
+    return out
 
 
 def quantiles(hist: np.ndarray, q_pct: int) -> np.ndarray:
