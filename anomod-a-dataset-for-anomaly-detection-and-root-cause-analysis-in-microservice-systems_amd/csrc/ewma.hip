@@ -11,6 +11,7 @@
 // 4/W B/sample written.  Loads are double-buffered 32 steps deep per lane to
 // keep enough bytes in flight with only S/64 waves on the chip.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 #include "synth.h"
@@ -104,6 +105,175 @@ __global__ __launch_bounds__(64) void ewma_z_kernel(const float* __restrict__ X,
   gm[s] = st.m;
   gv[s] = st.v;
   gn[s] = st.n;
+}
+
+// Time-parallel form.  A 64-series strip is one workgroup of kNW waves; a
+// super-chunk of kNW*U steps gives every wave U consecutive steps (U a
+// multiple of W, so every window lies inside one wave's steps).
+//  phase A  each wave summarises its U samples as a transfer of the state:
+//           with r = its first valid sample x_f, the samples after x_f map an
+//           incoming (m = r + delta, v) to
+//             m' = M + A*delta,  v' = A*v + Q0 + Q1*delta + Q2*delta^2
+//           (M: the mean run from r; A = beta^c; Q*: the variance recurrence
+//           expanded in delta).  Exact algebra, f64, terms of the size of the
+//           signal around r, so no cancellation at large means.
+//  combine  every wave folds the transfers of the waves before it onto the
+//           carried state, sub-chunk by sub-chunk in time order (x_f first:
+//           the fresh start m = x_f, v = 0 when no sample was seen yet), so
+//           its incoming state is the same fold whatever the super-chunk
+//           grouping — results do not depend on how T is cut into calls when
+//           the cuts fall on multiples of U;
+//  phase C  each wave re-runs its U samples from registers with that exact
+//           incoming state (the sequential recurrence, unchanged) and writes
+//           its window maxima.
+// HBM: every sample is read once (4 B) and every window score written once.
+constexpr int kTpWaves = 12;
+constexpr int kTpThreads = kTpWaves * 64;
+
+struct Transfer {
+  double xf, M, A, Q0, Q1, Q2;
+  uint32_t c;  // valid samples after x_f; bit 31 set when x_f exists
+};
+
+__device__ __forceinline__ void apply_transfer(const Transfer& t, double alpha, double beta,
+                                               double& m, double& v, uint32_t& n) {
+  if (!(t.c & 0x80000000u)) return;  // no valid sample in this sub-chunk
+  const uint32_t c = t.c & 0x7FFFFFFFu;
+  double delta, v1;
+  if (n == 0u) {  // fresh start at x_f: m = x_f, v = 0
+    delta = 0.0;
+    v1 = 0.0;
+  } else {
+    const double d = t.xf - m;
+    const double m1 = fma(alpha, d, m);
+    v1 = beta * fma(alpha * d, d, v);
+    delta = m1 - t.xf;
+  }
+  m = fma(t.A, delta, t.M);
+  v = fma(t.A, v1, fma(fma(t.Q2, delta, t.Q1), delta, t.Q0));
+  n += 1u + c;
+}
+
+template <int kCap>
+__global__ __launch_bounds__(kTpThreads) void ewma_tp_kernel(
+    const float* __restrict__ X, uint64_t T, uint64_t S, double alpha, uint32_t W, uint32_t U,
+    float eps, float* __restrict__ Z, double* __restrict__ gm, double* __restrict__ gv,
+    uint32_t* __restrict__ gn) {
+  __shared__ double ls[6][kTpWaves][64];
+  __shared__ uint32_t lc[kTpWaves][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const uint64_t s = (uint64_t)blockIdx.x * 64 + lane;
+  const bool sv = s < S;
+  const double beta = 1.0 - alpha;
+  double m = sv ? gm[s] : 0.0, v = sv ? gv[s] : 0.0;
+  uint32_t n = sv ? gn[s] : 0u;
+  const uint64_t SC = (uint64_t)kTpWaves * U;
+  const uint32_t row_bytes = (uint32_t)(S * 4u);
+  for (uint64_t t0 = 0; t0 < T; t0 += SC) {
+    const uint64_t tw = __builtin_amdgcn_readfirstlane((uint32_t)(t0 >> 32)) * 0x100000000ull +
+                        __builtin_amdgcn_readfirstlane((uint32_t)t0) + (uint64_t)w * U;
+    const uint32_t cnt = tw < T ? (uint32_t)((T - tw) < U ? (T - tw) : U) : 0u;  // wave-uniform
+    // rows [tw, tw + cnt) through one descriptor: a scalar row offset per load,
+    // one lane offset for all (rows past cnt read as 0 and are never used)
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X + tw * S), (short)0,
+                                                      (int)(cnt * row_bytes), 0x00020000);
+    float x[kCap];
+#pragma unroll
+    for (int u = 0; u < kCap; ++u)
+      x[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           rx, (int)(s * 4u), (int)(u * row_bytes), 0));
+#pragma unroll
+    for (int u = 0; u < kCap; ++u)
+      if ((uint32_t)u >= cnt || !sv) x[u] = NAN;
+    // phase A (branch-free: every update is computed and selected)
+    Transfer tr{0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0u};
+    bool seen = false;
+#pragma unroll
+    for (int u = 0; u < kCap; ++u) {
+      const float xv = x[u];
+      const bool valid = xv == xv;
+      const bool upd = valid && seen;
+      const bool first = valid && !seen;
+      const double xd = (double)xv;
+      const double d = xd - tr.M;
+      const double ad = alpha * d;
+      const double q0 = beta * fma(ad, d, tr.Q0);
+      const double q1 = beta * fma(-2.0 * ad, tr.A, tr.Q1);
+      const double q2 = beta * fma(alpha * tr.A, tr.A, tr.Q2);
+      tr.Q0 = upd ? q0 : tr.Q0;
+      tr.Q1 = upd ? q1 : tr.Q1;
+      tr.Q2 = upd ? q2 : tr.Q2;
+      tr.M = first ? xd : (upd ? tr.M + ad : tr.M);
+      tr.xf = first ? xd : tr.xf;
+      tr.A = upd ? tr.A * beta : tr.A;
+      tr.c += upd ? 1u : 0u;
+      seen = seen || valid;
+    }
+    if (seen) tr.c |= 0x80000000u;
+    ls[0][w][lane] = tr.xf;
+    ls[1][w][lane] = tr.M;
+    ls[2][w][lane] = tr.A;
+    ls[3][w][lane] = tr.Q0;
+    ls[4][w][lane] = tr.Q1;
+    ls[5][w][lane] = tr.Q2;
+    lc[w][lane] = tr.c;
+    __syncthreads();
+    // combine: fold the sub-chunks in time order; remember the state entering
+    // this wave's sub-chunk; the fold of all of them is the carried state
+    double mw = m, vw = v;
+    uint32_t nw = n;
+    for (int j = 0; j < kTpWaves; ++j) {
+      if (j == w) {
+        mw = m;
+        vw = v;
+        nw = n;
+      }
+      const Transfer tj{ls[0][j][lane], ls[1][j][lane], ls[2][j][lane], ls[3][j][lane],
+                        ls[4][j][lane], ls[5][j][lane], lc[j][lane]};
+      apply_transfer(tj, alpha, beta, m, v, n);
+    }
+    // (opaque to the optimiser: keeps it from carrying phase A's 64 f64
+    // conversions of x into phase C — 128 extra registers)
+#pragma unroll
+    for (int u = 0; u < kCap; ++u) asm volatile("" : "+v"(x[u]));
+    // phase C: the sequential recurrence from the exact incoming state
+    // (branch-free form of ewma_step: same arithmetic)
+    double sm = mw, svv = vw;
+    uint32_t sn = nw;
+    float wmax = 0.f;
+    uint32_t wpos = 0;
+    float* zp = Z + (tw / W) * S + s;  // this wave's first window row
+#pragma unroll
+    for (int u = 0; u < kCap; ++u) {
+      if ((uint32_t)u < cnt) {
+        const float xv = x[u];
+        const bool valid = xv == xv;
+        const bool init = valid && sn == 0u;
+        const bool upd = valid && sn != 0u;
+        const double d = (double)xv - sm;
+        const float z = upd ? (float)d * rsqrtf((float)svv + eps) : 0.f;
+        const double m1 = fma(alpha, d, sm);
+        const double v1 = beta * fma(alpha * d, d, svv);
+        sm = init ? (double)xv : (upd ? m1 : sm);
+        svv = init ? 0.0 : (upd ? v1 : svv);
+        sn += valid ? 1u : 0u;
+        wmax = fmaxf(wmax, fabsf(z));
+        if (++wpos == W) {
+          if (sv) *zp = wmax;
+          zp += S;
+          wpos = 0;
+          wmax = 0.f;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (w == 0 && sv) {
+    gm[s] = m;
+    gv[s] = v;
+    gn[s] = n;
+  }
 }
 
 // Synthetic metric matrix: x = mu_s + sigma_s*N(0,1)
@@ -224,10 +394,33 @@ int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint3
     ser->z_cap = zbytes;
   }
   if (int rc = stage_begin(ctx, kStageEwma)) return rc;
-  // One wave per block so the S/64 waves spread evenly over the CUs.
-  const unsigned blocks = (unsigned)((ser->S + 63) / 64);
-  hipLaunchKernelGGL(ewma_z_kernel, dim3(blocks), dim3(64), 0, ctx->stream, ser->X, ser->T,
-                     ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);
+  const unsigned strips = (unsigned)((ser->S + 63) / 64);
+  // Kernel choice: one series per lane down T while the strips alone fill the
+  // chip (>= 4 waves per CU: the sequential recurrence does half the
+  // arithmetic); the time-parallel form when they do not (small S, e.g. one
+  // GPU's shard of series) or when ANOMOD_EWMA_MODE=2 asks for it
+  // (1 = always sequential; tests use both).
+  const char* mode_env = getenv("ANOMOD_EWMA_MODE");
+  const int mode = mode_env ? atoi(mode_env) : 0;
+  const bool time_parallel =
+      W <= 128 && (mode == 2 || (mode == 0 && strips < 4u * (unsigned)ctx->num_cus));
+  if (time_parallel) {
+    // time-parallel: U = the most whole windows that fit the register block
+    const uint32_t cap = W <= 64 ? 64u : 128u;
+    const uint32_t U = W * (cap / W);
+    if (cap == 64)
+      hipLaunchKernelGGL(ewma_tp_kernel<64>, dim3(strips), dim3(kTpThreads), 0, ctx->stream,
+                         ser->X, ser->T, ser->S, (double)alpha, W, U, eps, ser->Z, ser->m, ser->v,
+                         ser->n);
+    else
+      hipLaunchKernelGGL(ewma_tp_kernel<128>, dim3(strips), dim3(kTpThreads), 0, ctx->stream,
+                         ser->X, ser->T, ser->S, (double)alpha, W, U, eps, ser->Z, ser->m, ser->v,
+                         ser->n);
+  } else {
+    // windows longer than a register block: one series per lane down T
+    hipLaunchKernelGGL(ewma_z_kernel, dim3(strips), dim3(64), 0, ctx->stream, ser->X, ser->T,
+                       ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);
+  }
   ANOMOD_HIP(ctx, hipGetLastError());
   if (int rc = stage_end(ctx, kStageEwma)) return rc;
   if (Z_host)

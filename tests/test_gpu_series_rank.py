@@ -21,8 +21,16 @@ def test_ewma_matches_pandas_golden(ctx, golden):
                                rtol=Z_RTOL, atol=Z_ATOL)
 
 
-@pytest.mark.parametrize("T,S,W", [(60, 1, 60), (600, 1000, 60), (4800, 77, 16), (256, 5000, 1)])
-def test_ewma_matches_oracle(ctx, T, S, W):
+@pytest.fixture(params=[1, 2], ids=["sequential", "time_parallel"])
+def ewma_mode(request, monkeypatch):
+    """Run a test under both EWMA kernels (ANOMOD_EWMA_MODE, read per call)."""
+    monkeypatch.setenv("ANOMOD_EWMA_MODE", str(request.param))
+    return request.param
+
+
+@pytest.mark.parametrize("T,S,W", [(60, 1, 60), (600, 1000, 60), (4800, 77, 16), (256, 5000, 1),
+                                   (960, 130, 96), (1200, 70, 150)])
+def test_ewma_matches_oracle(ctx, ewma_mode, T, S, W):
     rng = np.random.default_rng(T + S)
     X = (rng.uniform(0, 1e4, S) + rng.uniform(0.1, 10, S) * rng.standard_normal((T, S)))
     X = X.astype(np.float32)
@@ -32,7 +40,7 @@ def test_ewma_matches_oracle(ctx, T, S, W):
                                rtol=Z_RTOL, atol=Z_ATOL)
 
 
-def test_ewma_streaming_chunks_equal_one_pass(ctx):
+def test_ewma_streaming_chunks_equal_one_pass(ctx, ewma_mode):
     rng = np.random.default_rng(1)
     T, S, W = 1200, 300, 60
     X = (100 + rng.standard_normal((T, S))).astype(np.float32)
@@ -44,6 +52,23 @@ def test_ewma_streaming_chunks_equal_one_pass(ctx):
     z2 = ser.ewma_z(2 / 61, W)
     np.testing.assert_array_equal(np.concatenate([z1, z2]), one)
     ser.free()
+
+
+def test_ewma_time_parallel_nan_runs_and_fresh_start(ctx, monkeypatch):
+    """Leading all-NaN sub-chunks, NaN runs across sub-chunk and super-chunk
+    boundaries, series that never see a sample: the fresh-start and carried
+    paths of the time-parallel fold against the sequential oracle."""
+    rng = np.random.default_rng(17)
+    T, S, W = 2400, 200, 60
+    X = (500 + 20 * rng.standard_normal((T, S))).astype(np.float32)
+    X[:700, :50] = np.nan            # first samples appear mid super-chunk
+    X[900:1500, 50:100] = np.nan     # a gap longer than a sub-chunk
+    X[:, 100:110] = np.nan           # never a sample
+    X[rng.random((T, S)) < 0.2] = np.nan
+    ref = native.ewma_z(X, 2 / 61, W)
+    for mode in ("1", "2"):
+        monkeypatch.setenv("ANOMOD_EWMA_MODE", mode)
+        np.testing.assert_allclose(ctx.ewma_z(X, 2 / 61, W), ref, rtol=Z_RTOL, atol=Z_ATOL)
 
 
 def test_pagerank_matches_networkx_golden(ctx, golden):
