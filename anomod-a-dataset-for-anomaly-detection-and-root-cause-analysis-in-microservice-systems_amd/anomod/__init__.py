@@ -19,6 +19,7 @@ from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec,
                      synth_generate_host, synth_services)
 from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
                      load_experiment, rank)
+from .segments import SegmentSet, service_name_of, trace_infos
 from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
 
 __all__ = [
@@ -29,4 +30,19 @@ __all__ = [
     "decode_skywalking_raw", "default_context", "device_count", "device_count_safe", "edge_rows", "fault_target",
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
     "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
+    "SegmentSet", "service_name_of", "trace_infos", "analyze_trace_patterns",
 ]
+
+
+def analyze_trace_patterns(traces_or_segments, ctx: "Context | None" = None) -> dict:
+    """Drop-in for EnhancedTraceCollector.analyze_trace_patterns
+    (enhanced_trace_collector.py:216-296): accepts its input (a list of
+    extract_trace_info dicts), a raw Elasticsearch segment response, or a
+    SegmentSet; the reductions run on the GPU."""
+    if isinstance(traces_or_segments, SegmentSet):
+        seg = traces_or_segments
+    elif isinstance(traces_or_segments, dict):
+        seg = SegmentSet.from_es(traces_or_segments)
+    else:
+        seg = SegmentSet.from_traces(list(traces_or_segments or []))
+    return (ctx or default_context()).segment_summary(seg)

@@ -78,6 +78,24 @@ class TraceStructC(C.Structure):
     ]
 
 
+class SegmentSummaryC(C.Structure):
+    _fields_ = [
+        ("n_services", C.c_uint32),
+        ("n_endpoints", C.c_uint32),
+        ("service_counts", C.POINTER(C.c_uint64)),
+        ("endpoint_counts", C.POINTER(C.c_uint64)),
+        ("total", C.c_uint64),
+        ("error_count", C.c_uint64),
+        ("latency_count", C.c_uint64),
+        ("latency_sum", C.c_int64),
+        ("latency_min", C.c_int64),
+        ("latency_max", C.c_int64),
+        ("start_count", C.c_uint64),
+        ("start_min", C.c_int64),
+        ("start_max", C.c_int64),
+    ]
+
+
 class SynthSpec(C.Structure):
     _fields_ = [
         ("topology", C.c_uint32),
@@ -119,6 +137,8 @@ _SIGS = {
     "anomod_edge_aggregate": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(EdgeTableC)]),
     "anomod_trace_structure_spans": (_i32, [_vp, _vp, _P(TraceStructC)]),
     "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),
+    "anomod_segment_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_int32), _P(C.c_int64),
+                                      _P(C.c_int64), _u64, _P(SegmentSummaryC)]),
     "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),
     "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),

@@ -215,6 +215,11 @@ class Context:
             if tmp is not None:
                 tmp.free()
 
+    def segment_summary(self, seg) -> dict:
+        """analyze_trace_patterns over a SegmentSet (segment-summary kernel)."""
+        from .segments import segment_summary
+        return segment_summary(self, seg)
+
     # -- metric series
     def ewma_z(self, X: np.ndarray, alpha: float, W: int, eps: float = 1e-12) -> np.ndarray:
         X = np.ascontiguousarray(X, dtype=np.float32)

@@ -214,6 +214,33 @@ int anomod_trace_structure(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t
                            const uint64_t* trace_ptr, uint64_t n_traces,
                            anomod_trace_struct_out* out);
 
+/* ---- segment summary -------------------------------
+ * analyze_trace_patterns (enhanced_trace_collector.py:216-296) over columnar
+ * segment records: svc / endpoint are indices into the caller's name lists
+ * (service_name decoded as extract_trace_info does, :130-150), is_error the
+ * raw value, latency and start_time in ms.
+ *   service_counts[s], endpoint_counts[e]  call counts (:246-253)
+ *   error_count        records with is_error == 1 (:256-257)
+ *   latency_*          count / sum / min / max over latency > 0 (:260-283;
+ *                      avg = sum / count)
+ *   start_*            count / min / max over start_time != 0 (:265-270)
+ * min/max are 0 when their count is 0.                                      */
+typedef struct {
+  uint32_t n_services;       /* in : service ids are < n_services          */
+  uint32_t n_endpoints;      /* in : endpoint ids are < n_endpoints        */
+  uint64_t* service_counts;  /* [n_services] (may be NULL)                 */
+  uint64_t* endpoint_counts; /* [n_endpoints] (may be NULL)                */
+  uint64_t total;            /* out                                        */
+  uint64_t error_count;      /* out                                        */
+  uint64_t latency_count;    /* out                                        */
+  int64_t latency_sum, latency_min, latency_max; /* out                    */
+  uint64_t start_count;      /* out                                        */
+  int64_t start_min, start_max; /* out                                     */
+} anomod_segment_summary_out;
+int anomod_segment_summary(anomod_ctx* ctx, const uint32_t* svc, const uint32_t* endpoint,
+                           const int32_t* is_error, const int64_t* latency,
+                           const int64_t* start_time, uint64_t n, anomod_segment_summary_out* out);
+
 /* ---- windowed EWMA / z-score -------------------------
  * X is time-major [T][S] f32 (NaN = missing sample).  Per series:
  *   d_t = x_t - m_{t-1};  z_t = d_t / sqrt(v_{t-1} + eps)
