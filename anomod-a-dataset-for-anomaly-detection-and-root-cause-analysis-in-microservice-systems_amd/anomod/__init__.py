@@ -20,6 +20,7 @@ from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec,
 from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
                      load_experiment, rank)
 from .segments import SegmentSet, service_name_of, trace_infos
+from .writers import jaeger_to_csv, write_jaeger_csv, write_metric_long_csv
 from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
 
 __all__ = [
@@ -31,6 +32,7 @@ __all__ = [
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
     "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
     "SegmentSet", "service_name_of", "trace_infos", "analyze_trace_patterns",
+    "jaeger_to_csv", "write_jaeger_csv", "write_metric_long_csv",
 ]
 
 

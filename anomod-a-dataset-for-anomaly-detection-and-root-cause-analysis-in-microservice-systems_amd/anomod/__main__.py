@@ -1,4 +1,5 @@
 """CLI:  python -m anomod features <trace file|dir> [--metrics PATH] [--out FILE]
+       python -m anomod jaeger-to-csv <all_traces.json> <all_traces.csv>
 
 Computes the RCA features of one experiment on the GPU and writes them as JSON:
 the call-graph edge table (count, errors, mean/min/max, p50/p99 per edge), the
@@ -25,7 +26,14 @@ def main(argv=None) -> int:
     f.add_argument("--window", type=int, default=60)
     f.add_argument("--alpha", type=float, default=0.85, help="PageRank damping")
     f.add_argument("--out", help="output JSON (default: stdout)")
+    j = sub.add_parser("jaeger-to-csv",
+                       help="span CSV identical to jaeger_to_csv.py's (collect_trace.sh:70)")
+    j.add_argument("input")
+    j.add_argument("output")
     args = ap.parse_args(argv)
+    if args.cmd == "jaeger-to-csv":
+        from .writers import jaeger_to_csv
+        return jaeger_to_csv(args.input, args.output)
 
     exp = load_experiment(args.traces, metrics=args.metrics)
     feats = features(exp, W=args.window)

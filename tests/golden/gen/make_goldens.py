@@ -19,10 +19,14 @@ inputs and the outputs the reference computed from them are written.
   percentiles.json
       latency lists -> SN .../api_responses/monitor_http_responses.py
       OpenAPIResponseCollector.generate_summary
+  metric_long.csv / metric_results.json
+      synthetic Prometheus query_range results -> TT_collection-scripts/
+      T-Dataset/metric_collector.py MetricCollector.collect_experiment_metrics_csv
+      (the HTTP query, boot-time probe and sleeps replaced by stubs; TZ=UTC)
   ewma_pandas.npz        pandas Series.ewm(alpha, adjust=False) mean/var
   pagerank_networkx.npz  networkx.pagerank (3.4.2, scipy backend)
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py [--only metric]
 """
 from __future__ import annotations
 
@@ -324,8 +328,81 @@ def pagerank_golden(seed=13, N=300, alpha=0.85):
             "x": np.asarray([x[i] for i in range(N)])}
 
 
+# ---------------------------------------------------------------------------
+# TT long-format metric CSV (metric_collector.py:400-478)
+# ---------------------------------------------------------------------------
+def prometheus_results(seed: int = 23) -> dict:
+    """Synthetic query_range answers for a few of the collector's queries:
+    several series per query, label sets that differ between series, 'NaN'
+    samples, a query with no data (absent from the CSV) and a series without
+    'metric' labels."""
+    rng = random.Random(seed)
+    t0 = 1762178400  # 2025-11-03 14:00:00 UTC
+    pods = ["ts-order-service-7d9c", "ts-travel-service-5b8f", "ts-route-service-66a1"]
+
+    def series(labels, n=12, nan_p=0.1, scale=1.0):
+        vals = []
+        for k in range(n):
+            v = "NaN" if rng.random() < nan_p else repr(round(rng.uniform(0, 100) * scale, 6))
+            vals.append([t0 + 15 * k, v])
+        item = {"values": vals}
+        if labels is not None:
+            item["metric"] = labels
+        return item
+
+    res = {}
+    res["rate(container_cpu_usage_seconds_total[1m])"] = [
+        series({"__name__": "x", "namespace": "default", "pod": p, "container": p.rsplit("-", 1)[0]})
+        for p in pods]
+    res["container_memory_usage_bytes"] = [
+        series({"pod": p, "namespace": "default"}, scale=1e6) for p in pods[:2]] + [
+        series({"pod": pods[2], "instance": "10.0.0.7:9100", "job": "kubelet"}, scale=1e6)]
+    res["up"] = [series({"job": "prometheus", "instance": "localhost:9090"}, nan_p=0.0),
+                 series(None, n=5, nan_p=0.0)]
+    res["process_open_fds"] = [series({"job": "node", "instance": "n1"}, n=8)]
+    res["node_load1"] = []  # no data -> skipped by the collector
+    return res
+
+
+def metric_long_golden(results: dict, out_csv: Path) -> None:
+    os.environ["TZ"] = "UTC"
+    import time
+    time.tzset()
+    sys.path.insert(0, str(REF / "TT_collection-scripts/T-Dataset"))
+    try:
+        import metric_collector as mc  # noqa: E402  (reference, run time only)
+    finally:
+        sys.path.pop(0)
+    import datetime as dt
+    with tempfile.TemporaryDirectory() as tmp:
+        col = mc.MetricCollector(prometheus_url="http://prometheus.invalid:9090", output_dir=tmp)
+        col.key_metrics = list(results)
+
+        def fake_range(self, query, start, end, step="15s"):
+            r = results[query]
+            return {"status": "success", "data": {"resultType": "matrix", "result": r}}
+
+        col.query_prometheus_range = types.MethodType(fake_range, col)
+        col.get_system_startup_time = types.MethodType(
+            lambda self: dt.datetime(2025, 11, 3, 14, 0, 0), col)
+        real_sleep = mc.time.sleep
+        mc.time.sleep = lambda s: None
+        try:
+            path = col.collect_experiment_metrics_csv(experiment_name="golden", step="15s")
+        finally:
+            mc.time.sleep = real_sleep
+        Path(out_csv).write_bytes(Path(path).read_bytes())
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only in (None, "metric"):
+        res = prometheus_results()
+        (OUT / "metric_results.json").write_text(json.dumps(res))
+        metric_long_golden(res, OUT / "metric_long.csv")
+    if only is not None:
+        return
     doc = jaeger_doc()
     (OUT / "jaeger_small.json").write_text(json.dumps(doc))
     run_jaeger_to_csv(doc, OUT / "jaeger_small.csv")
