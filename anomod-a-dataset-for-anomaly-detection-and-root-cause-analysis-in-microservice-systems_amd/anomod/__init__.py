@@ -11,7 +11,7 @@ ctypes C ABI (include/anomod.h); there is no CPU fallback.
 """
 from ._lib import (FLAG_ERROR, HIST_BINS, HIST_SUB_BITS, AnomodError, EXPORTED_SYMBOLS,
                    LIB_PATH, lib)
-from .decode import (MetricMatrix, decode_jaeger, decode_metric_long_csv,
+from .decode import (MetricMatrix, decode_jaeger, decode_native, load_trace_file, decode_metric_long_csv,
                      decode_prometheus_csv_dir, decode_skywalking_payload, decode_skywalking_raw,
                      jaeger_span_rows, merge_jaeger_dumps, skywalking_parents)
 from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec, device_count,
@@ -32,7 +32,8 @@ __all__ = [
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
     "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
     "SegmentSet", "service_name_of", "trace_infos", "analyze_trace_patterns",
-    "jaeger_to_csv", "write_jaeger_csv", "write_metric_long_csv",
+    "jaeger_to_csv", "write_jaeger_csv", "write_metric_long_csv", "decode_native",
+    "load_trace_file",
 ]
 
 

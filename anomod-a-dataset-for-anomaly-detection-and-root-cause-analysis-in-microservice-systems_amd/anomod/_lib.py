@@ -139,6 +139,13 @@ _SIGS = {
     "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),
     "anomod_segment_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_int32), _P(C.c_int64),
                                       _P(C.c_int64), _u64, _P(SegmentSummaryC)]),
+    "anomod_decode_jaeger": (_i32, [C.c_char_p, _u64, _P(C.c_char_p), _u32, _P(_vp)]),
+    "anomod_decode_skywalking": (_i32, [C.c_char_p, _u64, _P(C.c_char_p), _u32, _P(_vp)]),
+    "anomod_decoded_info": (_i32, [_vp, _P(_u64), _P(_u64), _P(_u32)]),
+    "anomod_decoded_service": (C.c_char_p, [_vp, _u32]),
+    "anomod_decoded_columns": (_i32, [_vp, _P(SpanSoA), _P(_u64)]),
+    "anomod_decoded_free": (_i32, [_vp]),
+    "anomod_hash64": (_u64, [C.c_char_p, _u64]),
     "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),
     "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),

@@ -14,16 +14,19 @@ collector that wrote the file (paths relative to the reference root):
 from __future__ import annotations
 
 import csv
-import hashlib
+import ctypes as C
 import json
 import math
+import re
 from dataclasses import dataclass
 from datetime import datetime
 from pathlib import Path
 from typing import Iterable
 
 import numpy as np
+import xxhash
 
+from . import _lib as L
 from .spans import SpanSet
 
 U32_MAX = 0xFFFFFFFF
@@ -31,24 +34,24 @@ ORPHAN_ID = 0xFFFFFFFFFFFFFFFF  # a parent id no dense local id can equal
 
 
 def hash64(s: str) -> int:
-    """Stable 64-bit id of a string (never 0)."""
-    h = int.from_bytes(hashlib.blake2b(s.encode("utf-8", "surrogatepass"),
-                                       digest_size=8).digest(), "little")
-    return h or 1
+    """Stable 64-bit id of a string (never 0): xxh64, seed 0 — the hash of the
+    native decoders (anomod_hash64)."""
+    return xxhash.xxh64_intdigest(s.encode("utf-8", "surrogatepass")) or 1
+
+
+_HEX_ID = re.compile(r"[0-9a-fA-F]{1,16}")
 
 
 def jaeger_id(s) -> int:
-    """Jaeger spanID (hex string, up to 16 digits) -> u64; '' -> 0."""
+    """Jaeger spanID -> u64: its value when it is 1-16 hex digits and not 0,
+    else xxh64 | 2^63; '' -> 0."""
     if s is None or s == "":
         return 0
     s = str(s)
-    if 0 < len(s) <= 16:
-        try:
-            v = int(s, 16)
-            if v != 0:
-                return v
-        except ValueError:
-            pass
+    if _HEX_ID.fullmatch(s):
+        v = int(s, 16)
+        if v != 0:
+            return v
     return hash64(s) | (1 << 63)
 
 
@@ -358,6 +361,65 @@ def decode_prometheus_csv_dir(directory) -> MetricMatrix:
                     v = row.get("value", "")
                     d[t] = float(v) if v not in ("", None) else math.nan
     return _to_matrix(samples, ts_set)
+
+
+# --------------------------------------------------------------------------
+# Native decoders (libanomod, csrc/decode.cpp): same columns as the Python
+# decoders above, without a Python object per span
+# --------------------------------------------------------------------------
+
+def decode_native(data: bytes, kind: str, services: list[str] | None = None) -> SpanSet:
+    """A Jaeger dump (kind 'jaeger') or a SkyWalking collector payload
+    (kind 'skywalking') -> SpanSet, parsed by the native decoder."""
+    lib = L.lib()
+    fn = {"jaeger": lib.anomod_decode_jaeger, "skywalking": lib.anomod_decode_skywalking}[kind]
+    names = None
+    if services is not None:
+        names = (C.c_char_p * max(1, len(services)))(*[s.encode() for s in services])
+    h = C.c_void_p()
+    L.check(fn(data, len(data), names, 0 if services is None else len(services), C.byref(h)))
+    try:
+        ns, nt, nsv = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        L.check(lib.anomod_decoded_info(h, C.byref(ns), C.byref(nt), C.byref(nsv)))
+        n = ns.value
+        arr = dict(trace_hash=np.empty(n, np.uint64), span_id=np.empty(n, np.uint64),
+                   parent_span_id=np.empty(n, np.uint64), svc=np.empty(n, np.uint16),
+                   flags=np.empty(n, np.uint16), dur_us=np.empty(n, np.uint32))
+        ptr = np.empty(nt.value + 1, np.uint64)
+        soa = L.SpanSoA(*[L.ptr(arr[k], t) for k, t in (
+            ("trace_hash", C.c_uint64), ("span_id", C.c_uint64), ("parent_span_id", C.c_uint64),
+            ("svc", C.c_uint16), ("flags", C.c_uint16), ("dur_us", C.c_uint32))])
+        L.check(lib.anomod_decoded_columns(h, C.byref(soa), L.ptr(ptr, C.c_uint64)))
+        svcs = [lib.anomod_decoded_service(h, i).decode() for i in range(nsv.value)]
+    finally:
+        lib.anomod_decoded_free(h)
+    return SpanSet(svcs, ptr, **arr)
+
+
+def _first_key(data: bytes) -> str | None:
+    m = re.match(rb'\s*\{\s*"((?:[^"\\]|\\.)*)"', data[:4096])
+    return m.group(1).decode("utf-8", "replace") if m else None
+
+
+def load_trace_file(path, services: list[str] | None = None) -> SpanSet:
+    """A trace file of the dataset -> SpanSet: Jaeger dumps ({"data": ...})
+    and collector payloads ({"metadata": ..., "traces": ...}) go through the
+    native decoder; anything else (raw GraphQL span lists) through the
+    Python decoders."""
+    data = Path(path).read_bytes()
+    key = _first_key(data)
+    if key == "data":
+        return decode_native(data, "jaeger", services)
+    if key in ("metadata", "traces"):
+        return decode_native(data, "skywalking", services)
+    doc = json.loads(data)
+    if isinstance(doc, dict) and "traces" in doc:
+        return decode_skywalking_payload(doc, services)
+    if isinstance(doc, dict) and "data" in doc:
+        return decode_jaeger(doc, services)
+    if isinstance(doc, list):
+        return decode_skywalking_raw(doc, services)
+    raise ValueError(f"{path}: not a Jaeger dump or SkyWalking payload")
 
 
 def load_json(path) -> dict:

@@ -120,15 +120,7 @@ def load_experiment(source, *, metrics=None, name: str | None = None,
             if not cands:
                 raise FileNotFoundError(f"no trace JSON under {path}")
             doc_path = cands[-1]
-    doc = decode.load_json(doc_path)
-    if isinstance(doc, dict) and "traces" in doc:
-        spans = decode.decode_skywalking_payload(doc, services)
-    elif isinstance(doc, dict) and "data" in doc:
-        spans = decode.decode_jaeger(doc, services)
-    elif isinstance(doc, list):
-        spans = decode.decode_skywalking_raw(doc, services)
-    else:
-        raise ValueError(f"{doc_path}: not a Jaeger dump or SkyWalking payload")
+    spans = decode.load_trace_file(doc_path, services)
     mm = None
     if metrics is not None:
         mp = Path(metrics)

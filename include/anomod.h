@@ -164,6 +164,32 @@ int anomod_synth_generate_host(const anomod_synth_spec* spec, uint64_t shard, ui
 int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64_t shard,
                           uint64_t n_traces, anomod_spans** out);
 
+/* ---- native trace-file decoders --------------------
+ * Parse a whole file image (caller's bytes, UTF-8 JSON) into span columns
+ * without a Python object per span:
+ *   anomod_decode_jaeger      Jaeger /api/traces dump (all_traces.json), the
+ *                             columns jaeger_to_csv.py:21-90 derives
+ *   anomod_decode_skywalking  trace_collector.py collector payload
+ *                             ({metadata, traces:[{summary, spans}]}, :564-578)
+ * services (may be NULL): the service-name list to index against; NULL =
+ * the sorted distinct names of the file.  Ids: Jaeger spanIDs of 1-16 hex
+ * digits are their value, other ids xxh64 | 2^63; SkyWalking node ids become
+ * dense per-trace ids (first occurrence + 1; a parent naming no node of the
+ * trace = UINT64_MAX).  trace_hash = xxh64 of the trace id.                 */
+typedef struct anomod_decoded anomod_decoded;
+int anomod_decode_jaeger(const char* json, uint64_t len, const char* const* services,
+                         uint32_t n_services, anomod_decoded** out);
+int anomod_decode_skywalking(const char* json, uint64_t len, const char* const* services,
+                             uint32_t n_services, anomod_decoded** out);
+int anomod_decoded_info(const anomod_decoded* d, uint64_t* n_spans, uint64_t* n_traces,
+                        uint32_t* n_services);
+const char* anomod_decoded_service(const anomod_decoded* d, uint32_t i);
+int anomod_decoded_columns(const anomod_decoded* d, const anomod_span_soa_out* dst,
+                           uint64_t* trace_ptr /* [n_traces + 1] */);
+int anomod_decoded_free(anomod_decoded* d);
+/* The 64-bit id hash of the decoders (xxh64, seed 0; 0 maps to 1).       */
+uint64_t anomod_hash64(const char* s, uint64_t len);
+
 /* ---- edge aggregation (the hot path) -------------------------------------
  * Call-graph edge table with per-edge latency histogram, count, errors,
  * sum/min/max and p50/p99.  Replaces and extends the per-span loops of

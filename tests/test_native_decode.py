@@ -1,0 +1,113 @@
+"""Native decoders (csrc/decode.cpp) column-equal to the
+Python decoders, which are pinned to the reference's own outputs
+(test_decode.py / test_oracle_goldens.py).  Host-only: no GPU needed."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+import anomod
+from anomod import _lib as L
+from anomod import decode
+
+COLS = ("trace_ptr", "trace_hash", "span_id", "parent_span_id", "svc", "flags", "dur_us")
+
+
+def _same(a, b):
+    assert a.services == b.services
+    for k in COLS:
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
+def test_hash64_matches_python():
+    lib = L.lib()
+    rng = random.Random(1)
+    for s in ["", "a", "abc", "x" * 31, "y" * 32, "z" * 33, "ü€😀", "7c2fc07fa518f930"] + [
+            "".join(rng.choice("0123456789abcdef") for _ in range(rng.randint(1, 80)))
+            for _ in range(200)]:
+        b = s.encode()
+        assert lib.anomod_hash64(b, len(b)) == decode.hash64(s)
+
+
+def test_jaeger_golden_native_equals_python(golden):
+    data = (golden / "jaeger_small.json").read_bytes()
+    _same(anomod.decode_native(data, "jaeger"), decode.decode_jaeger(json.loads(data)))
+
+
+def test_skywalking_payload_native_equals_python(golden):
+    g = json.loads((golden / "skywalking_small.json").read_text())
+    data = json.dumps(g["payload"]).encode()
+    _same(anomod.decode_native(data, "skywalking"), decode.decode_skywalking_payload(g["payload"]))
+    data2 = json.dumps(g["payload"], indent=2, ensure_ascii=False).encode()  # collector's format
+    _same(anomod.decode_native(data2, "skywalking"),
+          decode.decode_skywalking_payload(g["payload"]))
+
+
+def _messy_jaeger(rng, n_traces=60):
+    svcs = ["svc-α", "svc \"q\"", "svc\\b", "plain", "emoji😀"]
+    data = []
+    for t in range(n_traces):
+        procs = {f"p{k}": {"serviceName": rng.choice(svcs)} for k in range(3)}
+        spans = []
+        ids = [("%016x" % rng.getrandbits(64)) if rng.random() < 0.8 else
+               rng.choice(["", "0", "zz-not-hex", "00000000000000000001", "0000000000000000"])
+               for _ in range(rng.randint(0, 12))]
+        for j, sid in enumerate(ids):
+            refs = []
+            if j and rng.random() < 0.9:
+                refs.append({"refType": rng.choice(["CHILD_OF", "FOLLOWS_FROM"]),
+                             "spanID": rng.choice(ids[:j])})
+                if rng.random() < 0.3:
+                    refs.append({"refType": "CHILD_OF", "spanID": rng.choice(ids)})
+            tags = []
+            for _ in range(rng.randint(0, 4)):
+                k = rng.choice(["error", "http.status_code", "component", "x"])
+                v = rng.choice([True, False, "true", "TRUE", "false", 200, 503, "503", " 500 ",
+                                "5_03", "499", 503.7, 12.0, "abc", None, -1])
+                tags.append({"key": k, "type": "x", "value": v})
+            dur = rng.choice([0, 1, 123, 2**32 + 5, -4, 17.9, "88", "x", None])
+            sp = {"traceID": "t", "spanID": sid, "operationName": "op", "references": refs,
+                  "startTime": 1762207158839501 + j, "duration": dur, "tags": tags,
+                  "logs": [], "processID": rng.choice(["p0", "p1", "p2", "p9"])}
+            if rng.random() < 0.05:
+                del sp["references"]
+            spans.append(sp)
+        data.append({"traceID": rng.choice(["%032x" % rng.getrandbits(128), "", "tr\\u00e9"]),
+                     "spans": spans, "processes": procs})
+    return {"data": data}
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_jaeger_messy_native_equals_python(seed):
+    doc = _messy_jaeger(random.Random(seed))
+    for text in (json.dumps(doc), json.dumps(doc, indent=2, ensure_ascii=False),
+                 json.dumps(doc, separators=(",", ":"))):
+        _same(anomod.decode_native(text.encode(), "jaeger"), decode.decode_jaeger(json.loads(text)))
+
+
+def test_service_list_and_errors(golden):
+    data = (golden / "jaeger_small.json").read_bytes()
+    py = decode.decode_jaeger(json.loads(data))
+    fixed = ["zzz-extra"] + py.services
+    got = anomod.decode_native(data, "jaeger", fixed)
+    assert got.services == fixed
+    np.testing.assert_array_equal(got.svc, py.svc + 1)
+    with pytest.raises(anomod.AnomodError):
+        anomod.decode_native(data, "jaeger", ["only-one"])
+    with pytest.raises(anomod.AnomodError):
+        anomod.decode_native(b'{"data": [1, 2', "jaeger")
+    empty = anomod.decode_native(b'{"data": []}', "jaeger")
+    assert empty.n_spans == 0 and empty.n_traces == 0
+
+
+def test_load_trace_file_dispatch(golden, tmp_path):
+    g = json.loads((golden / "skywalking_small.json").read_text())
+    p = tmp_path / "x_skywalking_traces_1.json"
+    p.write_text(json.dumps(g["payload"], indent=2))
+    _same(anomod.load_trace_file(p), decode.decode_skywalking_payload(g["payload"]))
+    r = tmp_path / "raw.json"
+    r.write_text(json.dumps(g["inputs"]))
+    _same(anomod.load_trace_file(r), decode.decode_skywalking_raw(g["inputs"]))
+    _same(anomod.load_trace_file(golden / "jaeger_small.json"),
+          decode.decode_jaeger(json.loads((golden / "jaeger_small.json").read_text())))
