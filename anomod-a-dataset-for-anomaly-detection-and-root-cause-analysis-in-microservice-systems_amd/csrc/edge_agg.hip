@@ -59,12 +59,6 @@ constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
 #endif
-#ifndef ANOMOD_CASCADE
-#define ANOMOD_CASCADE 0  // 1 = descending-select parent scan from the trace start
-#endif
-#ifndef ANOMOD_HB
-#define ANOMOD_HB 0  // 1 = batch the first histogram probes of a lane's 4 spans
-#endif
 
 // LDS carve (bytes, every offset a multiple of 16).
 constexpr int kOffHt = 0;                                // u64 slots (count<<32 | key)
@@ -235,27 +229,6 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
   }
 }
 
-#if ANOMOD_CASCADE
-// Cascade form: 8 ids per step read from the trace start on (ds_read_b64,
-// any 8-B alignment, so no position below a is ever compared); the lowest
-// matching position of a step comes from a descending select chain.  A
-// match at or past b means no in-trace match (every in-trace position of the
-// step is lower).  First match in trace order (jaeger_to_csv.py:34-38 /
-// trace_collector.py:424-443).
-__device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
-                                           uint64_t pid) {
-  for (uint32_t q0 = a; q0 < b; q0 += 8) {
-    uint64_t v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];
-    uint32_t idx = 8u;
-#pragma unroll
-    for (int j = 7; j >= 0; --j) idx = (v[j] == pid) ? (uint32_t)j : idx;
-    if (idx < 8u) return (q0 + idx < b) ? (int)(q0 + idx) : -1;
-  }
-  return -1;
-}
-#else
 // First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read_b128
 // from a 16-B aligned start), matches folded into a bit mask.  First match in
 // trace order (the reference rule: jaeger_to_csv.py:34-38 /
@@ -277,7 +250,6 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   }
   return -1;
 }
-#endif
 
 template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
@@ -303,7 +275,6 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   }
   uint64_t Sm[kPer];
   start_masks(lflag, c, lane, Sm);
-  uint32_t edge[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
@@ -317,14 +288,9 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
         if (q >= 0) p = lsvc[q];
       }
     }
-    edge[r] = p * S + (R.sf[r] & 0xFFFFu);
-#if !ANOMOD_HB
-    if (i < c.n) record<LDS_HIST, LDS_STATS>(smem, edge[r], R.dur[r], R.sf[r] >> 16, tab);
-#endif
+    if (i < c.n) record<LDS_HIST, LDS_STATS>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r],
+                                             R.sf[r] >> 16, tab);
   }
-#if ANOMOD_HB
-  record4<LDS_HIST, LDS_STATS>(smem, lane, c.n, edge, R, tab);
-#endif
   wave_sync();
 }
 
