@@ -199,13 +199,20 @@ class Context:
             if tmp is not None:
                 tmp.free()
 
-    def trace_structure(self, spans: DeviceSpans | SpanSet) -> TraceStructure:
+    def trace_structure(self, spans: DeviceSpans | SpanSet,
+                        download: bool = True) -> TraceStructure | None:
         """Per-span parent/depth/children and per-trace roots/services
-        (the trace-structure HIP kernel)."""
+        (the trace-structure HIP kernel).  download=False runs the kernel
+        without copying the outputs back (timing)."""
         tmp = None
         if isinstance(spans, SpanSet):
             tmp = spans = self.upload(spans)
         try:
+            if not download:
+                cs = L.TraceStructC(len(spans.services))
+                self._check(self._lib.anomod_trace_structure_spans(self.handle, spans.handle,
+                                                                   C.byref(cs)))
+                return None
             ts = TraceStructure.empty(spans.services, spans.n_spans, spans.n_traces)
             cs = ts.c_struct()
             self._check(self._lib.anomod_trace_structure_spans(self.handle, spans.handle,
@@ -281,6 +288,17 @@ class DeviceGraph:
                                                       L.ptr(p, C.c_double), alpha, iters, tol,
                                                       L.ptr(x, C.c_double), C.byref(done)))
         return x, done.value
+
+    def pagerank_batch(self, P, alpha=0.85, iters=100, tol=0.0):
+        """K personalizations ([K, N]) in one batched solve -> x [K, N]."""
+        P = np.ascontiguousarray(np.atleast_2d(P), np.float64)
+        K = P.shape[0]
+        X = np.empty((K, self.N), np.float64)
+        done = C.c_uint32()
+        self.ctx._check(L.lib().anomod_graph_pagerank_batch(
+            self.ctx.handle, self.handle, L.ptr(P, C.c_double), K, alpha, iters, tol,
+            L.ptr(X, C.c_double), C.byref(done)))
+        return X, done.value
 
     def free(self):
         if self.handle:

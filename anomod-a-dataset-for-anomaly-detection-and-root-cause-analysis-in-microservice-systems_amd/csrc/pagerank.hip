@@ -35,6 +35,12 @@ struct anomod_graph {
   // buffers 0..2 dangling mass (2^-62 units), 3..5 L1 change (2^-61 units).
   unsigned long long* acc = nullptr;
   std::vector<unsigned long long> host_acc;
+  // batched solves (anomod_graph_pagerank_batch): node-major [N][Kb] vectors
+  uint32_t kb = 0;                  // allocated batch width
+  double* bp = nullptr;             // [N][kb] personalizations
+  double* bx[2] = {nullptr, nullptr};
+  unsigned long long* bacc = nullptr;  // [6][kb][kAccSlots]
+  std::vector<unsigned long long> host_bacc;
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
   uint32_t exec_iters = 0;
@@ -133,11 +139,88 @@ __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
   }
 }
 
+// K personalization vectors per launch (replica mode, SURVEY.md §8e: one
+// vector per experiment or fault hypothesis): the in-edge CSR is read once
+// for all K, x is node-major [N][K] so an edge gathers K contiguous doubles.
+// Per vector the arithmetic, the block partition and the reduction order are
+// those of ppr_iter_kernel, so each column equals its single-vector solve
+// bit for bit.  Vectors whose bit is set in `frozen` (converged in tolerance
+// mode) are carried unchanged.
+template <int K>
+__global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
+    uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
+    const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
+    const double* __restrict__ p, double alpha, const double* __restrict__ x_in,
+    double* __restrict__ x_out, const unsigned long long* __restrict__ d_in,
+    unsigned long long* d_out, unsigned long long* d_zero, unsigned long long* e_out,
+    unsigned long long* e_zero, uint32_t frozen) {
+  __shared__ double red[kPprThreads / 64];
+  __shared__ double s_dsum[K];
+  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  double acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.0;
+  if (r < N) {
+    const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
+    for (uint32_t k0 = b; k0 < e; k0 += kEdgeBatch) {
+      uint32_t c[kEdgeBatch];
+      float wv[kEdgeBatch];
+#pragma unroll
+      for (int j = 0; j < kEdgeBatch; ++j) {
+        const bool ok = k0 + j < e;
+        c[j] = ok ? in_col[k0 + j] : 0u;
+        wv[j] = ok ? in_w[k0 + j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kEdgeBatch; ++j) {
+        if (k0 + j < e) {
+          const double* xr = x_in + (uint64_t)c[j] * K;
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc[k] += xr[k] * (double)wv[j];
+        }
+      }
+    }
+  }
+  // dangling mass of every vector of x_in (fixed-point slots, exact)
+  for (int k = threadIdx.x >> 6; k < K; k += kPprThreads / 64) {
+    unsigned long long v = d_in[k * kAccSlots + (threadIdx.x & 63)];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_dsum[k] = (double)v * (1.0 / kDScale);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double dacc = 0.0, eacc = 0.0;
+    if (r < N) {
+      const double pr = p[(uint64_t)r * K + k];
+      const double xo = x_in[(uint64_t)r * K + k];
+      const double y = (frozen >> k) & 1u ? xo
+                                           : alpha * (acc[k] + s_dsum[k] * pr) + (1.0 - alpha) * pr;
+      x_out[(uint64_t)r * K + k] = y;
+      if (dangling[r]) dacc = y;
+      eacc = fabs(y - xo);
+    }
+    const double ds = block_sum(dacc, red);
+    const double es = block_sum(eacc, red);
+    if (threadIdx.x == 0) {
+      const int slot = k * kAccSlots + (blockIdx.x & (kAccSlots - 1));
+      atomicAdd(&d_out[slot], __double2ull_rn(ds * kDScale));
+      atomicAdd(&e_out[slot], __double2ull_rn(es * kEScale));
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < K * kAccSlots; i += kPprThreads) {
+      d_zero[i] = 0ull;
+      e_zero[i] = 0ull;
+    }
+}
+
 void free_graph(anomod_graph* g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, g->x[0], g->x[1], g->acc};
+  void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,  g->x[0],
+                g->x[1],   g->acc,    g->bp,   g->bx[0],    g->bx[1], g->bacc};
   for (void* q : ps)
     if (q) (void)hipFree(q);
   delete g;
@@ -332,6 +415,108 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   ANOMOD_HIP(ctx, hipMemcpyAsync(x_out, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
                                  ctx->stream));
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (iters_done) *iters_done = done;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* P, uint32_t K,
+                                double alpha, uint32_t iters, double tol, double* X,
+                                uint32_t* iters_done) {
+  ANOMOD_REQUIRE(nullptr, ctx && g && P && X, "anomod_graph_pagerank_batch: NULL argument");
+  ANOMOD_REQUIRE(ctx, K >= 1 && K <= 16, "K=%u outside [1, 16]", K);
+  ANOMOD_REQUIRE(ctx, alpha > 0.0 && alpha < 1.0, "alpha=%g outside (0, 1)", alpha);
+  ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
+  ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
+  const uint32_t N = g->N;
+  const uint32_t kb = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;  // padded with vector 0
+  // node-major, normalised personalizations
+  std::vector<double> pn((size_t)N * kb);
+  for (uint32_t k = 0; k < kb; ++k) {
+    const double* pk = P + (size_t)(k < K ? k : 0) * N;
+    double s = 0.0;
+    for (uint32_t i = 0; i < N; ++i) {
+      ANOMOD_REQUIRE(ctx, std::isfinite(pk[i]) && pk[i] >= 0.0,
+                     "personalization[%u][%u] invalid", k, i);
+      s += pk[i];
+    }
+    ANOMOD_REQUIRE(ctx, s > 0.0, "personalization %u sums to zero", k);
+    for (uint32_t i = 0; i < N; ++i) pn[(size_t)i * kb + k] = pk[i] / s;
+  }
+  if (int rc = bind(ctx)) return rc;
+  if (g->kb < kb) {
+    for (void* q : {(void*)g->bp, (void*)g->bx[0], (void*)g->bx[1], (void*)g->bacc})
+      if (q) (void)hipFree(q);
+    g->bp = g->bx[0] = g->bx[1] = nullptr;
+    g->bacc = nullptr;
+    g->kb = 0;
+    bool ok = hipMalloc(&g->bp, (size_t)N * kb * 8) == hipSuccess;
+    for (int i = 0; i < 2; ++i) ok = ok && hipMalloc(&g->bx[i], (size_t)N * kb * 8) == hipSuccess;
+    ok = ok && hipMalloc(&g->bacc, 6ull * kb * kAccSlots * 8) == hipSuccess;
+    if (!ok) {
+      set_error(ctx, "hipMalloc failed for a %u-vector PageRank batch", kb);
+      return ANOMOD_ENOMEM;
+    }
+    g->kb = kb;
+    g->host_bacc.assign(6ull * kb * kAccSlots, 0ull);
+  }
+  const int S = kAccSlots * (int)kb;  // one accumulator block = kb x kAccSlots
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bp, pn.data(), pn.size() * 8, hipMemcpyHostToDevice,
+                                 ctx->stream));
+  std::vector<double> x0((size_t)N * kb, 1.0 / N);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bx[0], x0.data(), x0.size() * 8, hipMemcpyHostToDevice,
+                                 ctx->stream));
+  std::fill(g->host_bacc.begin(), g->host_bacc.end(), 0ull);
+  for (uint32_t k = 0; k < kb; ++k)
+    g->host_bacc[k * kAccSlots] =
+        (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bacc, g->host_bacc.data(), g->host_bacc.size() * 8,
+                                 hipMemcpyHostToDevice, ctx->stream));
+  auto launch = [&](uint32_t it, uint32_t frozen) {
+    const int a = it & 1, b = a ^ 1;
+    const int rr = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
+    unsigned long long* A = g->bacc;
+#define ANOMOD_PPR_BATCH(KK)                                                                   \
+  hipLaunchKernelGGL(ppr_batch_iter_kernel<KK>, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream, \
+                     N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->bp, alpha, g->bx[a],      \
+                     g->bx[b], A + rr * S, A + w * S, A + z * S, A + (3 + w) * S,               \
+                     A + (3 + z) * S, frozen)
+    switch (kb) {
+      case 2: ANOMOD_PPR_BATCH(2); break;
+      case 4: ANOMOD_PPR_BATCH(4); break;
+      case 8: ANOMOD_PPR_BATCH(8); break;
+      default: ANOMOD_PPR_BATCH(16); break;
+    }
+#undef ANOMOD_PPR_BATCH
+  };
+  uint32_t done = 0, frozen = 0;
+  const uint32_t all = kb >= 32 ? 0xFFFFFFFFu : ((1u << kb) - 1u);
+  if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  for (uint32_t it = 0; it < iters; ++it) {
+    launch(it, frozen);
+    ANOMOD_HIP(ctx, hipGetLastError());
+    done = it + 1;
+    if (tol > 0.0) {  // per-vector L1 test; converged vectors are carried unchanged
+      const int w = (it + 1) % 3;
+      unsigned long long* eh = g->host_bacc.data() + (3 + w) * S;
+      ANOMOD_HIP(ctx, hipMemcpyAsync(eh, g->bacc + (3 + w) * S, S * 8ull, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      for (uint32_t k = 0; k < kb; ++k) {
+        unsigned long long et = 0;
+        for (int i = 0; i < kAccSlots; ++i) et += eh[k * kAccSlots + i];
+        if (!((frozen >> k) & 1u) && (double)et * (1.0 / kEScale) < (double)N * tol)
+          frozen |= 1u << k;
+      }
+      if ((frozen & all) == all) break;
+    }
+  }
+  if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+  std::vector<double> xs((size_t)N * kb);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(xs.data(), g->bx[done & 1], xs.size() * 8, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (uint32_t k = 0; k < K; ++k)
+    for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;
 }

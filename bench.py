@@ -194,6 +194,20 @@ def main() -> int:
             "bytes_per_launch": bytes_launch,
         },
     }
+    if not args.no_extras:
+        # --- trace structure on the same resident spans:
+        # reads 20 B/span + 8 B/trace, writes 13 B/span + 12 B/trace
+        ctx.trace_structure(spans, download=False)
+        ts_ms = []
+        for _ in range(3):
+            ctx.trace_structure(spans, download=False)
+            ts_ms.append(ctx.stage_ms(L.STAGE_TRACE_STRUCT))
+        t_ms = float(np.mean(ts_ms))
+        ts_bytes = 33 * spans.n_spans + 20 * spans.n_traces
+        result["trace_structure"] = {
+            "spans_per_s": allsum(spans.n_spans / (t_ms * 1e-3)), "kernel_ms": t_ms,
+            "bytes_per_launch": ts_bytes, "achieved_GBps": ts_bytes / (t_ms * 1e-3) / 1e9,
+            "frac": ts_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     spans.free()
 
     if not args.no_extras:
@@ -218,6 +232,18 @@ def main() -> int:
             "bytes_per_iter": ppr_bytes,
             "achieved_GBps": ppr_bytes * args.ppr_iters / (np.mean(pr_ms) * 1e-3) / 1e9,
         }
+        # batched personalizations (one per fault hypothesis)
+        kb = 8
+        Pb = np.random.default_rng(100 + rank).random((kb, g.N))
+        g.pagerank_batch(Pb, iters=args.ppr_iters)
+        bt = []
+        for _ in range(3):
+            g.pagerank_batch(Pb, iters=args.ppr_iters)
+            bt.append(ctx.stage_ms(L.STAGE_PAGERANK))
+        b_ms = float(np.mean(bt))
+        result["pagerank"]["batched"] = {
+            "vectors": kb, "vector_iters_per_s_per_gpu": kb * args.ppr_iters / (b_ms * 1e-3),
+            "iters_per_s_per_gpu": args.ppr_iters / (b_ms * 1e-3)}
         g.free()
         # --- EWMA/z over a [T][S] f32 chunk resident in HBM (config 4 shape)
         ser = anomod.DeviceSeries(ctx, args.ewma_steps, args.ewma_series)

@@ -308,6 +308,15 @@ int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, ui
 int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz);
 int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
                           uint32_t iters, double tol, double* x_out, uint32_t* iters_done);
+/* K (<= 16) personalizations solved together (replica mode, SURVEY.md §8e:
+ * one vector per experiment / fault hypothesis): the CSR is read once per
+ * iteration for all K.  P and X are [K][N]; every column equals its
+ * anomod_graph_pagerank solve bit for bit (same arithmetic and reduction
+ * order).  tol > 0: each vector stops at its own convergence iteration
+ * (later iterations carry it unchanged); iters_done = iterations launched. */
+int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* P, uint32_t K,
+                                double alpha, uint32_t iters, double tol, double* X,
+                                uint32_t* iters_done);
 int anomod_graph_free(anomod_graph* g);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------*/

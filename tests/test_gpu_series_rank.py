@@ -107,6 +107,23 @@ def test_device_graph_replay(ctx):
     g.free()
 
 
+@pytest.mark.parametrize("K", [1, 3, 8, 16])
+def test_pagerank_batch_equals_single_solves(ctx, K):
+    g = anomod.DeviceGraph(ctx, synthetic=(30000, 8, 5))
+    rng = np.random.default_rng(K)
+    P = rng.random((K, g.N))
+    P[:, rng.random(g.N) < 0.5] = 0.0  # sparse personalizations
+    for iters, tol in ((37, 0.0), (500, 1e-10)):
+        X, done = g.pagerank_batch(P, iters=iters, tol=tol)
+        worst = 0
+        for k in range(K):
+            x, it = g.pagerank(P[k], iters=iters, tol=tol)
+            np.testing.assert_array_equal(X[k], x)  # same arithmetic, same order
+            worst = max(worst, it)
+        assert done == worst
+    g.free()
+
+
 def test_features_and_rank_find_injected_fault(ctx):
     fault = "post-storage-service"
     base = anomod.load_experiment(anomod.SynthSpec("SN", seed=21), n_traces=20000)
