@@ -65,7 +65,7 @@ extern "C" {
 
 typedef struct anomod_ctx anomod_ctx;       /* device + stream + comm      */
 typedef struct anomod_spans anomod_spans;   /* device-resident span set    */
-typedef struct anomod_series anomod_series; /* device-resident X[T][S]     */
+typedef struct anomod_series anomod_series; /* device-resident metric matrix */
 typedef struct anomod_graph anomod_graph;   /* device-resident CSR graph   */
 
 /* Span set in struct-of-arrays form, grouped by trace: the spans of trace t
@@ -280,7 +280,11 @@ int anomod_segment_summary(anomod_ctx* ctx, const uint32_t* svc, const uint32_t*
 int anomod_ewma_z(anomod_ctx* ctx, const float* X, uint64_t T, uint64_t S, float alpha,
                   uint32_t W, float eps, float* Z);
 /* Device-resident streaming variant: X stays in HBM, the (m, v, n) state is
- * carried across calls so T can be processed in chunks.                   */
+ * carried across calls so T can be processed in chunks.  upload takes
+ * row-major host X[T][S]; the device copy is laid out for the kernel that
+ * reads it (16-step tiles for the sequential kernel, rows for the
+ * time-parallel one; ANOMOD_EWMA_MODE=1/2/3 forces sequential-tiles /
+ * time-parallel / sequential-rows) — opaque to the caller.                */
 int anomod_series_create(anomod_ctx* ctx, uint64_t T, uint64_t S, anomod_series** out);
 int anomod_series_upload(anomod_ctx* ctx, anomod_series* ser, const float* X);
 int anomod_series_fill_synthetic(anomod_ctx* ctx, anomod_series* ser, uint64_t seed,

@@ -12,8 +12,7 @@ import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
 import os
-for mode, T, S, W in ((1, 7680, 100000, 60), (2, 7680, 100000, 60), (1, 7680, 12500, 60),
-                       (2, 7680, 12500, 60), (0, 7800, 100000, 200)):
+for mode, T, S, W in ((3, 7680, 100000, 60), (1, 7680, 100000, 60), (0, 7680, 100000, 60), (2, 7680, 100000, 60), (1, 7680, 12500, 60), (0, 7680, 12500, 60), (0, 7800, 100000, 200)):
     os.environ["ANOMOD_EWMA_MODE"] = str(mode)
     with anomod.Context(0) as ctx:
         ser = anomod.DeviceSeries(ctx, T, S)

@@ -21,15 +21,16 @@ def test_ewma_matches_pandas_golden(ctx, golden):
                                rtol=Z_RTOL, atol=Z_ATOL)
 
 
-@pytest.fixture(params=[1, 2], ids=["sequential", "time_parallel"])
+@pytest.fixture(params=[1, 2, 3], ids=["sequential_tiles", "time_parallel", "sequential_rows"])
 def ewma_mode(request, monkeypatch):
-    """Run a test under both EWMA kernels (ANOMOD_EWMA_MODE, read per call)."""
+    """Run a test under every EWMA kernel (ANOMOD_EWMA_MODE, read per call)."""
     monkeypatch.setenv("ANOMOD_EWMA_MODE", str(request.param))
     return request.param
 
 
 @pytest.mark.parametrize("T,S,W", [(60, 1, 60), (600, 1000, 60), (4800, 77, 16), (256, 5000, 1),
-                                   (960, 130, 96), (1200, 70, 150)])
+                                   (960, 130, 96), (1200, 70, 150), (1010, 90, 10),
+                                   (7, 3, 7)])
 def test_ewma_matches_oracle(ctx, ewma_mode, T, S, W):
     rng = np.random.default_rng(T + S)
     X = (rng.uniform(0, 1e4, S) + rng.uniform(0.1, 10, S) * rng.standard_normal((T, S)))
@@ -66,9 +67,41 @@ def test_ewma_time_parallel_nan_runs_and_fresh_start(ctx, monkeypatch):
     X[:, 100:110] = np.nan           # never a sample
     X[rng.random((T, S)) < 0.2] = np.nan
     ref = native.ewma_z(X, 2 / 61, W)
-    for mode in ("1", "2"):
+    for mode in ("1", "2", "3"):
         monkeypatch.setenv("ANOMOD_EWMA_MODE", mode)
         np.testing.assert_allclose(ctx.ewma_z(X, 2 / 61, W), ref, rtol=Z_RTOL, atol=Z_ATOL)
+
+
+def test_ewma_layout_changes_between_calls(ctx, monkeypatch):
+    """A series created for one layout (rows for the time-parallel kernel,
+    tiles for the sequential one) and then scored by the other kernel is
+    re-laid out on the device; state carries across the switch."""
+    rng = np.random.default_rng(5)
+    T, S, W = 1000, 150, 50  # T % 16 != 0: a padded last tile
+    X = (300 + 5 * rng.standard_normal((2 * T, S))).astype(np.float32)
+    X[rng.random((2 * T, S)) < 0.05] = np.nan
+    ref = native.ewma_z(X, 0.1, W)
+    for first, second in (("2", "1"), ("1", "3"), ("3", "2")):
+        monkeypatch.setenv("ANOMOD_EWMA_MODE", first)
+        ser = anomod.DeviceSeries(ctx, T, S)
+        ser.upload(X[:T])
+        z1 = ser.ewma_z(0.1, W)
+        monkeypatch.setenv("ANOMOD_EWMA_MODE", second)
+        ser.upload(X[T:])
+        z2 = ser.ewma_z(0.1, W)
+        ser.free()
+        np.testing.assert_allclose(np.concatenate([z1, z2]), ref, rtol=Z_RTOL, atol=Z_ATOL)
+
+
+def test_ewma_synthetic_fill_same_in_both_layouts(ctx, monkeypatch):
+    out = []
+    for mode in ("1", "3"):
+        monkeypatch.setenv("ANOMOD_EWMA_MODE", mode)
+        ser = anomod.DeviceSeries(ctx, 1200, 20000)
+        ser.fill_synthetic(9, t0=4800)
+        out.append(ser.ewma_z(2 / 61, 60))
+        ser.free()
+    np.testing.assert_array_equal(out[0], out[1])
 
 
 def test_pagerank_matches_networkx_golden(ctx, golden):
