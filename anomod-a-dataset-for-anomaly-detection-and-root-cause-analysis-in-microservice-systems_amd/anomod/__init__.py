@@ -19,6 +19,7 @@ from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec,
                      synth_generate_host, synth_services)
 from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
                      load_experiment, rank)
+from . import api
 from .segments import SegmentSet, service_name_of, trace_infos
 from .writers import jaeger_to_csv, write_jaeger_csv, write_metric_long_csv
 from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
@@ -33,7 +34,7 @@ __all__ = [
     "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
     "SegmentSet", "service_name_of", "trace_infos", "analyze_trace_patterns",
     "jaeger_to_csv", "write_jaeger_csv", "write_metric_long_csv", "decode_native",
-    "load_trace_file",
+    "load_trace_file", "api",
 ]
 
 

@@ -27,7 +27,7 @@ OK, EINVAL, EHIP, ERCCL, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
 _STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", ESTATE: "ESTATE"}
 
 (STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK,
- STAGE_TRACE_STRUCT, STAGE_SEGMENTS) = range(7)
+ STAGE_TRACE_STRUCT, STAGE_SEGMENTS, STAGE_SUMMARY) = range(8)
 NO_PARENT = 0xFFFFFFFF
 SPAN_ROOT, SPAN_FIRST = 0x1, 0x2
 
@@ -75,6 +75,29 @@ class TraceStructC(C.Structure):
         ("span_flags", C.POINTER(C.c_uint8)),
         ("n_roots", C.POINTER(C.c_uint32)),
         ("svc_mask", C.POINTER(C.c_uint64)),
+    ]
+
+
+class ValueSummaryC(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint64),
+        ("min", C.c_double),
+        ("max", C.c_double),
+        ("sum", C.c_double),
+        ("median", C.c_double),
+        ("p95", C.c_double),
+        ("p99", C.c_double),
+    ]
+
+
+class ResponseSummaryC(C.Structure):
+    _fields_ = [
+        ("n_status", C.c_uint32),
+        ("n_ctype", C.c_uint32),
+        ("status_counts", C.POINTER(C.c_uint64)),
+        ("ctype_counts", C.POINTER(C.c_uint64)),
+        ("error_count", C.c_uint64),
+        ("latency", ValueSummaryC),
     ]
 
 
@@ -137,6 +160,9 @@ _SIGS = {
     "anomod_edge_aggregate": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(EdgeTableC)]),
     "anomod_trace_structure_spans": (_i32, [_vp, _vp, _P(TraceStructC)]),
     "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),
+    "anomod_value_summary": (_i32, [_vp, _P(C.c_double), _u64, C.c_int, _P(ValueSummaryC)]),
+    "anomod_response_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_uint8), _P(C.c_double),
+                                       _u64, _P(ResponseSummaryC)]),
     "anomod_segment_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_int32), _P(C.c_int64),
                                       _P(C.c_int64), _u64, _P(SegmentSummaryC)]),
     "anomod_decode_jaeger": (_i32, [C.c_char_p, _u64, _P(C.c_char_p), _u32, _P(_vp)]),

@@ -17,7 +17,8 @@ namespace anomod {
 void set_error(anomod_ctx* ctx, const char* fmt, ...);
 
 enum Stage { kStageEdgeAgg = 0, kStageEdgeFinal = 1, kStageEdgeReduce = 2, kStageEwma = 3,
-             kStagePagerank = 4, kStageTraceStruct = 5, kStageSegments = 6, kNumStages = 7 };
+             kStagePagerank = 4, kStageTraceStruct = 5, kStageSegments = 6, kStageSummary = 7,
+             kNumStages = 8 };
 
 }  // namespace anomod
 

@@ -117,7 +117,8 @@ int anomod_ctx_synchronize(anomod_ctx* ctx);
 /* Milliseconds of the last launch of a stage, measured with hipEvents on the
  * ctx stream.  stage: 0 = edge aggregation kernel, 1 = edge finalize kernel,
  * 2 = edge all-reduce, 3 = ewma kernel, 4 = pagerank iterations,
- * 5 = trace-structure kernel, 6 = segment-summary kernel.                 */
+ * 5 = trace-structure kernel, 6 = segment-summary kernel,
+ * 7 = value summary (select + sort + sum + picks).                        */
 int anomod_ctx_stage_ms(const anomod_ctx* ctx, int stage, double* ms);
 
 /* ---- histogram helpers (host) ------------------------------------------- */
@@ -266,6 +267,39 @@ typedef struct {
 int anomod_segment_summary(anomod_ctx* ctx, const uint32_t* svc, const uint32_t* endpoint,
                            const int32_t* is_error, const int64_t* latency,
                            const int64_t* start_time, uint64_t n, anomod_segment_summary_out* out);
+
+/* ---- API-response summary ----------------------------
+ * Latency statistics of monitor_http_responses.py generate_summary
+ * (:150-207) and enhanced_openapi_monitor.py generate_reports (:318-332):
+ * the selected values (positive_only: v > 0, as generate_summary :167-169;
+ * else every non-NaN value, as generate_reports :324) sorted, then
+ *   min = x[0], max = x[c-1], median = x[c//2],
+ *   p95 = x[int(c*0.95)], p99 = x[int(c*0.99)]   (f64 product, truncated)
+ * exactly, and sum over the sorted values (fixed tree order: reproducible,
+ * within c*2^-53 relative of Python's left-to-right sum).  All 0 when c = 0. */
+typedef struct {
+  uint64_t count;             /* out: values selected                      */
+  double min, max, sum;       /* out                                       */
+  double median, p95, p99;    /* out                                       */
+} anomod_value_summary_out;
+int anomod_value_summary(anomod_ctx* ctx, const double* values, uint64_t n, int positive_only,
+                         anomod_value_summary_out* out);
+/* generate_summary's distributions in the same pass: status_id / ctype_id
+ * index the caller's first-appearance lists of status codes and content
+ * types (content_type.split(';')[0], 'unknown' when absent: :163-173),
+ * has_error = the response carries an 'error' key (:176-177); latency is
+ * the value summary of latency_ms > 0.                                       */
+typedef struct {
+  uint32_t n_status;          /* in : status ids are < n_status            */
+  uint32_t n_ctype;           /* in : content-type ids are < n_ctype       */
+  uint64_t* status_counts;    /* [n_status] out                            */
+  uint64_t* ctype_counts;     /* [n_ctype] out                             */
+  uint64_t error_count;       /* out                                       */
+  anomod_value_summary_out latency; /* out                                 */
+} anomod_response_summary_out;
+int anomod_response_summary(anomod_ctx* ctx, const uint32_t* status_id, const uint32_t* ctype_id,
+                            const uint8_t* has_error, const double* latency_ms, uint64_t n,
+                            anomod_response_summary_out* out);
 
 /* ---- windowed EWMA / z-score -------------------------
  * X is time-major [T][S] f32 (NaN = missing sample).  Per series:

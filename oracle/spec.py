@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import math
 from collections import deque
+from datetime import datetime
 
 import numpy as np
 
@@ -116,6 +117,76 @@ def analyze_trace_patterns(traces: list[dict]) -> dict:
 def nearest_rank(values, q_pct: int):
     v = sorted(values)
     return v[len(v) * q_pct // 100]
+
+
+# ---- monitor_http_responses.py:150-207 / enhanced_openapi_monitor.py:318-393
+def latency_picks(values: list, suffix: str = "") -> dict:
+    """min / max / mean / median / p95 / p99 of a sorted copy (:180-190)."""
+    if not values:
+        return {}
+    v = sorted(values)
+    n = len(v)
+    return {"min" + suffix: v[0], "max" + suffix: v[-1], "mean" + suffix: sum(v) / n,
+            "median" + suffix: v[n // 2], "p95" + suffix: v[int(n * 0.95)],
+            "p99" + suffix: v[int(n * 0.99)]}
+
+
+def response_summary(responses: list[dict], start_time, duration, endpoints):
+    """generate_summary's dict (:150-205); None for no responses."""
+    if not responses:
+        return None
+    codes, ctypes_, lat, err = {}, {}, [], 0
+    for r in responses:
+        c = r.get("status_code", 0)
+        codes[c] = codes.get(c, 0) + 1
+        x = r.get("latency_ms", 0)
+        if x > 0:
+            lat.append(x)
+        t = r.get("content_type", "unknown").split(";")[0]
+        ctypes_[t] = ctypes_.get(t, 0) + 1
+        err += "error" in r
+    n = len(responses)
+    return {"collection_info": {"start_time": datetime.fromtimestamp(start_time).isoformat(),
+                                "duration_seconds": duration, "total_responses": n,
+                                "endpoints_monitored": endpoints},
+            "status_code_distribution": codes, "latency_statistics": latency_picks(lat),
+            "content_type_distribution": ctypes_, "error_count": err,
+            "success_rate": (n - err) / n * 100}
+
+
+def response_reports(responses, stats, start_time, duration, endpoints, sample_interval):
+    """generate_reports' three outputs (:318-393): summary dict, CSV text,
+    endpoint-performance dict."""
+    codes = dict(stats["status_codes"])
+    summary = {
+        "collection_info": {"start_time": datetime.fromtimestamp(start_time).isoformat(),
+                            "duration_seconds": duration, "total_responses": len(responses),
+                            "endpoints_monitored": endpoints,
+                            "sample_interval_seconds": sample_interval},
+        "statistics": {"total_requests": stats["total_requests"],
+                       "successful_requests": stats["successful_requests"],
+                       "failed_requests": stats["failed_requests"],
+                       "success_rate_percent": (stats["successful_requests"]
+                                                / max(1, stats["total_requests"])) * 100},
+        "status_code_distribution": codes,
+        "latency_statistics": latency_picks(stats["response_times"], "_ms"),
+        "error_summary": {"total_errors": len(stats["errors"]),
+                          "unique_errors": len(set(stats["errors"])),
+                          "common_errors": list(set(stats["errors"]))}}
+    total = sum(codes.values())
+    csv_text = "status_code,count,percentage\n" + "".join(
+        f"{c},{k},{(k / total * 100) if total > 0 else 0:.2f}\n" for c, k in sorted(codes.items()))
+    perf: dict = {}
+    for r in responses:
+        e = perf.setdefault(r.get("endpoint", "unknown"),
+                            {"count": 0, "avg_latency": 0, "status_codes": {}})
+        e["count"] += 1
+        e["avg_latency"] += r.get("latency_ms", 0)
+        st = r.get("status_code", 0)
+        e["status_codes"][st] = e["status_codes"].get(st, 0) + 1
+    for e in perf.values():
+        e["avg_latency"] /= e["count"]
+    return summary, csv_text, perf
 
 
 # ---- histogram binning (build-defined, include/anomod.h) ------------------

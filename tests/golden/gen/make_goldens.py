@@ -19,6 +19,10 @@ inputs and the outputs the reference computed from them are written.
   percentiles.json
       latency lists -> SN .../api_responses/monitor_http_responses.py
       OpenAPIResponseCollector.generate_summary
+  api_summary.json
+      synthetic monitor responses -> SN .../api_responses/monitor_http_responses.py
+      OpenAPIResponseCollector.generate_summary and enhanced_openapi_monitor.py
+      EnhancedOpenAPIMonitor.generate_reports (the three report files; TZ=UTC)
   metric_long.csv / metric_results.json
       synthetic Prometheus query_range results -> TT_collection-scripts/
       T-Dataset/metric_collector.py MetricCollector.collect_experiment_metrics_csv
@@ -26,7 +30,7 @@ inputs and the outputs the reference computed from them are written.
   ewma_pandas.npz        pandas Series.ewm(alpha, adjust=False) mean/var
   pagerank_networkx.npz  networkx.pagerank (3.4.2, scipy backend)
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py [--only metric]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py [--only metric|api]
 """
 from __future__ import annotations
 
@@ -282,6 +286,93 @@ def percentile_cases(seed=3):
 
 
 # ---------------------------------------------------------------------------
+# API-response monitors (generate_summary / generate_reports)
+# ---------------------------------------------------------------------------
+_EPS = ["/", "/wrk2-api/home-timeline/read", "/wrk2-api/user-timeline/read",
+        "/wrk2-api/post/compose", "/wrk2-api/user/login"]
+_CTYPES = ["application/json", "application/json; charset=utf-8", "text/html; charset=UTF-8",
+           "text/plain", ""]
+
+
+def api_responses(rng, n, int_latency=False):
+    """Responses shaped as monitor_http_responses.py builds them (:62-111):
+    ok responses with a rounded latency, timeouts (408 + 'error') and
+    exceptions (status 0 + 'error'); some without content_type."""
+    out, stats = [], {"total_requests": 0, "successful_requests": 0, "failed_requests": 0,
+                      "status_codes": {}, "response_times": [], "errors": []}
+    for _ in range(n):
+        ep = rng.choice(_EPS)
+        lat = rng.lognormvariate(3.0, 1.2)
+        u = rng.random()
+        if int_latency:
+            lat = rng.randint(0, 2000) if rng.random() < 0.9 else 0
+        if u < 0.06:
+            r = {"endpoint": ep, "status_code": 408, "latency_ms": lat, "content_type": "",
+                 "error": "timeout"}
+            stats["errors"].append("timeout")
+            stats["total_requests"] += 1
+            stats["failed_requests"] += 1
+        elif u < 0.09:
+            r = {"endpoint": ep, "status_code": 0, "latency_ms": lat, "content_type": "",
+                 "error": rng.choice(["Cannot connect", "Server disconnected"])}
+            stats["errors"].append(r["error"])
+            stats["total_requests"] += 1
+            stats["failed_requests"] += 1
+        else:
+            code = rng.choice([200] * 12 + [201, 301, 302, 400, 404, 500, 502, 503])
+            r = {"endpoint": ep, "status_code": code,
+                 "latency_ms": lat if int_latency else round(lat, 2)}
+            if rng.random() < 0.9:
+                r["content_type"] = rng.choice(_CTYPES)
+            stats["total_requests"] += 1
+            stats["status_codes"][code] = stats["status_codes"].get(code, 0) + 1
+            stats["response_times"].append(lat)
+            if 200 <= code < 400:
+                stats["successful_requests"] += 1
+            else:
+                stats["failed_requests"] += 1
+        out.append(r)
+    return out, stats
+
+
+def api_goldens(seed=5):
+    import logging
+    d = REF / "SN_collection-scripts/Dataset/api_responses"
+    sys.path.insert(0, str(d))
+    try:
+        import enhanced_openapi_monitor as eom  # noqa: E402
+        import monitor_http_responses as mhr  # noqa: E402
+    finally:
+        sys.path.pop(0)
+    rng = random.Random(seed)
+    cases = []
+    for n, int_lat in [(1, False), (2, True), (17, False), (64, True), (300, False),
+                       (1000, False)]:
+        responses, stats = api_responses(rng, n, int_lat)
+        info = {"start_time": 1762128000.25 + n, "duration": 60 + n,
+                "endpoints": _EPS[: 1 + n % 5], "sample_interval": 2}
+        ns = types.SimpleNamespace(responses=responses, start_time=info["start_time"],
+                                   duration=info["duration"], endpoints=info["endpoints"])
+        with tempfile.TemporaryDirectory() as td:
+            p = Path(td) / "s.json"
+            mhr.OpenAPIResponseCollector.generate_summary(ns, p)
+            summary = p.read_text()
+        ens = types.SimpleNamespace(
+            responses=responses, stats=copy.deepcopy(stats), start_time=info["start_time"],
+            duration=info["duration"], endpoints=info["endpoints"],
+            sample_interval=info["sample_interval"], logger=logging.getLogger("golden"))
+        with tempfile.TemporaryDirectory() as td:
+            ens.output_dir = Path(td)
+            eom.EnhancedOpenAPIMonitor.generate_reports(ens)
+            reports = {f: (Path(td) / f).read_text() for f in
+                       ("response_summary.json", "status_code_distribution.csv",
+                        "endpoint_performance.json")}
+        cases.append({"responses": responses, "stats": stats, "info": info,
+                      "summary_json": summary, "reports": reports})
+    return cases
+
+
+# ---------------------------------------------------------------------------
 # pandas ewm / networkx pagerank
 # ---------------------------------------------------------------------------
 def ewma_golden(seed=11, T=600, S=6, alpha=2.0 / 61.0):
@@ -401,6 +492,8 @@ def main():
         res = prometheus_results()
         (OUT / "metric_results.json").write_text(json.dumps(res))
         metric_long_golden(res, OUT / "metric_long.csv")
+    if only in (None, "api"):
+        (OUT / "api_summary.json").write_text(json.dumps(api_goldens()))
     if only is not None:
         return
     doc = jaeger_doc()
