@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Time PageRank solves on the bench's config-5 graph (N = 1e5, ~7e5 edges):
+auto / per-iteration launches (ANOMOD_PPR_MODE=1) / cooperative one-launch solve (2)."""
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "anomod-a-dataset-for-anomaly-detection-and-root-cause-analysis-in-microservice-systems_amd"), str(ROOT)]
+import numpy as np  # noqa: E402
+
+import anomod  # noqa: E402
+from anomod import _lib as L  # noqa: E402
+
+with anomod.Context(0) as ctx:
+    g = anomod.DeviceGraph(ctx, synthetic=(100000, 10, 11))
+    p = np.random.default_rng(0).random(g.N)
+    for mode in ("0", "1", "2"):
+        os.environ["ANOMOD_PPR_MODE"] = mode
+        for iters, tol in ((100, 0.0), (1000, 1e-10)):
+            g.pagerank(p, iters=iters, tol=tol)
+            ms, wall, its = [], [], 0
+            for _ in range(5):
+                t = time.perf_counter()
+                _, its = g.pagerank(p, iters=iters, tol=tol)
+                wall.append((time.perf_counter() - t) * 1e3)
+                ms.append(ctx.stage_ms(L.STAGE_PAGERANK))
+            k = float(np.median(ms))
+            print(json.dumps({"mode": mode, "iters": its, "tol": tol, "kernel_ms": k,
+                              "us_per_iter": k * 1e3 / its, "iters_per_s": its / k * 1e3,
+                              "wall_ms": float(np.median(wall))}), flush=True)
+    g.free()

@@ -140,6 +140,23 @@ def test_device_graph_replay(ctx):
     g.free()
 
 
+def test_pagerank_persistent_equals_per_launch(ctx, monkeypatch):
+    """The cooperative one-launch solve (grid barrier per iteration) and the
+    per-iteration launches give the same bits and stop at the same iteration."""
+    g = anomod.DeviceGraph(ctx, synthetic=(100000, 7, 3))
+    p = np.random.default_rng(2).random(g.N)
+    out = {}
+    for mode in ("2", "1"):  # persistent, per-launch
+        monkeypatch.setenv("ANOMOD_PPR_MODE", mode)
+        out[mode] = [g.pagerank(p, iters=it, tol=tol) for it, tol in
+                     ((1, 0.0), (2, 0.0), (100, 0.0), (1000, 1e-10), (1000, 1e-6))]
+    for (xa, ia), (xb, ib) in zip(out["2"], out["1"]):
+        assert ia == ib
+        np.testing.assert_array_equal(xa, xb)
+    assert out["2"][3][1] < 1000 and out["2"][4][1] < out["2"][3][1]
+    g.free()
+
+
 @pytest.mark.parametrize("K", [1, 3, 8, 16])
 def test_pagerank_batch_equals_single_solves(ctx, K):
     g = anomod.DeviceGraph(ctx, synthetic=(30000, 8, 5))
