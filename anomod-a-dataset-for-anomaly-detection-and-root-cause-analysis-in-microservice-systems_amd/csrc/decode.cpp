@@ -23,6 +23,12 @@
 //
 // The parser builds a compact DOM (24 B per JSON value) over the caller's
 // bytes in one pass; strings are unescaped only when they contain escapes.
+// Large documents are decoded element-parallel: a structural scan finds the
+// trace array's elements, the rest of the document is validated on its own,
+// and byte-balanced runs of elements are parsed and decoded on up to 16
+// threads (ANOMOD_DECODE_THREADS), concatenated in file order — the same
+// columns as the one-thread path, which is also the fallback for anything
+// the scan does not recognise.
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -31,6 +37,7 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 #include <algorithm>
 
@@ -192,6 +199,7 @@ struct Dom {
       return true;
     };
     bool expect_key = false;
+    bool after_comma = false;  // a ',' must be followed by a value (no trailing commas)
     skip();
     while (true) {
       skip();
@@ -202,7 +210,10 @@ struct Dom {
       }
       const bool in_obj = !stack.empty() && nodes[stack.back().node].type == J_OBJ;
       char c = s[i];
-      if (c == '}' || c == ']') {
+      const bool closer = c == '}' || c == ']';
+      if (closer && after_comma) break;  // trailing comma
+      after_comma = false;
+      if (closer) {
         if (stack.empty()) break;
         const uint8_t want = c == '}' ? J_OBJ : J_ARR;
         if (nodes[stack.back().node].type != want) break;
@@ -254,6 +265,7 @@ struct Dom {
       skip();
       if (i < n && s[i] == ',') {
         ++i;
+        after_comma = true;
         expect_key = nodes[stack.back().node].type == J_OBJ;
       } else if (i < n && (s[i] == '}' || s[i] == ']')) {
         // handled at the top of the loop
@@ -456,139 +468,368 @@ bool truthy(const Dom& d, uint32_t id) {  // Python bool() of a JSON value
   }
 }
 
-struct Builder {
-  anomod_decoded* out;
-  std::vector<std::string> names;  // per span, until ranks are known
-  void finish(const std::vector<std::string>* fixed) {
-    std::vector<std::string> svc_names;
-    if (fixed) {
-      svc_names = *fixed;
-    } else {
-      svc_names = names;
-      std::sort(svc_names.begin(), svc_names.end());
-      svc_names.erase(std::unique(svc_names.begin(), svc_names.end()), svc_names.end());
-    }
-    std::unordered_map<std::string, uint32_t> rank;
-    for (uint32_t k = 0; k < svc_names.size(); ++k) rank.emplace(svc_names[k], k);
-    out->svc.resize(names.size());
-    for (size_t k = 0; k < names.size(); ++k) {
-      auto it = rank.find(names[k]);
-      out->svc[k] = it == rank.end() ? 0xFFFF : (uint16_t)it->second;
-    }
-    out->services = std::move(svc_names);
+// Per-span service names as ids into a small local dictionary (a thread's or
+// the whole file's), resolved to sorted-name ranks once at the end — no
+// string per span.
+struct Names {
+  std::unordered_map<std::string, uint32_t> index;
+  std::vector<const std::string*> list;  // id -> name (keys of index)
+  std::vector<uint32_t> ids;              // per span
+  void push(std::string&& nm) {
+    auto [it, inserted] = index.try_emplace(std::move(nm), (uint32_t)list.size());
+    if (inserted) list.push_back(&it->first);
+    ids.push_back(it->second);
   }
 };
 
-bool decode_jaeger(const Dom& d, anomod_decoded* out, Builder& B, std::string& err) {
+// Ranks of the names in `parts` (in order, one svc per span) against the
+// sorted distinct names (or the caller's fixed list; 0xFFFF = absent).
+void resolve_names(const std::vector<Names*>& parts, const std::vector<std::string>* fixed,
+                   anomod_decoded* out) {
+  std::vector<std::string> svc_names;
+  if (fixed) {
+    svc_names = *fixed;
+  } else {
+    for (const Names* p : parts)
+      for (const std::string* nm : p->list) svc_names.push_back(*nm);
+    std::sort(svc_names.begin(), svc_names.end());
+    svc_names.erase(std::unique(svc_names.begin(), svc_names.end()), svc_names.end());
+  }
+  std::unordered_map<std::string, uint32_t> rank;
+  for (uint32_t k = 0; k < svc_names.size(); ++k) rank.emplace(svc_names[k], k);
+  size_t ns = 0;
+  for (const Names* p : parts) ns += p->ids.size();
+  out->svc.resize(ns);
+  size_t o = 0;
+  for (const Names* p : parts) {
+    std::vector<uint16_t> lut(p->list.size());
+    for (size_t k = 0; k < p->list.size(); ++k) {
+      auto it = rank.find(*p->list[k]);
+      lut[k] = it == rank.end() ? 0xFFFF : (uint16_t)it->second;
+    }
+    for (uint32_t id : p->ids) out->svc[o++] = lut[id];
+  }
+  out->services = std::move(svc_names);
+}
+
+// One element of the dump's "data" array -> its spans (jaeger_to_csv.py:21-90).
+void jaeger_trace(const Dom& d, uint32_t tr, anomod_decoded* out, Names& names,
+                  std::unordered_map<std::string, std::string>& proc) {
+  const uint64_t th = hash64(py_str(d, d.get(tr, "traceID")));
+  proc.clear();
+  const uint32_t procs = d.get(tr, "processes");
+  if (procs != kNone && d.at(procs).type == J_OBJ) {
+    for (uint32_t k = d.at(procs).first; k != kNone; k = d.at(d.at(k).next).next) {
+      const uint32_t info = d.at(k).next;
+      const uint32_t sn = d.get(info, "serviceName");
+      proc[d.text(k)] = sn == kNone ? std::string() : py_str(d, sn);
+      if (info == kNone) break;
+    }
+  }
+  const uint32_t spans = d.get(tr, "spans");
+  if (spans != kNone && d.at(spans).type == J_ARR) {
+    for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next) {
+      uint64_t parent = 0;
+      const uint32_t refs = d.get(sp, "references");
+      if (refs != kNone && d.at(refs).type == J_ARR) {
+        for (uint32_t r = d.at(refs).first; r != kNone; r = d.at(r).next) {
+          const uint32_t rt = d.get(r, "refType");
+          if (rt != kNone && d.at(rt).type == J_STR && d.text(rt) == "CHILD_OF") {
+            parent = span_id_of(d, d.get(r, "spanID"));
+            break;
+          }
+        }
+      }
+      uint32_t err_tag = kNone, status = kNone;
+      const uint32_t tags = d.get(sp, "tags");
+      if (tags != kNone && d.at(tags).type == J_ARR) {
+        for (uint32_t t = d.at(tags).first; t != kNone; t = d.at(t).next) {
+          const uint32_t key = d.get(t, "key");
+          const std::string ks = key == kNone ? std::string() : py_str(d, key);
+          if (ks == "error") err_tag = d.get(t, "value");
+          else if (ks == "http.status_code") status = d.get(t, "value");
+        }
+      }
+      long double code = 0;
+      const bool error = truthy_error_tag(d, err_tag) || (py_int(d, status, code) && code >= 500);
+      const uint32_t pid = d.get(sp, "processID");
+      auto it = proc.find(pid == kNone ? std::string() : py_str(d, pid));
+      names.push(it == proc.end() ? std::string() : it->second);
+      out->trace_hash.push_back(th);
+      out->span_id.push_back(span_id_of(d, d.get(sp, "spanID")));
+      out->parent.push_back(parent);
+      out->flags.push_back(error ? ANOMOD_FLAG_ERROR : 0);
+      out->dur.push_back(clamp_u32(d, d.get(sp, "duration")));
+    }
+  }
+  out->trace_ptr.push_back(out->span_id.size());
+}
+
+// One element of the payload's "traces" array (trace_collector.py:564-578).
+void skywalking_trace(const Dom& d, uint32_t tr, anomod_decoded* out, Names& names,
+                      std::unordered_map<std::string, uint64_t>& first) {
+  const uint32_t spans = d.get(tr, "spans");
+  if (spans == kNone || d.at(spans).type != J_ARR || d.at(spans).len == 0) return;
+  std::string tid;
+  const uint32_t summ = d.get(tr, "summary");
+  const uint32_t st = d.get(summ, "trace_id");
+  if (st != kNone && truthy(d, st)) tid = py_str(d, st);
+  else {
+    const uint32_t s0 = d.get(d.at(spans).first, "trace_id");
+    if (s0 != kNone && truthy(d, s0)) tid = py_str(d, s0);
+  }
+  const uint64_t th = hash64(tid);
+  first.clear();
+  uint64_t k = 0;
+  for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next, ++k)
+    first.emplace(py_str(d, d.get(sp, "node_id")), k + 1);
+  for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next) {
+    out->trace_hash.push_back(th);
+    out->span_id.push_back(first[py_str(d, d.get(sp, "node_id"))]);
+    const uint32_t pn = d.get(sp, "parent_node_id");
+    uint64_t p = 0;
+    if (pn != kNone && d.at(pn).type != J_NULL) {
+      auto it = first.find(py_str(d, pn));
+      p = it == first.end() ? ~0ull : it->second;
+    }
+    out->parent.push_back(p);
+    const uint32_t sc = d.get(sp, "service_code");
+    names.push(sc != kNone && truthy(d, sc) ? py_str(d, sc) : std::string());
+    long double a = 0, b = 0;
+    const uint32_t sa = d.get(sp, "start_timestamp_ms"), sb = d.get(sp, "end_timestamp_ms");
+    const bool ok = (!truthy(d, sa) || py_int(d, sa, a)) && (!truthy(d, sb) || py_int(d, sb, b));
+    if (!truthy(d, sa)) a = 0;
+    if (!truthy(d, sb)) b = 0;
+    long double us = ok ? (b - a) * 1000.0L : 0;
+    if (us < 0) us = 0;
+    out->dur.push_back(us > 4294967295.0L ? 0xFFFFFFFFu : (uint32_t)us);
+    out->flags.push_back(truthy(d, d.get(sp, "is_error")) ? ANOMOD_FLAG_ERROR : 0);
+  }
+  out->trace_ptr.push_back(out->span_id.size());
+}
+
+constexpr const char* kTopKey[2] = {"data", "traces"};  // Jaeger dump, SkyWalking payload
+
+bool decode_sequential(const Dom& d, int kind, anomod_decoded* out, Names& names,
+                       std::string& err) {
   const uint32_t root = 0;
   if (d.at(root).type != J_OBJ) {
-    err = "Jaeger dump: top level is not an object";
+    err = kind == 0 ? "Jaeger dump: top level is not an object"
+                    : "SkyWalking payload: top level is not an object";
     return false;
   }
-  const uint32_t data = d.get(root, "data");
-  if (data == kNone || d.at(data).type != J_ARR) return true;  // no traces
+  const uint32_t arr = d.get(root, kTopKey[kind]);
+  if (arr == kNone || d.at(arr).type != J_ARR) return true;  // no traces
   std::unordered_map<std::string, std::string> proc;
-  for (uint32_t tr = d.at(data).first; tr != kNone; tr = d.at(tr).next) {
-    const uint64_t th = hash64(py_str(d, d.get(tr, "traceID")));
-    proc.clear();
-    const uint32_t procs = d.get(tr, "processes");
-    if (procs != kNone && d.at(procs).type == J_OBJ) {
-      for (uint32_t k = d.at(procs).first; k != kNone; k = d.at(d.at(k).next).next) {
-        const uint32_t info = d.at(k).next;
-        const uint32_t sn = d.get(info, "serviceName");
-        proc[d.text(k)] = sn == kNone ? std::string() : py_str(d, sn);
-        if (info == kNone) break;
-      }
-    }
-    const uint32_t spans = d.get(tr, "spans");
-    if (spans != kNone && d.at(spans).type == J_ARR) {
-      for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next) {
-        uint64_t parent = 0;
-        const uint32_t refs = d.get(sp, "references");
-        if (refs != kNone && d.at(refs).type == J_ARR) {
-          for (uint32_t r = d.at(refs).first; r != kNone; r = d.at(r).next) {
-            const uint32_t rt = d.get(r, "refType");
-            if (rt != kNone && d.at(rt).type == J_STR && d.text(rt) == "CHILD_OF") {
-              parent = span_id_of(d, d.get(r, "spanID"));
-              break;
-            }
-          }
-        }
-        uint32_t err_tag = kNone, status = kNone;
-        const uint32_t tags = d.get(sp, "tags");
-        if (tags != kNone && d.at(tags).type == J_ARR) {
-          for (uint32_t t = d.at(tags).first; t != kNone; t = d.at(t).next) {
-            const uint32_t key = d.get(t, "key");
-            const std::string ks = key == kNone ? std::string() : py_str(d, key);
-            if (ks == "error") err_tag = d.get(t, "value");
-            else if (ks == "http.status_code") status = d.get(t, "value");
-          }
-        }
-        long double code = 0;
-        const bool error = truthy_error_tag(d, err_tag) || (py_int(d, status, code) && code >= 500);
-        const uint32_t pid = d.get(sp, "processID");
-        auto it = proc.find(pid == kNone ? std::string() : py_str(d, pid));
-        B.names.push_back(it == proc.end() ? std::string() : it->second);
-        out->trace_hash.push_back(th);
-        out->span_id.push_back(span_id_of(d, d.get(sp, "spanID")));
-        out->parent.push_back(parent);
-        out->flags.push_back(error ? ANOMOD_FLAG_ERROR : 0);
-        out->dur.push_back(clamp_u32(d, d.get(sp, "duration")));
-      }
-    }
-    out->trace_ptr.push_back(out->span_id.size());
+  std::unordered_map<std::string, uint64_t> first;
+  for (uint32_t tr = d.at(arr).first; tr != kNone; tr = d.at(tr).next) {
+    if (kind == 0) jaeger_trace(d, tr, out, names, proc);
+    else skywalking_trace(d, tr, out, names, first);
   }
   return true;
 }
 
-bool decode_skywalking_payload(const Dom& d, anomod_decoded* out, Builder& B, std::string& err) {
-  const uint32_t root = 0;
-  if (d.at(root).type != J_OBJ) {
-    err = "SkyWalking payload: top level is not an object";
-    return false;
-  }
-  const uint32_t traces = d.get(root, "traces");
-  if (traces == kNone || d.at(traces).type != J_ARR) return true;
-  std::unordered_map<std::string, uint64_t> first;
-  for (uint32_t tr = d.at(traces).first; tr != kNone; tr = d.at(tr).next) {
-    const uint32_t spans = d.get(tr, "spans");
-    if (spans == kNone || d.at(spans).type != J_ARR || d.at(spans).len == 0) continue;
-    std::string tid;
-    const uint32_t summ = d.get(tr, "summary");
-    const uint32_t st = d.get(summ, "trace_id");
-    if (st != kNone && truthy(d, st)) tid = py_str(d, st);
-    else {
-      const uint32_t s0 = d.get(d.at(spans).first, "trace_id");
-      if (s0 != kNone && truthy(d, s0)) tid = py_str(d, s0);
+// ------------------------------------------------------- parallel decode
+// Structural scan: the byte ranges of the elements of the array that is the
+// value of the LAST top-level member `key` (the one json.load keeps).  Only
+// strings (with escapes) and nesting are tracked; anything unexpected makes
+// it return false and the caller takes the sequential path, whose parser
+// reports the error.
+struct ByteRange {
+  size_t b, e;
+};
+
+bool top_array_elements(const char* s, size_t n, std::string_view key, size_t& open, size_t& close,
+                        std::vector<ByteRange>& elems) {
+  auto ws = [](char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; };
+  size_t i = 0;
+  while (i < n && ws(s[i])) ++i;
+  if (i >= n || s[i] != '{') return false;
+  int depth = 0;
+  bool expect_key = false, found = false, in_target = false, want_value = false;
+  bool key_is_target = false;
+  size_t elem_start = 0;
+  bool elem_open = false;
+  auto end_string = [&](size_t q) -> size_t {  // q just past the opening quote -> closing quote
+    while (true) {
+      const void* hit = std::memchr(s + q, '"', n - q);
+      if (!hit) return n;
+      const size_t c = (size_t)((const char*)hit - s);
+      size_t bs = 0;
+      while (c > bs && s[c - 1 - bs] == '\\') ++bs;
+      if ((bs & 1u) == 0) return c;
+      q = c + 1;
     }
-    const uint64_t th = hash64(tid);
-    first.clear();
-    uint64_t k = 0;
-    for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next, ++k)
-      first.emplace(py_str(d, d.get(sp, "node_id")), k + 1);
-    for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next) {
-      out->trace_hash.push_back(th);
-      out->span_id.push_back(first[py_str(d, d.get(sp, "node_id"))]);
-      const uint32_t pn = d.get(sp, "parent_node_id");
-      uint64_t p = 0;
-      if (pn != kNone && d.at(pn).type != J_NULL) {
-        auto it = first.find(py_str(d, pn));
-        p = it == first.end() ? ~0ull : it->second;
+  };
+  for (; i < n; ++i) {
+    const char c = s[i];
+    if (ws(c)) {
+      // indentation runs: skip 8 spaces at a time
+      while (i + 9 <= n) {
+        uint64_t w;
+        std::memcpy(&w, s + i + 1, 8);
+        if (w != 0x2020202020202020ull) break;
+        i += 8;
       }
-      out->parent.push_back(p);
-      const uint32_t sc = d.get(sp, "service_code");
-      B.names.push_back(sc != kNone && truthy(d, sc) ? py_str(d, sc) : std::string());
-      long double a = 0, b = 0;
-      const uint32_t sa = d.get(sp, "start_timestamp_ms"), sb = d.get(sp, "end_timestamp_ms");
-      const bool ok = (!truthy(d, sa) || py_int(d, sa, a)) && (!truthy(d, sb) || py_int(d, sb, b));
-      if (!truthy(d, sa)) a = 0;
-      if (!truthy(d, sb)) b = 0;
-      long double us = ok ? (b - a) * 1000.0L : 0;
-      if (us < 0) us = 0;
-      out->dur.push_back(us > 4294967295.0L ? 0xFFFFFFFFu : (uint32_t)us);
-      out->flags.push_back(truthy(d, d.get(sp, "is_error")) ? ANOMOD_FLAG_ERROR : 0);
+      continue;
     }
-    out->trace_ptr.push_back(out->span_id.size());
+    if (in_target && depth == 2 && !elem_open && c != ']' && c != ',') {
+      elem_start = i;
+      elem_open = true;
+    }
+    if (c == '"') {
+      const size_t q = end_string(i + 1);
+      if (q >= n) return false;
+      if (depth == 1 && expect_key) {
+        const std::string_view k(s + i + 1, q - i - 1);
+        if (k.find('\\') != std::string_view::npos) return false;  // escaped key: rare, bail
+        key_is_target = k == key;
+        expect_key = false;
+        want_value = true;
+      }
+      i = q;
+      continue;
+    }
+    if (c == ':') continue;
+    if (c == '{' || c == '[') {
+      ++depth;
+      if (depth == 1) {
+        expect_key = true;
+      } else if (depth == 2 && want_value) {
+        want_value = false;
+        if (key_is_target && c == '[') {
+          in_target = true;
+          found = true;
+          open = i;
+          elems.clear();
+          elem_open = false;
+        }
+      }
+      continue;
+    }
+    if (c == '}' || c == ']') {
+      if (in_target && depth == 2) {
+        if (elem_open) {
+          size_t e = i;
+          while (e > elem_start && ws(s[e - 1])) --e;
+          elems.push_back({elem_start, e});
+          elem_open = false;
+        } else if (!elems.empty()) {
+          return false;  // trailing comma
+        }
+        close = i;
+        in_target = false;
+      } else if (in_target && depth == 3) {
+        // closing an element's container: the element continues to the separator
+      }
+      --depth;
+      if (depth < 0) return false;
+      if (depth == 0) {
+        // root closed: only whitespace may follow
+        for (++i; i < n; ++i)
+          if (!ws(s[i])) return false;
+        return found;
+      }
+      continue;
+    }
+    if (c == ',') {
+      if (depth == 1) {
+        expect_key = true;
+        want_value = false;
+      } else if (in_target && depth == 2) {
+        if (!elem_open) return false;  // empty element
+        size_t e = i;
+        while (e > elem_start && ws(s[e - 1])) --e;
+        elems.push_back({elem_start, e});
+        elem_open = false;
+      }
+      continue;
+    }
+    // scalar byte (number / literal)
+    if (depth == 1) want_value = false;
+  }
+  return false;
+}
+
+int decode_threads() {
+  const char* e = getenv("ANOMOD_DECODE_THREADS");
+  if (e && atoi(e) > 0) return atoi(e);
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::min<unsigned>(hc ? hc : 1u, 16u);
+}
+
+// Element-parallel decode: the skeleton (the document with the array
+// emptied) is parsed to validate everything outside the elements; the
+// elements are split into contiguous byte-balanced runs, one per thread, each
+// parsed and decoded independently and concatenated in order.  Returns false
+// when the document is not in that shape or an element fails to parse (the
+// caller then runs the sequential path).
+bool decode_parallel(const char* json, size_t len, int kind, anomod_decoded* out,
+                     std::vector<Names>& names, int threads) {
+  size_t open = 0, close = 0;
+  std::vector<ByteRange> elems;
+  if (!top_array_elements(json, len, kTopKey[kind], open, close, elems)) return false;
+  if (elems.size() < 2 * (size_t)threads) return false;  // not worth it
+  {
+    std::string skel(json, open + 1);
+    skel.append(json + close, len - close);
+    Dom sd;
+    if (!sd.parse(skel.data(), skel.size()) || sd.at(0).type != J_OBJ) return false;
+    const uint32_t arr = sd.get(0, kTopKey[kind]);
+    if (arr == kNone || sd.at(arr).type != J_ARR) return false;
+  }
+  const size_t total = elems.back().e - elems.front().b;
+  std::vector<size_t> cut{0};
+  for (int t = 1; t < threads; ++t) {
+    const size_t target = elems.front().b + total * (size_t)t / (size_t)threads;
+    size_t k = cut.back();
+    while (k < elems.size() && elems[k].b < target) ++k;
+    cut.push_back(k);
+  }
+  cut.push_back(elems.size());
+  std::vector<anomod_decoded> part(threads);
+  names.assign(threads, Names());
+  std::vector<char> ok(threads, 1);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) {
+    pool.emplace_back([&, t] {
+      Dom d;
+      std::unordered_map<std::string, std::string> proc;
+      std::unordered_map<std::string, uint64_t> first;
+      for (size_t k = cut[t]; k < cut[t + 1]; ++k) {
+        if (!d.parse(json + elems[k].b, elems[k].e - elems[k].b)) {
+          ok[t] = 0;
+          return;
+        }
+        if (kind == 0) jaeger_trace(d, 0, &part[t], names[t], proc);
+        else skywalking_trace(d, 0, &part[t], names[t], first);
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  for (int t = 0; t < threads; ++t)
+    if (!ok[t]) return false;
+  size_t ns = 0, nt = 0;
+  for (const auto& p : part) {
+    ns += p.span_id.size();
+    nt += p.trace_ptr.size() - 1;
+  }
+  out->trace_hash.reserve(ns);
+  out->span_id.reserve(ns);
+  out->parent.reserve(ns);
+  out->flags.reserve(ns);
+  out->dur.reserve(ns);
+  out->trace_ptr.reserve(nt + 1);
+  for (int t = 0; t < threads; ++t) {
+    const uint64_t base = out->span_id.size();
+    auto app = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
+    app(out->trace_hash, part[t].trace_hash);
+    app(out->span_id, part[t].span_id);
+    app(out->parent, part[t].parent);
+    app(out->flags, part[t].flags);
+    app(out->dur, part[t].dur);
+    for (size_t k = 1; k < part[t].trace_ptr.size(); ++k)
+      out->trace_ptr.push_back(base + part[t].trace_ptr[k]);
   }
   return true;
 }
@@ -602,25 +843,33 @@ int decode_common(const char* json, uint64_t len, const char* const* services, u
     return ANOMOD_EINVAL;
   }
   *out = nullptr;
-  Dom d;
-  if (!d.parse(json, (size_t)len)) {
-    anomod::set_error(nullptr, "anomod_decode: %s", d.err.c_str());
-    return ANOMOD_EINVAL;
-  }
   auto* res = new anomod_decoded();
-  Builder B{res, {}};
-  std::string err;
-  const bool ok = kind == 0 ? decode_jaeger(d, res, B, err) : decode_skywalking_payload(d, res, B, err);
-  if (!ok) {
-    delete res;
-    anomod::set_error(nullptr, "anomod_decode: %s", err.c_str());
-    return ANOMOD_EINVAL;
+  std::vector<Names> names;
+  const int threads = decode_threads();
+  if (threads <= 1 || len < (64u << 10) ||
+      !decode_parallel(json, (size_t)len, kind, res, names, threads)) {
+    *res = anomod_decoded();
+    names.assign(1, Names());
+    Dom d;
+    if (!d.parse(json, (size_t)len)) {
+      delete res;
+      anomod::set_error(nullptr, "anomod_decode: %s", d.err.c_str());
+      return ANOMOD_EINVAL;
+    }
+    std::string err;
+    if (!decode_sequential(d, kind, res, names[0], err)) {
+      delete res;
+      anomod::set_error(nullptr, "anomod_decode: %s", err.c_str());
+      return ANOMOD_EINVAL;
+    }
   }
   std::vector<std::string> fixed;
   if (services) {
     for (uint32_t k = 0; k < n_services; ++k) fixed.emplace_back(services[k] ? services[k] : "");
   }
-  B.finish(services ? &fixed : nullptr);
+  std::vector<Names*> parts;
+  for (Names& nm : names) parts.push_back(&nm);
+  resolve_names(parts, services ? &fixed : nullptr, res);
   for (uint16_t v : res->svc) {
     if (v == 0xFFFF) {
       delete res;

@@ -111,3 +111,62 @@ def test_load_trace_file_dispatch(golden, tmp_path):
     _same(anomod.load_trace_file(r), decode.decode_skywalking_raw(g["inputs"]))
     _same(anomod.load_trace_file(golden / "jaeger_small.json"),
           decode.decode_jaeger(json.loads((golden / "jaeger_small.json").read_text())))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_parallel_decode_equals_one_thread(seed, monkeypatch):
+    """Element-parallel decode (structural scan + per-thread parse) gives the
+    one-thread columns on large messy dumps and SkyWalking payloads."""
+    doc = _messy_jaeger(random.Random(100 + seed), n_traces=900)
+    text = json.dumps(doc, indent=2 if seed % 2 else None, ensure_ascii=bool(seed % 3)).encode()
+    assert len(text) > 64 << 10
+    out = {}
+    for th in ("1", "3", "8"):
+        monkeypatch.setenv("ANOMOD_DECODE_THREADS", th)
+        out[th] = anomod.decode_native(text, "jaeger")
+    _same(out["3"], out["1"])
+    _same(out["8"], out["1"])
+    _same(out["1"], decode.decode_jaeger(json.loads(text)))
+
+
+def test_parallel_decode_structure_edge_cases(monkeypatch):
+    """Shapes the structural scan must get right (or hand to the one-thread
+    path): a repeated top-level key (json.load keeps the last), keys and
+    strings with escapes / brackets, scalar elements, extra members after the
+    array, invalid separators."""
+    big = _messy_jaeger(random.Random(7), n_traces=400)["data"]
+    first = _messy_jaeger(random.Random(8), n_traces=300)["data"]
+    docs = [
+        '{"data": %s, "total": 0, "errors": null}' % json.dumps(big),
+        '{"x\\"y": "[{", "data": %s, "data": %s}' % (json.dumps(first), json.dumps(big)),
+        '{"meta": {"data": [1, 2]}, "data": %s}' % json.dumps(big),
+        '{"data": [1, "s", null, %s]}' % json.dumps(big)[1:-1],
+        '  {"data": %s}  \n' % json.dumps(big),
+    ]
+    for k, text in enumerate(docs):
+        raw = text.encode()
+        monkeypatch.setenv("ANOMOD_DECODE_THREADS", "1")
+        one = anomod.decode_native(raw, "jaeger")
+        monkeypatch.setenv("ANOMOD_DECODE_THREADS", "8")
+        _same(anomod.decode_native(raw, "jaeger"), one)
+        if k != 3:  # scalar traces: the reference (and the Python twin) raise on .get
+            _same(one, decode.decode_jaeger(json.loads(raw)))
+    bad = ['{"data": [%s, ]}' % json.dumps(big)[1:-1], '{"data": [%s}' % json.dumps(big)[1:-1],
+           '{"data": %s} x' % json.dumps(big), '{"data": [%s,, 1]}' % json.dumps(big)[1:-1]]
+    for text in bad:
+        for th in ("1", "8"):
+            monkeypatch.setenv("ANOMOD_DECODE_THREADS", th)
+            with pytest.raises(anomod.AnomodError):
+                anomod.decode_native(text.encode(), "jaeger")
+
+
+def test_parallel_decode_skywalking(golden, monkeypatch):
+    g = json.loads((golden / "skywalking_small.json").read_text())
+    payload = dict(g["payload"])
+    payload["traces"] = payload["traces"] * 60  # > 64 KiB
+    raw = json.dumps(payload, indent=2).encode()
+    monkeypatch.setenv("ANOMOD_DECODE_THREADS", "1")
+    one = anomod.decode_native(raw, "skywalking")
+    monkeypatch.setenv("ANOMOD_DECODE_THREADS", "6")
+    _same(anomod.decode_native(raw, "skywalking"), one)
+    _same(one, decode.decode_skywalking_payload(payload))
