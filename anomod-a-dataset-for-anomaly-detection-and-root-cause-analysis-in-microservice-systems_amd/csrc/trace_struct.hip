@@ -22,8 +22,9 @@
 //   n_roots     distinct root nodes of the trace (len(root_span_node_ids))
 //   svc_mask    services_involved (:536) as a bit set of service indices
 //
-// GPU form: the chunk walk of the edge kernel (chunk.h) — whole traces in a
-// wave's LDS, ordered scans for the id questions, parent pointer-jumping in
+// GPU form: the chunk walk of the edge kernel (chunk.h) with its software
+// pipeline — whole traces in a wave's LDS, one fused ordered scan (8 ids per
+// step) for the three id questions of a span, parent pointer-jumping in
 // LDS for the depth (<= 8 rounds for a 256-span chunk), per-trace counters in
 // LDS.  A trace longer than 256 spans is resolved by the whole wave against
 // HBM (O(L^2 / 64) compares; rare).
@@ -62,18 +63,38 @@ struct TsOut {
   uint32_t words;                // ceil(S / 64)
 };
 
-// First / last position in [a, b) whose id equals x (-1 when none).  The
-// scan covers the whole range (the last match is wanted too).
-__device__ __forceinline__ void first_last(const uint64_t* lsid, uint32_t a, uint32_t b,
-                                           uint64_t x, int& f, int& l) {
-  f = -1;
-  l = -1;
-  for (uint32_t q = a; q < b; ++q) {
-    if (lsid[q] == x) {
-      if (f < 0) f = (int)q;
-      l = (int)q;
+// One ordered pass over [a, b), 8 ids per step (4 x ds_read_b128 from a
+// 16-B aligned start), answering the three per-span id questions together:
+// f / l = first / last position whose id equals x (the span's own id: the
+// whole range is scanned for l), pf = first position whose id equals y (the
+// span's parent reference; -1 when y == 0).  -1 when none.
+__device__ __forceinline__ void scan_ids(const uint64_t* lsid, uint32_t a, uint32_t b, uint64_t x,
+                                         uint64_t y, int& f, int& l, int& pf) {
+  f = l = pf = -1;
+  for (uint32_t q0 = a & ~3u; q0 < b; q0 += 8) {
+    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
+    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
+    const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 4);
+    const ulonglong2 v3 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 6);
+    const uint64_t v[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+    uint32_t mx = 0, my = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mx |= (v[j] == x ? 1u : 0u) << j;
+      my |= (v[j] == y ? 1u : 0u) << j;
     }
+    const uint32_t lo = a > q0 ? a - q0 : 0u;           // < 4
+    const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;  // >= 1
+    const uint32_t rm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    mx &= rm;
+    my &= rm;
+    if (mx) {
+      if (f < 0) f = (int)(q0 + __ffs(mx) - 1u);
+      l = (int)(q0 + 31u - __clz(mx));
+    }
+    if (my && pf < 0) pf = (int)(q0 + __ffs(my) - 1u);
   }
+  if (y == 0ull) pf = -1;
 }
 
 // First position in [a, b) whose id equals x (-1 when none or x == 0).
@@ -116,9 +137,8 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
     if (i < c.n) {
       uint32_t b;
       trace_bounds(Sm, r, lane, c.n, a[r], b);
-      int l;
-      first_last(lsid, a[r], b, sid[r], f[r], l);
-      const int pf = first_of(lsid, a[r], b, pid[r]);  // own parent: child lists
+      int l, pf;  // pf: own parent (child lists)
+      scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
       np[r] = (l == (int)i) ? pf : first_of(lsid, a[r], b, lpid[l]);  // node parent
       if (pf >= 0) atomicAdd(&lcnt[pf], 1u);
     }
@@ -279,21 +299,16 @@ __global__ __launch_bounds__(kTsThreads) void trace_struct_kernel(
   const uint64_t gw = (uint64_t)blockIdx.x * kTsWaves + wid;
   const uint64_t nw = (uint64_t)gridDim.x * kTsWaves;
   const uint64_t t_end = uniform64(n_traces * (gw + 1) / nw);
-  uint64_t t = uniform64(n_traces * gw / nw);
-  while (t < t_end) {
-    uint64_t lo, hi;
-    load_bounds(trace_ptr, t, t_end, lane, lo, hi);
-    const Chunk c = make_chunk(t, t_end, lane, lo, hi);
-    if (c.k == 0) {
-      ts_big(lane, c.base, c.base + c.n, t, span_id, parent, svcfl, o);
-      t += 1;
-      continue;
-    }
-    const auto rsid = rsrc(span_id + c.base, c.n * 8u);
-    const auto rpid = rsrc(parent + c.base, c.n * 8u);
-    const auto rsf = rsrc(svcfl + c.base, c.n * 4u);
-    uint64_t sid[kPer], pid[kPer];
-    uint32_t svc[kPer];
+  const uint64_t t_begin = uniform64(n_traces * gw / nw);
+  if (t_begin >= t_end) return;
+  // Software pipeline (as the edge kernel): the bounds of chunk c+2 and the
+  // span columns of chunk c+1 are in flight while chunk c is resolved.
+  auto load_cols = [&](const Chunk& c, uint64_t (&sid)[kPer], uint64_t (&pid)[kPer],
+                       uint32_t (&svc)[kPer]) {
+    const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by ts_big()
+    const auto rsid = rsrc(span_id + c.base, n * 8u);
+    const auto rpid = rsrc(parent + c.base, n * 8u);
+    const auto rsf = rsrc(svcfl + c.base, n * 4u);
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const uint32_t i = (uint32_t)lane + (uint32_t)(r * kWave);
@@ -301,8 +316,39 @@ __global__ __launch_bounds__(kTsThreads) void trace_struct_kernel(
       pid[r] = bload64(rpid, i * 8u);
       svc[r] = bload32(rsf, i * 4u) & 0xFFFFu;
     }
-    ts_chunk(wsm, lane, c, t, sid, pid, svc, o);
-    t += c.k;
+  };
+  uint64_t lo, hi;
+  load_bounds(trace_ptr, t_begin, t_end, lane, lo, hi);
+  Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi);
+  uint64_t t_cur = t_begin;
+  uint64_t sid[kPer], pid[kPer];
+  uint32_t svc[kPer];
+  load_cols(cur, sid, pid, svc);
+  uint64_t t_next = t_begin + (cur.k ? cur.k : 1u);
+  load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
+  while (true) {
+    const bool has_next = t_next < t_end;
+    Chunk nxt{};
+    uint64_t sid_n[kPer], pid_n[kPer];
+    uint32_t svc_n[kPer];
+    const uint64_t t_nxt = t_next;
+    if (has_next) {
+      nxt = make_chunk(t_next, t_end, lane, lo, hi);
+      load_cols(nxt, sid_n, pid_n, svc_n);
+      t_next += nxt.k ? nxt.k : 1u;
+      load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
+    }
+    if (cur.k == 0) ts_big(lane, cur.base, cur.base + cur.n, t_cur, span_id, parent, svcfl, o);
+    else ts_chunk(wsm, lane, cur, t_cur, sid, pid, svc, o);
+    if (!has_next) break;
+    cur = nxt;
+    t_cur = t_nxt;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      sid[r] = sid_n[r];
+      pid[r] = pid_n[r];
+      svc[r] = svc_n[r];
+    }
   }
 }
 
