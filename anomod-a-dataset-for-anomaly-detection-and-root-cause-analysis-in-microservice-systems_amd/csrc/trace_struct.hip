@@ -12,9 +12,13 @@
 //               whose id equals the parent reference of the LAST span with
 //               this node's id; ANOMOD_NO_PARENT when that reference is 0 or
 //               names no span of the trace (:427-437)
-//   depth       distance from the node's root along those parents (the BFS
-//               of :441-449); 0 when the chain never reaches a root (a parent
-//               cycle: unreachable from the roots, :477 default)
+//   depth       the BFS of :441-449 over the child lists: it enqueues a node
+//               once per child-list entry and keeps the LAST (= deepest)
+//               visit, i.e. the longest path from a root along the edges
+//               "first span of my own parent reference -> my node".  0 when
+//               no root reaches the node (:477 default) or when a cycle the
+//               BFS reaches feeds it (the reference never terminates there).
+//               Without duplicated ids this is the walk up the node parents.
 //   n_children  spans whose own parent reference names this node (:438-439),
 //               shared by every span carrying the node's id (:476)
 //   span_flags  ANOMOD_SPAN_ROOT (node parent not in the trace, :443) |
@@ -25,9 +29,12 @@
 // GPU form: the chunk walk of the edge kernel (chunk.h) with its software
 // pipeline — whole traces in a wave's LDS, one fused ordered scan (8 ids per
 // step) for the three id questions of a span, parent pointer-jumping in
-// LDS for the depth (<= 8 rounds for a 256-span chunk), per-trace counters in
-// LDS.  A trace longer than 256 spans is resolved by the whole wave against
-// HBM (O(L^2 / 64) compares; rare).
+// LDS for the depth (<= 8 rounds for a 256-span chunk) when the chunk has no
+// duplicated id, else longest-path relaxation in LDS (rounds until nothing
+// changes, bounded by 2L + 2 so a reached cycle is recognised by its depth
+// outgrowing L); per-trace counters in LDS.  A trace longer than 256 spans is
+// resolved by the whole wave against HBM (O(L^2 / 64) compares plus
+// relaxation rounds over a scratch edge list; rare).
 #include "chunk.h"
 #include "common.h"
 
@@ -46,7 +53,8 @@ constexpr int kTPid = kTSid + (kStage + 8) * 8;   // u64 parent refs [kStage + 8
 constexpr int kTNxt = kTPid + (kStage + 8) * 8;   // u32 jump target | kDone [kStage]
 constexpr int kTDst = kTNxt + kStage * 4;         // u32 distance to the target [kStage]
 constexpr int kTCnt = kTDst + kStage * 4;         // u32 child counts [kStage]
-constexpr int kTSvc = kTCnt + kStage * 4;         // u16 services [kStage]
+constexpr int kTPfl = kTCnt + kStage * 4;         // u32 (own parent pos + 1) | trace len << 16
+constexpr int kTSvc = kTPfl + kStage * 4;         // u16 services [kStage]
 constexpr int kTRf = kTSvc + kStage * 2;          // u8 root-node flag of first spans [kStage]
 constexpr int kTFlag = kTRf + kStage;             // u8 trace-start flags [kStage]
 constexpr int kTBytes = kTFlag + kStage;
@@ -61,6 +69,8 @@ struct TsOut {
   uint32_t* n_roots;
   unsigned long long* svc_mask;  // [n_traces * words]
   uint32_t words;                // ceil(S / 64)
+  int* scr_f;                    // big traces only: node (first span) of each span
+  int* scr_pf;                   // big traces only: first span of its own parent ref
 };
 
 // One ordered pass over [a, b), 8 ids per step (4 x ds_read_b128 from a
@@ -113,6 +123,7 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
   auto* lnxt = reinterpret_cast<uint32_t*>(wsm + kTNxt);
   auto* ldst = reinterpret_cast<uint32_t*>(wsm + kTDst);
   auto* lcnt = reinterpret_cast<uint32_t*>(wsm + kTCnt);
+  auto* lpfl = reinterpret_cast<uint32_t*>(wsm + kTPfl);
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kTSvc);
   auto* lrf = reinterpret_cast<uint8_t*>(wsm + kTRf);
   auto* lflag = reinterpret_cast<uint8_t*>(wsm + kTFlag);
@@ -129,11 +140,13 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
 
   int f[kPer], np[kPer];
   uint32_t a[kPer], nxt[kPer], dst[kPer];
+  bool dup = false;
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
     f[r] = np[r] = -1;
     a[r] = 0;
+    uint32_t pfl = 0;
     if (i < c.n) {
       uint32_t b;
       trace_bounds(Sm, r, lane, c.n, a[r], b);
@@ -141,7 +154,10 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
       scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
       np[r] = (l == (int)i) ? pf : first_of(lsid, a[r], b, lpid[l]);  // node parent
       if (pf >= 0) atomicAdd(&lcnt[pf], 1u);
+      dup |= f[r] != (int)i;
+      pfl = (uint32_t)(pf + 1) | (b - a[r]) << 16;
     }
+    lpfl[i] = pfl;
     lrf[i] = (uint8_t)(i < c.n && np[r] < 0 && f[r] == (int)i);
     nxt[r] = np[r] >= 0 ? (uint32_t)np[r] : (i | kDone);
     dst[r] = np[r] >= 0 ? 1u : 0u;
@@ -149,6 +165,41 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
     ldst[i] = dst[r];
   }
   wave_sync();
+  if (__ballot(dup) != 0ull) {
+    // Duplicated ids: a node may have several parents (one per span carrying
+    // its id), and the BFS keeps its deepest visit.  Longest-path relaxation
+    // of the edges pf -> f over the node depths in LDS (reusing the jump
+    // array), from the roots (depth 0); -1 = not reached.
+    auto* ld = reinterpret_cast<int*>(lnxt);
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const uint32_t i = lane + r * kWave;
+      ld[i] = lrf[i] ? 0 : -1;
+    }
+    wave_sync();
+    for (uint32_t round = 0; round < 2u * c.n + 2u; ++round) {
+      bool changed = false;
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        const int pf = (int)(lpfl[lane + r * kWave] & 0xFFFFu) - 1;
+        if (pf >= 0) {
+          const int dp = ld[pf];
+          if (dp >= 0 && dp + 1 > ld[f[r]]) {
+            atomicMax(&ld[f[r]], dp + 1);
+            changed = true;
+          }
+        }
+      }
+      wave_sync();
+      if (__ballot(changed) == 0ull) break;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int d = f[r] >= 0 ? ld[f[r]] : -1;
+      nxt[r] = kDone;  // the output below reads dst as the depth
+      dst[r] = (d >= 0 && d < (int)(lpfl[lane + r * kWave] >> 16)) ? (uint32_t)d : 0u;
+    }
+  }
   // Pointer jumping: after round k every span points 2^k ancestors up (or at
   // its root, flagged kDone) and knows the distance; 8 rounds cover 256.
   for (int round = 0; round < 8; ++round) {
@@ -233,7 +284,9 @@ __device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
   };
   uint32_t roots = 0;
   unsigned long long mask = 0;
-  // pass 1: node parents, flags, child counts (atomics on n_children)
+  int* D = reinterpret_cast<int*>(o.depth + lo);  // node depths during relaxation
+  // pass 1: node parents, flags, child counts (atomics on n_children), the
+  // edge list (own node, own parent's node) and the root depths
   for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
     const uint32_t i = i0 + lane;
     if (i < L) {
@@ -246,6 +299,9 @@ __device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
       o.flags[lo + i] = (uint8_t)((np < 0 ? ANOMOD_SPAN_ROOT : 0u) |
                                     (f == (int)i ? ANOMOD_SPAN_FIRST : 0u));
       if (np < 0 && f == (int)i) ++roots;
+      D[i] = (np < 0 && f == (int)i) ? 0 : -1;
+      o.scr_f[lo + i] = f;
+      o.scr_pf[lo + i] = pf;
       const uint32_t sv = svcfl[lo + i] & 0xFFFFu;
       if (o.words == 1u) mask |= 1ull << sv;
       else
@@ -254,26 +310,48 @@ __device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
   __builtin_amdgcn_wave_barrier();
-  // pass 2: depth by walking the node parents (<= L steps: longer = cycle);
-  // a duplicate id takes its first span's child count
+  // pass 2: longest-path relaxation of the edges pf -> f (the BFS keeps a
+  // node's deepest visit); a reached cycle keeps growing past L
+  for (uint32_t round = 0; round < 2u * L + 2u; ++round) {
+    bool changed = false;
+    for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      if (i < L) {
+        const int pf = o.scr_pf[lo + i];
+        if (pf >= 0) {
+          const int f = o.scr_f[lo + i];
+          const int dp = __hip_atomic_load(&D[pf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (dp >= 0 &&
+              dp + 1 > __hip_atomic_load(&D[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            atomicMax(&D[f], dp + 1);
+            changed = true;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (__ballot(changed) == 0ull) break;
+  }
+  // pass 3: each span's depth (its node's, staged in scr_pf: D is read
+  // until every lane is done) and a duplicate id's child count (its first
+  // span's)
   for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
     const uint32_t i = i0 + lane;
     if (i < L) {
-      uint32_t j = i, d = 0;
-      while (d <= L) {
-        const uint32_t p = __hip_atomic_load(&o.parent_pos[lo + j], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        if (p == ANOMOD_NO_PARENT) break;
-        j = p;
-        ++d;
-      }
-      o.depth[lo + i] = d <= L ? d : 0u;
-      int f, l;
-      first_last_g(span_id[lo + i], f, l);
+      const int f = o.scr_f[lo + i];
+      const int d = __hip_atomic_load(&D[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      o.scr_pf[lo + i] = (d >= 0 && d < (int)L) ? d : 0;
       if (f != (int)i)
         o.n_children[lo + i] = __hip_atomic_load(&o.n_children[lo + f], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    if (i < L) o.depth[lo + i] = (uint32_t)o.scr_pf[lo + i];
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
   __builtin_amdgcn_wave_barrier();
@@ -288,7 +366,7 @@ __device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
   }
 }
 
-__global__ __launch_bounds__(kTsThreads) void trace_struct_kernel(
+__global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4))) void trace_struct_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint64_t* __restrict__ trace_ptr, uint64_t n_traces,
     TsOut o) {
@@ -375,7 +453,9 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   const size_t off_depth = n * 4, off_cnt = 2 * n * 4, off_flags = 3 * n * 4;
   const size_t off_roots = (off_flags + n + 7) & ~(size_t)7;
   const size_t off_mask = (off_roots + nt * 4 + 7) & ~(size_t)7;
-  const size_t bytes = off_mask + nt * words * 8 + 8;
+  // + scratch for traces longer than a chunk: (own node, parent's node) per span
+  const size_t off_scr = (off_mask + nt * words * 8 + 15) & ~(size_t)15;
+  const size_t bytes = off_scr + n * 8 + 8;
   char* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) {
     set_error(ctx, "hipMalloc(%zu) for trace-structure outputs failed", bytes);
@@ -397,6 +477,8 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   o.n_roots = reinterpret_cast<uint32_t*>(d + off_roots);
   o.svc_mask = reinterpret_cast<unsigned long long*>(d + off_mask);
   o.words = words;
+  o.scr_f = reinterpret_cast<int*>(d + off_scr);
+  o.scr_pf = reinterpret_cast<int*>(d + off_scr + n * 4);
   if (int rc = stage_begin(ctx, kStageTraceStruct)) {
     (void)hipFree(d);
     return rc;

@@ -216,8 +216,11 @@ int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t 
  *               id equals the parent reference of the LAST span carrying the
  *               node's id), ANOMOD_NO_PARENT when the reference is 0 or names
  *               no span of the trace (:427-437, :443)
- *   depth       distance from the node's root along those parents (the BFS of
- *               :441-449); 0 when no root reaches the node (parent cycle, :477)
+ *   depth       the BFS of :441-449: the node's deepest visit from the roots,
+ *               i.e. the longest path along "node of a span's own parent
+ *               reference -> the span's node" (with unique ids: the distance
+ *               along the parents); 0 when no root reaches the node (:477) or
+ *               a cycle the BFS reaches feeds it (the reference never ends)
  *   n_children  spans whose own parent reference names the node (:438-439)
  *   span_flags  ANOMOD_SPAN_ROOT | ANOMOD_SPAN_FIRST (first span with its id)
  *   n_roots     distinct root nodes of the trace (len(root_span_node_ids))

@@ -197,7 +197,8 @@ uint32_t oracle_pagerank(const uint32_t* row_ptr, const uint32_t* col, const flo
  *                   every such span counts as a child of that node (:438-439)
  *   node parent   : own parent of last(i) — parents[node_id] keeps the last
  *                   span's value (:437)
- *   depth         : walk node parents to a root; > L steps = cycle -> 0 (:477)
+ *   depth         : BFS deepest visit = longest path from a root (:441-449);
+ *                   unreached or fed by a reached cycle -> 0 (:477)
  *   roots         : first spans whose node parent is missing (:443)
  * parent_pos is trace-local; 0xFFFFFFFF = no parent.  n_children, svc_mask
  * must be zeroed by the caller. */
@@ -215,6 +216,9 @@ void oracle_trace_structure(const uint64_t* span_id, const uint64_t* parent, con
   for (uint64_t t = t0; t < t1; ++t) {
     const uint64_t a = trace_ptr[t], b = trace_ptr[t + 1], L = b - a;
     uint32_t roots = 0;
+    long* F = (long*)malloc((L ? L : 1) * sizeof(long));   /* node: first span with the id */
+    long* PF = (long*)malloc((L ? L : 1) * sizeof(long));  /* own parent reference resolved */
+    long* D = (long*)malloc((L ? L : 1) * sizeof(long));   /* node depth, -1 = not reached */
     for (uint64_t i = a; i < b; ++i) {
       long f = -1, l = -1;
       for (uint64_t q = a; q < b; ++q)
@@ -229,19 +233,40 @@ void oracle_trace_structure(const uint64_t* span_id, const uint64_t* parent, con
       flags[i] = (uint8_t)((np < 0 ? 1u : 0u) | (f == (long)(i - a) ? 2u : 0u));
       if (np < 0 && f == (long)(i - a)) ++roots;
       svc_mask[t * words + (svc[i] >> 6)] |= 1ull << (svc[i] & 63u);
+      F[i - a] = f;
+      PF[i - a] = pf;
+      D[i - a] = -1;
+    }
+    /* Depth (trace_collector.py:441-449): the BFS from the roots enqueues a
+       node once per child-list entry — one per span whose own parent
+       reference resolves (:438-439) — and keeps its LAST visit, the deepest:
+       the longest path from a root (a node whose last span's parent does not
+       resolve) along those edges.  Relaxed to the fixpoint; a node still
+       growing after 2L + 2 rounds sits on or after a cycle the BFS reaches
+       (the reference never terminates there) and, like unreachable nodes,
+       gets 0.  Without duplicate ids this is the walk up the parent chain. */
+    for (uint64_t k = 0; k < L; ++k)
+      if (F[k] == (long)k && (flags[a + k] & 1u)) D[k] = 0;
+    for (uint64_t round = 0; round < 2 * L + 2; ++round) {
+      int changed = 0;
+      for (uint64_t k = 0; k < L; ++k) {
+        if (PF[k] < 0 || D[PF[k]] < 0) continue;
+        if (D[PF[k]] + 1 > D[F[k]]) {
+          D[F[k]] = D[PF[k]] + 1;
+          changed = 1;
+        }
+      }
+      if (!changed) break;
     }
     for (uint64_t i = a; i < b; ++i) {
-      long f = -1;
-      for (uint64_t q = a; q < b && f < 0; ++q)
-        if (span_id[q] == span_id[i]) f = (long)(q - a);
+      const long f = F[i - a];
       if (f != (long)(i - a)) n_children[i] = n_children[a + f];
-      uint64_t j = i - a, d = 0;
-      while (d <= L && parent_pos[a + j] != 0xFFFFFFFFu) {
-        j = parent_pos[a + j];
-        ++d;
-      }
-      depth[i] = d <= L ? (uint32_t)d : 0u;
+      const long d = D[f];
+      depth[i] = (d >= 0 && d < (long)L) ? (uint32_t)d : 0u;
     }
+    free(F);
+    free(PF);
+    free(D);
     n_roots[t] = roots;
   }
 }

@@ -13,6 +13,10 @@ inputs and the outputs the reference computed from them are written.
       synthetic raw GraphQL span lists -> TT_collection-scripts/T-Dataset/
       trace_collector.py SkyWalkingTraceCollector._build_span_records
       (+ SpanRecord.to_dict, and a collector payload built from them)
+  skywalking_dups.json
+      raw GraphQL span lists whose duplicated node ids carry different parents
+      (acyclic: a duplicate's parent was created before the node) ->
+      _build_span_records; its BFS keeps the deepest visit of a node
   analyze_patterns.json
       synthetic ES segment hits -> enhanced_trace_collector.py
       extract_trace_info + analyze_trace_patterns
@@ -30,7 +34,7 @@ inputs and the outputs the reference computed from them are written.
   ewma_pandas.npz        pandas Series.ewm(alpha, adjust=False) mean/var
   pagerank_networkx.npz  networkx.pagerank (3.4.2, scipy backend)
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py [--only metric|api]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen/make_goldens.py [--only metric|api|swdup]
 """
 from __future__ import annotations
 
@@ -188,6 +192,47 @@ def sw_traces(seed: int = 7, n_traces: int = 40) -> list[list[dict]]:
         if t == 8 and spans:
             spans[0]["parentSpanId"] = None
         rng.shuffle(spans)  # GraphQL order is not tree order
+        out.append(spans)
+    return out
+
+
+def sw_dup_traces(seed=13, n=60):
+    """Traces where node ids repeat with different parents (the depth is the
+    BFS's last = deepest visit).  Node k's parent and every duplicate's
+    parent are drawn from nodes created before node k, so no cycle is
+    reachable (the reference's BFS would not terminate)."""
+    rng = random.Random(seed)
+    out = []
+    for t in range(n):
+        tid = f"dup{t}"
+        nodes = []  # (segment, span) in creation order
+        spans = []
+        big = t in (7, 31)
+        n_nodes = rng.randint(200, 240) if big else rng.randint(2, 24)  # big: > 256 spans
+        for k in range(n_nodes):
+            seg = f"s{k // 3}"
+            node = (seg, k % 3)
+            parent = rng.randrange(k) if k and rng.random() < 0.95 else None
+            nodes.append(node)
+            copies = 1 + (rng.random() < 0.3) + (rng.random() < 0.1)
+            for c in range(copies):
+                p = parent if c == 0 else (rng.randrange(k) if k and rng.random() < 0.85 else None)
+                if p is None:
+                    ps, refs = -1, []
+                elif nodes[p][0] == seg:
+                    ps, refs = nodes[p][1], []
+                else:
+                    ps = -1
+                    refs = [{"traceId": tid, "parentSegmentId": nodes[p][0],
+                             "parentSpanId": nodes[p][1], "type": "CROSS_PROCESS"}]
+                spans.append({"traceId": tid, "segmentId": seg, "spanId": node[1],
+                              "parentSpanId": ps, "serviceCode": f"ts-s{rng.randint(0, 5)}-service",
+                              "serviceInstanceName": "pod", "startTime": 1762180000000 + k,
+                              "endTime": 1762180000000 + k + rng.randint(0, 50),
+                              "endpointName": "/x", "type": "Local", "peer": "", "component": "x",
+                              "isError": False, "layer": "Http", "tags": [], "logs": [],
+                              "refs": refs})
+        rng.shuffle(spans)
         out.append(spans)
     return out
 
@@ -494,6 +539,10 @@ def main():
         metric_long_golden(res, OUT / "metric_long.csv")
     if only in (None, "api"):
         (OUT / "api_summary.json").write_text(json.dumps(api_goldens()))
+    if only in (None, "swdup"):
+        dups = sw_dup_traces()
+        dexp, _ = sw_expected(dups)
+        (OUT / "skywalking_dups.json").write_text(json.dumps({"inputs": dups, "expected": dexp}))
     if only is not None:
         return
     doc = jaeger_doc()
