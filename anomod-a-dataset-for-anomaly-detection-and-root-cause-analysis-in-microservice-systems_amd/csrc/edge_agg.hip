@@ -28,9 +28,9 @@
 //    with ds_cmpst inserts measured 1.7x slower, and scanning a lane's 4
 //    slots in lockstep 1.1-1.4x slower: register pressure);
 //  * the E x 896 histogram does not fit LDS, so each workgroup privatises it
-//    in an 8 Ki-slot LDS hash table of packed (count << 32 | key) words
-//    (first probes of a lane's 4 spans issued together), flushed once with
-//    u64 atomics;
+//    in an 8 Ki-slot LDS hash table (2048 buckets x 4 u32 keys, one
+//    ds_read_b128 per lookup; u32 counts in a parallel array), flushed once
+//    with u64 atomics;
 //  * per-edge error/sum/min/max live in LDS (E <= 512) and are flushed once;
 //  * all merges are integer adds / min / max: results are bit-exact and
 //    independent of geometry, scheduling and shard count.
@@ -49,10 +49,13 @@ using namespace chunk;
 #endif
 constexpr int kWavesPerWG = ANOMOD_WAVES;
 constexpr int kThreads = kWave * kWavesPerWG;
-constexpr int kHtLog2 = 13;
-constexpr uint32_t kHtSlots = 1u << kHtLog2;
+constexpr int kHtBucketLog2 = 11;  // 2048 buckets of 4 slots
+constexpr uint32_t kHtSlots = 4u << kHtBucketLog2;
 constexpr int kMaxProbe = 48;
-constexpr uint32_t kLdsEdges = 512;
+#ifndef ANOMOD_LDS_EDGES
+#define ANOMOD_LDS_EDGES 512
+#endif
+constexpr uint32_t kLdsEdges = ANOMOD_LDS_EDGES;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
 // 2 = no histogram, 4 = no parent lookup, 16 = stream the columns only.
@@ -61,12 +64,16 @@ constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 #endif
 
 // LDS carve (bytes, every offset a multiple of 16).
-constexpr int kOffHt = 0;                                // u64 slots (count<<32 | key)
-constexpr int kOffSum = kOffHt + (int)kHtSlots * 8;
-constexpr int kOffErr = kOffSum + (int)kLdsEdges * 8;
-constexpr int kOffMin = kOffErr + (int)kLdsEdges * 4;
-constexpr int kOffMax = kOffMin + (int)kLdsEdges * 4;
-constexpr int kOffWave = kOffMax + (int)kLdsEdges * 4;
+constexpr int kOffHt = 0;                                // u32 slot keys (0 = empty)
+constexpr int kOffHc = kOffHt + (int)kHtSlots * 4;       // u32 slot counts
+#ifndef ANOMOD_SUM_REPS
+#define ANOMOD_SUM_REPS 8
+#endif
+constexpr uint32_t kSumReps = ANOMOD_SUM_REPS;           // u64 sum replicas per edge
+constexpr int kOffSum = kOffHc + (int)kHtSlots * 4;      // u64 [kLdsEdges][kSumReps]
+constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs
+constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts
+constexpr int kOffWave = kOffErr + (int)kLdsEdges * 4;
 constexpr int kWSid = 0;                         // u64 span ids [kStage + 8]
 constexpr int kWSvc = kWSid + (kStage + 8) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2; // u8 trace-start flags [kStage]
@@ -91,29 +98,33 @@ struct Cols {
 };
 
 // Histogram increment of key = edge*kBins + bin + 1 in the workgroup's LDS
-// hash table, probing from slot h.  Slot = (count << 32) | key; 0 = empty.
-// A resident key costs one LDS read + one fire-and-forget ds_add_u64 (new
-// keys: ds_cmpst); a workgroup sees < 2^32 spans so the count half never
-// carries into the key.  A saturated probe chain counts in HBM directly.
-__device__ __forceinline__ uint32_t ht_slot(uint32_t key) {
-  return (key * 0x9E3779B1u) >> (32 - kHtLog2);
+// hash table: 2048 buckets of 4 slots, keys and counts in separate u32
+// arrays, so one ds_read_b128 fetches a key's whole home bucket.  A key
+// resident in its home bucket costs that read + one fire-and-forget
+// ds_add_u32 (0 for lanes that miss, so no branch around it).  With the SN
+// mix a workgroup holds ~3.6 k keys in 8 Ki slots and 0.02 % of spans miss
+// their home bucket (1-slot linear probing at the same size: 3.1 %, which
+// sent 87 % of wave-instructions down the insert loop).  A workgroup sees
+// < 2^32 spans, so u32 counts do not wrap.  New keys take the first empty slot
+// in probe order from the bucket start (ds_cmpst; a key never moves); a
+// saturated probe chain counts in HBM directly.
+__device__ __forceinline__ uint32_t ht_bucket(uint32_t key) {
+  return (key * 0x9E3779B1u) >> (32 - kHtBucketLog2);
 }
 
-__device__ __forceinline__ void ht_insert(unsigned long long* ht, uint32_t key, uint32_t h,
+__device__ __attribute__((noinline)) void ht_insert(uint32_t* hk, uint32_t* hc, uint32_t key, uint32_t s,
                                           unsigned long long* __restrict__ ghist) {
   for (int probe = 0; probe < kMaxProbe; ++probe) {
-    unsigned long long cur = __hip_atomic_load(&ht[h], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == 0ull) {
-      const unsigned long long prev = atomicCAS(&ht[h], 0ull, (1ull << 32) | key);
-      if (prev == 0ull) return;
-      cur = prev;
+    uint32_t cur = __hip_atomic_load(&hk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0u) {
+      const uint32_t prev = atomicCAS(&hk[s], 0u, key);
+      cur = prev == 0u ? key : prev;
     }
-    if ((uint32_t)cur == key) {
-      atomicAdd(&ht[h], 1ull << 32);
+    if (cur == key) {
+      atomicAdd(&hc[s], 1u);
       return;
     }
-    h = (h + 1u) & (kHtSlots - 1u);
+    s = (s + 1u) & (kHtSlots - 1u);
   }
   atomicAdd(&ghist[key - 1u], 1ull);
 }
@@ -123,13 +134,19 @@ __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uin
                                          uint32_t fl, const Table& tab) {
   if constexpr (ANOMOD_ABL & 1) return;
   if constexpr (LDS_STATS) {
+    // Lanes of one wave-instruction share few edges, and same-address LDS
+    // atomics serialise: the sum is spread over kSumReps replicas by lane,
+    // and min / max are read first (a broadcast read) and only updated when
+    // the span beats them — after warm-up almost never.  A stale read only
+    // costs a redundant atomic.
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
-    auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
-    auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
-    atomicAdd(&lsum[edge], (unsigned long long)d);
-    atomicMin(&lmin[edge], d);
-    atomicMax(&lmax[edge], d);
+    atomicAdd(&lsum[edge * kSumReps + (__lane_id() & (kSumReps - 1u))], (unsigned long long)d);
+    using u32x2 = uint32_t __attribute__((ext_vector_type(2)));
+    const u32x2 mm = *reinterpret_cast<const u32x2*>(lmm + 2u * edge);
+    if (d < mm.x) atomicMin(&lmm[2u * edge], d);
+    if (d > mm.y) atomicMax(&lmm[2u * edge + 1u], d);
     if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&lerr[edge], 1u);
   } else {
     atomicAdd(&tab.sum[edge], (unsigned long long)d);
@@ -148,13 +165,17 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
     if constexpr (LDS_HIST) {
       // fast path: the key is resident in its home slot -> one read and an
       // unconditional add (0 for lanes that miss, so no branch around it)
-      auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
-      const uint32_t key = kidx + 1u, h = ht_slot(key);
-      const unsigned long long cur =
-          __hip_atomic_load(&ht[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const bool hit = (uint32_t)cur == key;
-      atomicAdd(&ht[h], hit ? (1ull << 32) : 0ull);
-      if (!hit) ht_insert(ht, key, h, tab.hist);
+      auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+      auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
+      const uint32_t key = kidx + 1u, s0 = ht_bucket(key) * 4u;
+      // a plain 16-B read (other waves insert concurrently; a stale empty
+      // slot only sends the lane down the insert path, which re-reads)
+      using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+      const u32x4 bk = *reinterpret_cast<const u32x4*>(hk + s0);
+      const uint32_t j = bk.x == key ? 0u : bk.y == key ? 1u : bk.z == key ? 2u : 3u;
+      const bool hit = (j < 3u) | (bk.w == key);
+      atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
+      if (!hit) ht_insert(hk, hc, key, s0, tab.hist);
     } else
       atomicAdd(&tab.hist[kidx], 1ull);
   }
@@ -307,18 +328,21 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
 
   // ---- init LDS tables
   {
-    auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
-    for (uint32_t s = tid; s < kHtSlots; s += kThreads) ht[s] = 0ull;
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
+    for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
+      hk[s] = 0u;
+      hc[s] = 0u;
+    }
     if constexpr (LDS_STATS) {
       auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+      auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
       auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
-      auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
-      auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
+      for (uint32_t e = tid; e < E * kSumReps; e += kThreads) lsum[e] = 0ull;
       for (uint32_t e = tid; e < E; e += kThreads) {
-        lsum[e] = 0ull;
         lerr[e] = 0u;
-        lmin[e] = 0xFFFFFFFFu;
-        lmax[e] = 0u;
+        lmm[2u * e] = 0xFFFFFFFFu;
+        lmm[2u * e + 1u] = 0u;
       }
     }
   }
@@ -364,24 +388,25 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
 
   // ---- flush the workgroup's private tables (integer atomics, order-free)
   if constexpr (LDS_HIST) {
-    auto* ht = reinterpret_cast<unsigned long long*>(smem + kOffHt);
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
     for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
-      const unsigned long long v = ht[s];
-      const uint32_t cnt = (uint32_t)(v >> 32);
-      if (cnt) atomicAdd(&tab.hist[(uint32_t)v - 1u], (unsigned long long)cnt);
+      const uint32_t cnt = hc[s];
+      if (cnt) atomicAdd(&tab.hist[hk[s] - 1u], (unsigned long long)cnt);
     }
   }
   if constexpr (LDS_STATS) {
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
-    auto* lmin = reinterpret_cast<uint32_t*>(smem + kOffMin);
-    auto* lmax = reinterpret_cast<uint32_t*>(smem + kOffMax);
+    auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
     for (uint32_t e = tid; e < E; e += kThreads) {
-      if (lmin[e] != 0xFFFFFFFFu || lmax[e] != 0u) {
-        atomicAdd(&tab.sum[e], lsum[e]);
+      if (lmm[2u * e] != 0xFFFFFFFFu || lmm[2u * e + 1u] != 0u) {
+        unsigned long long sum = 0;
+        for (uint32_t k = 0; k < kSumReps; ++k) sum += lsum[e * kSumReps + k];
+        atomicAdd(&tab.sum[e], sum);
         if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
-        atomicMin(&tab.mn[e], lmin[e]);
-        atomicMax(&tab.mx[e], lmax[e]);
+        atomicMin(&tab.mn[e], lmm[2u * e]);
+        atomicMax(&tab.mx[e], lmm[2u * e + 1u]);
       }
     }
   }
