@@ -22,12 +22,15 @@ def assert_table_equal(gpu: anomod.EdgeTable, ref: dict):
     np.testing.assert_array_equal(gpu.p99_us, ref["p99_us"])
 
 
-def _random_spanset(rng, S, n_traces, max_len, orphan=0.05, dup=0.0, wide_dur=True):
+def _random_spanset(rng, S, n_traces, max_len, orphan=0.05, dup=0.0, wide_dur=True,
+                    lo_alias=False):
     lens = rng.integers(0, max_len + 1, n_traces)
     ptr = np.zeros(n_traces + 1, np.uint64)
     np.cumsum(lens, out=ptr[1:])
     n = int(ptr[-1])
     sid = rng.integers(1, 2**63, n, dtype=np.uint64)
+    if lo_alias:  # ids that share their low 32-bit word with other ids of the trace
+        sid = (sid & np.uint64(0x7FFFFFFF00000000)) | rng.integers(1, 4, n, dtype=np.uint64)
     pid = np.zeros(n, np.uint64)
     t_of = np.repeat(np.arange(n_traces), lens)
     starts = ptr[:-1].astype(np.int64)[t_of]
@@ -37,6 +40,9 @@ def _random_spanset(rng, S, n_traces, max_len, orphan=0.05, dup=0.0, wide_dur=Tr
     pid[has_parent] = sid[pick[has_parent]]
     orph = has_parent & (rng.random(n) < orphan)
     pid[orph] = rng.integers(1, 2**63, int(orph.sum()), dtype=np.uint64)
+    if lo_alias:  # orphan references whose low word matches ids of the trace
+        pid[orph] = (pid[orph] & np.uint64(0x7FFFFFFF00000000)) | rng.integers(
+            1, 4, int(orph.sum()), dtype=np.uint64)
     if dup:
         d = has_parent & (rng.random(n) < dup)
         sid[d] = sid[pick[d]]  # duplicate span ids inside a trace
@@ -64,6 +70,18 @@ def test_native_library_is_loaded(ctx):
 def test_random_sets_bit_exact(ctx, S, n_traces, max_len):
     rng = np.random.default_rng(S * 1000 + n_traces)
     sp = _random_spanset(rng, S, n_traces, max_len, dup=0.02)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
+@pytest.mark.parametrize("S,max_len", [(12, 40), (46, 60)])
+def test_low_word_aliases(ctx, S, max_len):
+    """Span ids sharing their low 32-bit word inside a trace: the kernel scans
+    low words and must confirm the high word (false candidates, orphans whose
+    low word matches, duplicates), incl. traces longer than one chunk."""
+    rng = np.random.default_rng(S + 99)
+    parts = [_random_spanset(rng, S, 3000, max_len, dup=0.05, lo_alias=True),
+             _random_spanset(rng, S, 4, 700, lo_alias=True)]
+    sp = anomod.SpanSet.concat(parts)
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
 
 
