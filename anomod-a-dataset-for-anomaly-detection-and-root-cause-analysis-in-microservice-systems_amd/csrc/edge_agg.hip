@@ -560,7 +560,9 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
 
-  if (ctx->comm && ctx->nranks > 1) {
+  // Any attached communicator merges, a 1-rank one included (an identity
+  // reduce, so the RCCL call sequence is exercised on a single-GPU box too).
+  if (ctx->comm) {
     if (int rc = stage_begin(ctx, kStageEdgeReduce)) return rc;
     ANOMOD_RCCL(ctx, ncclGroupStart());
     // hist | err | sum are contiguous u64: one sum all-reduce.
