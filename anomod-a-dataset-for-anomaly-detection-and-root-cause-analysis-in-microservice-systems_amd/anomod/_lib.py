@@ -185,6 +185,8 @@ _SIGS = {
     "anomod_graph_synthetic": (_i32, [_vp, _u32, _u32, _u64, _P(_vp)]),
     "anomod_graph_info": (_i32, [_vp, _P(_u32), _P(_u64)]),
     "anomod_graph_pagerank": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _P(_f64), _P(_u32)]),
+    "anomod_graph_pagerank_sharded": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _u32,
+                                             _P(_f64), _P(_u32)]),
     "anomod_graph_pagerank_batch": (_i32, [_vp, _vp, _P(_f64), _u32, _f64, _u32, _f64, _P(_f64),
                                            _P(_u32)]),
     "anomod_graph_free": (_i32, [_vp]),

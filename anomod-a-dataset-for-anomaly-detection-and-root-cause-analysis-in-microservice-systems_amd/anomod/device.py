@@ -289,6 +289,18 @@ class DeviceGraph:
                                                       L.ptr(x, C.c_double), C.byref(done)))
         return x, done.value
 
+    def pagerank_sharded(self, p, alpha=0.85, iters=100, tol=0.0, virtual_shards=0):
+        """Row-sharded solve: over the ranks of the attached RCCL communicator,
+        or over ``virtual_shards`` row shards on this device when none is
+        attached.  Returns the whole vector on every rank."""
+        p = np.ascontiguousarray(p, np.float64)
+        x = np.empty(self.N, np.float64)
+        done = C.c_uint32()
+        self.ctx._check(L.lib().anomod_graph_pagerank_sharded(
+            self.ctx.handle, self.handle, L.ptr(p, C.c_double), alpha, iters, tol,
+            virtual_shards, L.ptr(x, C.c_double), C.byref(done)))
+        return x, done.value
+
     def pagerank_batch(self, P, alpha=0.85, iters=100, tol=0.0):
         """K personalizations ([K, N]) in one batched solve -> x [K, N]."""
         P = np.ascontiguousarray(np.atleast_2d(P), np.float64)

@@ -34,6 +34,7 @@ struct anomod_graph {
   double* p = nullptr;         // [N]
   uint32_t n_dangling = 0;
   double* x[2] = {nullptr, nullptr};
+  uint64_t x_cap = 0;          // doubles per x buffer (>= N; row-sharded solves pad)
   // Fixed-point accumulators, kAccSlots-way spread, triple-buffered by
   // iteration (k reads buffer k%3, adds into (k+1)%3, zeroes (k+2)%3):
   // buffers 0..2 dangling mass (2^-62 units), 3..5 L1 change (2^-61 units).
@@ -106,8 +107,9 @@ __device__ __forceinline__ void ppr_iter_body(
     const double* __restrict__ p, double alpha, const double* __restrict__ x_in,
     double* __restrict__ x_out, const unsigned long long* __restrict__ d_in,
     unsigned long long* d_out, unsigned long long* d_zero, unsigned long long* e_out,
-    unsigned long long* e_zero, double* red, double* s_dsum) {
-  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+    unsigned long long* e_zero, double* red, double* s_dsum, uint32_t block0 = 0) {
+  const uint32_t gb = block0 + blockIdx.x;  // global row block (row shards start at one)
+  const uint32_t r = gb * kRowsPerBlock + threadIdx.x;
   double acc = 0.0;
   if (r < N) {
     const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
@@ -146,11 +148,11 @@ __device__ __forceinline__ void ppr_iter_body(
   const double ds = block_sum(dacc, red);
   const double es = block_sum(eacc, red);
   if (threadIdx.x == 0) {
-    const int slot = blockIdx.x & (kAccSlots - 1);
+    const int slot = gb & (kAccSlots - 1);
     atomicAdd(&d_out[slot], __double2ull_rn(ds * kDScale));
     atomicAdd(&e_out[slot], __double2ull_rn(es * kEScale));
   }
-  if (blockIdx.x == 0 && threadIdx.x < kAccSlots) {
+  if (blockIdx.x == 0 && threadIdx.x < kAccSlots) {  // the launch's first block
     d_zero[threadIdx.x] = 0ull;
     e_zero[threadIdx.x] = 0ull;
   }
@@ -162,11 +164,11 @@ __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
     const double* __restrict__ p, double alpha, const double* __restrict__ x_in,
     double* __restrict__ x_out, const unsigned long long* __restrict__ d_in,
     unsigned long long* d_out, unsigned long long* d_zero, unsigned long long* e_out,
-    unsigned long long* e_zero) {
+    unsigned long long* e_zero, uint32_t block0) {
   __shared__ double red[kPprThreads / 64];
   __shared__ double s_dsum;
   ppr_iter_body(N, in_ptr, in_col, in_w, dangling, p, alpha, x_in, x_out, d_in, d_out, d_zero,
-                e_out, e_zero, red, &s_dsum);
+                e_out, e_zero, red, &s_dsum, block0);
 }
 
 // Grid-wide barrier of a cooperative launch.  Two-level arrival so no
@@ -434,15 +436,48 @@ void free_graph(anomod_graph* g) {
   delete g;
 }
 
-// Launch iteration `it` (x[it&1] -> x[(it+1)&1]).
-void launch_iter(anomod_ctx* ctx, anomod_graph* g, double alpha, uint32_t it) {
+// Launch iteration `it` (x[it&1] -> x[(it+1)&1]) over row blocks
+// [block0, block0 + nblocks) (default: all rows).
+void launch_iter(anomod_ctx* ctx, anomod_graph* g, double alpha, uint32_t it, uint32_t block0 = 0,
+                 uint32_t nblocks = 0) {
   const int a = it & 1, b = a ^ 1;
   const int r = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
   unsigned long long* A = g->acc;
   const int S = kAccSlots;
-  hipLaunchKernelGGL(ppr_iter_kernel, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream, g->N,
-                     g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, g->x[a], g->x[b],
-                     A + r * S, A + w * S, A + z * S, A + (3 + w) * S, A + (3 + z) * S);
+  hipLaunchKernelGGL(ppr_iter_kernel, dim3(nblocks ? nblocks : g->grid), dim3(kPprThreads), 0,
+                     ctx->stream, g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha,
+                     g->x[a], g->x[b], A + r * S, A + w * S, A + z * S, A + (3 + w) * S,
+                     A + (3 + z) * S, block0);
+}
+
+// Row shards of the sharded solve: whole 256-row blocks, ceil(grid / G) per
+// shard (the last may be short or empty), so every block's rows and its
+// fixed-point partials are the unsharded solve's.
+struct RowShard {
+  uint32_t block0, nblocks, rows_per_shard;
+};
+RowShard row_shard(const anomod_graph* g, uint32_t G, uint32_t k) {
+  const uint32_t per = (g->grid + G - 1) / G;
+  const uint32_t b0 = std::min(g->grid, k * per);
+  return {b0, std::min(g->grid, b0 + per) - b0, per * kRowsPerBlock};
+}
+
+// Size the x buffers for a G-way all-gather (G * rows_per_shard doubles).
+int ensure_shard_x(anomod_ctx* ctx, anomod_graph* g, uint32_t G) {
+  const uint64_t need = (uint64_t)row_shard(g, G, 0).rows_per_shard * G;
+  if (need <= g->x_cap) return ANOMOD_OK;
+  for (int i = 0; i < 2; ++i) {
+    double* nx = nullptr;
+    ANOMOD_HIP(ctx, hipMalloc(&nx, need * 8ull));
+    ANOMOD_HIP(ctx, hipFree(g->x[i]));
+    g->x[i] = nx;
+  }
+  g->x_cap = need;
+  if (g->exec) {  // the cached graph captured the old buffers
+    ANOMOD_HIP(ctx, hipGraphExecDestroy(g->exec));
+    g->exec = nullptr;
+  }
+  return ANOMOD_OK;
 }
 
 }  // namespace
@@ -497,6 +532,7 @@ int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t
   ok = ok && hipMalloc(&g->dangling, N) == hipSuccess;
   ok = ok && hipMalloc(&g->p, N * 8ull) == hipSuccess;
   for (int i = 0; i < 2; ++i) ok = ok && hipMalloc(&g->x[i], N * 8ull) == hipSuccess;
+  g->x_cap = N;
   ok = ok && hipMalloc(&g->acc, 6 * kAccSlots * 8) == hipSuccess;
   ok = ok && hipMalloc(&g->bar, kBarWords * sizeof(unsigned int)) == hipSuccess;
   g->host_acc.assign(6 * kAccSlots, 0ull);
@@ -765,6 +801,94 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (uint32_t k = 0; k < K; ++k)
     for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];
+  if (iters_done) *iters_done = done;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double* p,
+                                  double alpha, uint32_t iters, double tol,
+                                  uint32_t virtual_shards, double* x_out, uint32_t* iters_done) {
+  ANOMOD_REQUIRE(nullptr, ctx && g && p && x_out, "anomod_graph_pagerank_sharded: NULL argument");
+  ANOMOD_REQUIRE(ctx, alpha > 0.0 && alpha < 1.0, "alpha=%g outside (0, 1)", alpha);
+  ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
+  ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
+  const bool ranks = ctx->comm != nullptr;
+  ANOMOD_REQUIRE(ctx, !ranks || virtual_shards <= 1,
+                 "virtual_shards=%u needs a context without a communicator", virtual_shards);
+  const uint32_t G = ranks ? (uint32_t)ctx->nranks : (virtual_shards ? virtual_shards : 1u);
+  ANOMOD_REQUIRE(ctx, G <= 4096, "%u shards", G);
+  const uint32_t N = g->N;
+  double psum = 0.0;
+  for (uint32_t i = 0; i < N; ++i) {
+    ANOMOD_REQUIRE(ctx, std::isfinite(p[i]) && p[i] >= 0.0, "personalization[%u] invalid", i);
+    psum += p[i];
+  }
+  ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
+  std::vector<double> pn(p, p + N);
+  for (double& v : pn) v /= psum;
+  if (int rc = bind(ctx)) return rc;
+  if (int rc = ensure_shard_x(ctx, g, G)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, pn.data(), N * 8ull, hipMemcpyHostToDevice, ctx->stream));
+  for (unsigned long long& v : g->host_acc) v = 0ull;
+  g->host_acc[0] = (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->acc, g->host_acc.data(), g->host_acc.size() * 8,
+                                 hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(ppr_init_kernel, dim3(std::min<uint32_t>(g->grid, 1024)), dim3(kPprThreads),
+                     0, ctx->stream, N, 1.0 / N, g->x[0]);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  unsigned long long* A = g->acc;
+  const int S = kAccSlots;
+  uint32_t done = iters;
+  if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const int b = (it & 1) ^ 1, w = (it + 1) % 3, z = (it + 2) % 3;
+    if (ranks) {
+      // This rank's rows, then one grouped exchange: the fixed-point partials
+      // (u64 sums: order-free, so every rank holds the unsharded scalars)
+      // and an in-place all-gather of the new vector's row shards.
+      const RowShard sh = row_shard(g, G, (uint32_t)ctx->rank);
+      if (sh.nblocks) {
+        launch_iter(ctx, g, alpha, it, sh.block0, sh.nblocks);
+      } else {  // nothing to launch: still clear the slots iteration it+1 adds into
+        ANOMOD_HIP(ctx, hipMemsetAsync(A + z * S, 0, S * 8ull, ctx->stream));
+        ANOMOD_HIP(ctx, hipMemsetAsync(A + (3 + z) * S, 0, S * 8ull, ctx->stream));
+      }
+      ANOMOD_HIP(ctx, hipGetLastError());
+      double* xb = g->x[b];
+      ANOMOD_RCCL(ctx, ncclGroupStart());
+      ANOMOD_RCCL(ctx, ncclAllReduce(A + w * S, A + w * S, S, ncclUint64, ncclSum, ctx->comm,
+                                     ctx->stream));
+      ANOMOD_RCCL(ctx, ncclAllReduce(A + (3 + w) * S, A + (3 + w) * S, S, ncclUint64, ncclSum,
+                                     ctx->comm, ctx->stream));
+      ANOMOD_RCCL(ctx, ncclAllGather(xb + (size_t)ctx->rank * sh.rows_per_shard, xb,
+                                     sh.rows_per_shard, ncclFloat64, ctx->comm, ctx->stream));
+      ANOMOD_RCCL(ctx, ncclGroupEnd());
+    } else {
+      // Virtual shards on one device (the same row split, sequential
+      // launches into shared accumulators): rehearses the sharding exactly.
+      for (uint32_t k = 0; k < G; ++k) {
+        const RowShard sh = row_shard(g, G, k);
+        if (sh.nblocks) launch_iter(ctx, g, alpha, it, sh.block0, sh.nblocks);
+      }
+      ANOMOD_HIP(ctx, hipGetLastError());
+    }
+    if (tol > 0.0) {
+      unsigned long long* eh = g->host_acc.data() + (3 + w) * S;
+      ANOMOD_HIP(ctx, hipMemcpyAsync(eh, A + (3 + w) * S, S * 8, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      unsigned long long et = 0;
+      for (int i = 0; i < S; ++i) et += eh[i];
+      if ((double)et * (1.0 / kEScale) < (double)N * tol) {
+        done = it + 1;
+        break;
+      }
+    }
+  }
+  if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(x_out, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;
 }

@@ -232,6 +232,25 @@ def main() -> int:
             "bytes_per_iter": ppr_bytes,
             "achieved_GBps": ppr_bytes * args.ppr_iters / (np.mean(pr_ms) * 1e-3) / 1e9,
         }
+        # row-sharded solve (SURVEY §8e "sharded" series): one vector over all
+        # ranks, whole 256-row blocks per rank, one grouped RCCL exchange per
+        # iteration (u64 partial sums + in-place all-gather of x); at N=1 the
+        # same loop without a communicator
+        gs = anomod.DeviceGraph(ctx, synthetic=(args.ppr_nodes, 10, 11))  # same graph everywhere
+        ps = np.random.default_rng(7).random(gs.N)  # and the same vector
+        gs.pagerank_sharded(ps, iters=args.ppr_iters)
+        sh_ms = []
+        for _ in range(3):
+            barrier()
+            gs.pagerank_sharded(ps, iters=args.ppr_iters)
+            sh_ms.append(ctx.stage_ms(L.STAGE_PAGERANK))
+        gs.free()
+        s_ms = allmax(float(np.mean(sh_ms)))
+        result["pagerank"]["sharded"] = {
+            "iters_per_s": args.ppr_iters / (s_ms * 1e-3), "shards": world,
+            "us_per_iter": s_ms * 1e3 / args.ppr_iters,
+            "mode": "row-sharded, per-iteration launches + RCCL all-reduce/all-gather"
+                    if world > 1 else "row-sharded path, 1 shard (per-iteration launches)"}
         # batched personalizations (one per fault hypothesis)
         kb = 8
         Pb = np.random.default_rng(100 + rank).random((kb, g.N))

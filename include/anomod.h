@@ -358,6 +358,18 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
 int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* P, uint32_t K,
                                 double alpha, uint32_t iters, double tol, double* X,
                                 uint32_t* iters_done);
+/* Row-sharded solve (SURVEY.md §8e "sharded" series): with a communicator
+ * attached (anomod_ctx_attach_comm) each rank computes its share of whole
+ * 256-row blocks of the pull SpMV and every iteration ends in one grouped
+ * RCCL exchange — u64 sums of the fixed-point dangling / L1 partials and an
+ * in-place all-gather of the new vector.  Without a communicator,
+ * virtual_shards = G > 1 runs the same G-way row split on this one device
+ * (the single-GPU rehearsal of the sharded path).  Every rank returns the
+ * whole vector, equal bit for bit to anomod_graph_pagerank's per-launch
+ * solve for any G (same blocks, same integer-summed scalars).           */
+int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double* p,
+                                  double alpha, uint32_t iters, double tol,
+                                  uint32_t virtual_shards, double* x_out, uint32_t* iters_done);
 int anomod_graph_free(anomod_graph* g);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------*/

@@ -174,6 +174,41 @@ def test_pagerank_batch_equals_single_solves(ctx, K):
     g.free()
 
 
+@pytest.mark.parametrize("G", [1, 2, 3, 8, 500])
+def test_pagerank_row_sharded_equals_unsharded(ctx, monkeypatch, G):
+    """Row-sharded solve rehearsed on one device (G row shards of whole 256-row
+    blocks, 500 > blocks: empty shards) == the unsharded per-launch solve, bit
+    for bit, in fixed-iteration and tolerance mode."""
+    monkeypatch.setenv("ANOMOD_PPR_MODE", "1")
+    g = anomod.DeviceGraph(ctx, synthetic=(30000, 8, 6))
+    p = np.random.default_rng(G).random(g.N)
+    for iters, tol in ((1, 0.0), (37, 0.0), (1000, 1e-10)):
+        xs, ds = g.pagerank_sharded(p, iters=iters, tol=tol, virtual_shards=G)
+        x, d = g.pagerank(p, iters=iters, tol=tol)
+        assert ds == d
+        np.testing.assert_array_equal(xs, x)
+    x2, _ = g.pagerank(p, iters=37)  # the padded x buffers serve the other paths too
+    xs2, _ = g.pagerank_sharded(p, iters=37, virtual_shards=G)
+    np.testing.assert_array_equal(x2, xs2)
+    g.free()
+
+
+def test_pagerank_row_sharded_rccl_one_rank(ctx, monkeypatch):
+    """The RCCL form (grouped u64 all-reduces + in-place all-gather per
+    iteration) on a 1-rank communicator == the unsharded solve."""
+    monkeypatch.setenv("ANOMOD_PPR_MODE", "1")
+    with anomod.Context(0) as c:
+        c.attach_comm(anomod.Context.unique_id(), 1, 0)
+        g = anomod.DeviceGraph(c, synthetic=(30000, 8, 6))
+        p = np.random.default_rng(1).random(g.N)
+        for iters, tol in ((37, 0.0), (1000, 1e-10)):
+            xs, ds = g.pagerank_sharded(p, iters=iters, tol=tol)
+            x, d = g.pagerank(p, iters=iters, tol=tol)
+            assert ds == d
+            np.testing.assert_array_equal(xs, x)
+        g.free()
+
+
 def test_features_and_rank_find_injected_fault(ctx):
     fault = "post-storage-service"
     base = anomod.load_experiment(anomod.SynthSpec("SN", seed=21), n_traces=20000)
