@@ -256,7 +256,7 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
 // trace_collector.py:424-443).
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
-  for (uint32_t q0 = a & ~3u; q0 < b; q0 += 8) {
+  for (uint32_t q0 = a & ~1u; q0 < b; q0 += 8) {
     const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
     const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
     const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 4);
@@ -264,7 +264,7 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
     uint32_t m = (v0.x == pid ? 1u : 0u) | (v0.y == pid ? 2u : 0u) | (v1.x == pid ? 4u : 0u) |
                  (v1.y == pid ? 8u : 0u) | (v2.x == pid ? 16u : 0u) | (v2.y == pid ? 32u : 0u) |
                  (v3.x == pid ? 64u : 0u) | (v3.y == pid ? 128u : 0u);
-    const uint32_t lo = a > q0 ? a - q0 : 0u;             // < 4
+    const uint32_t lo = a > q0 ? a - q0 : 0u;             // < 2
     const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;    // >= 1
     m &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
     if (m) return (int)(q0 + __ffs(m) - 1u);
