@@ -44,6 +44,11 @@ namespace {
 using namespace chunk;
 
 constexpr int kTsWaves = 8;
+// Experiment-only ablations (never set in the shipped build): 1 = no per-trace
+// pass, 2 = no pointer jumping.
+#ifndef ANOMOD_TS_ABL
+#define ANOMOD_TS_ABL 0
+#endif
 constexpr int kTsThreads = kTsWaves * kWave;
 constexpr uint32_t kDone = 0x80000000u;  // pointer-jumping: chain reached a root
 
@@ -57,9 +62,11 @@ constexpr int kTPfl = kTCnt + kStage * 4;         // u32 (own parent pos + 1) | 
 constexpr int kTSvc = kTPfl + kStage * 4;         // u16 services [kStage]
 constexpr int kTRf = kTSvc + kStage * 2;          // u8 root-node flag of first spans [kStage]
 constexpr int kTFlag = kTRf + kStage;             // u8 trace-start flags [kStage]
-constexpr int kTBytes = kTFlag + kStage;
+constexpr int kTTm = kTFlag + kStage;             // u64 per-trace service bits [kWave]
+constexpr int kTTr = kTTm + kWave * 8;            // u32 per-trace root-node counts [kWave]
+constexpr int kTBytes = kTTr + kWave * 4;
 static_assert(kTBytes % 16 == 0, "wave area must stay 16-B aligned");
-static_assert(kTBytes * kTsWaves <= 160 * 1024, "LDS budget");
+static_assert(kTBytes * kTsWaves <= 80 * 1024, "LDS budget: two workgroups per CU");
 
 struct TsOut {
   uint32_t* parent_pos;
@@ -73,29 +80,26 @@ struct TsOut {
   int* scr_pf;                   // big traces only: first span of its own parent ref
 };
 
-// One ordered pass over [a, b), 8 ids per step (4 x ds_read_b128 from a
-// 16-B aligned start), answering the three per-span id questions together:
+// One ordered pass over [a, b), 8 ids per step (4 x ds_read2_b64 from the
+// trace start itself), answering the three per-span id questions together:
 // f / l = first / last position whose id equals x (the span's own id: the
 // whole range is scanned for l), pf = first position whose id equals y (the
 // span's parent reference; -1 when y == 0).  -1 when none.
 __device__ __forceinline__ void scan_ids(const uint64_t* lsid, uint32_t a, uint32_t b, uint64_t x,
                                          uint64_t y, int& f, int& l, int& pf) {
   f = l = pf = -1;
-  for (uint32_t q0 = a & ~3u; q0 < b; q0 += 8) {
-    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
-    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
-    const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 4);
-    const ulonglong2 v3 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 6);
-    const uint64_t v[8] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+  for (uint32_t q0 = a; q0 < b; q0 += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];  // 4 x ds_read2_b64
     uint32_t mx = 0, my = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       mx |= (v[j] == x ? 1u : 0u) << j;
       my |= (v[j] == y ? 1u : 0u) << j;
     }
-    const uint32_t lo = a > q0 ? a - q0 : 0u;           // < 4
     const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;  // >= 1
-    const uint32_t rm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    const uint32_t rm = (1u << hi) - 1u;
     mx &= rm;
     my &= rm;
     if (mx) {
@@ -127,6 +131,8 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kTSvc);
   auto* lrf = reinterpret_cast<uint8_t*>(wsm + kTRf);
   auto* lflag = reinterpret_cast<uint8_t*>(wsm + kTFlag);
+  auto* ltm = reinterpret_cast<unsigned long long*>(wsm + kTTm);
+  auto* ltr = reinterpret_cast<uint32_t*>(wsm + kTTr);
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
@@ -135,8 +141,16 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
     lcnt[i] = 0u;
     lsvc[i] = (uint16_t)svc[r];
   }
+  ltm[lane] = 0ull;
+  ltr[lane] = 0u;
   uint64_t Sm[kPer];
   start_masks(lflag, c, lane, Sm);
+  // Trace t (lane t < k) spans chunk positions [s, e).  Empty traces share a
+  // start position, so only without them is a span's trace the rank of its
+  // start among the start flags (trace_in_chunk).
+  const uint32_t next_start = (uint32_t)__shfl((int)c.start, (lane + 1) & (kWave - 1));
+  const uint32_t t_e = (lane + 1 < (int)c.k) ? next_start : c.n;
+  const bool span_par = __ballot((uint32_t)lane < c.k && t_e == c.start) == 0ull;
 
   int f[kPer], np[kPer];
   uint32_t a[kPer], nxt[kPer], dst[kPer];
@@ -158,7 +172,18 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
       pfl = (uint32_t)(pf + 1) | (b - a[r]) << 16;
     }
     lpfl[i] = pfl;
-    lrf[i] = (uint8_t)(i < c.n && np[r] < 0 && f[r] == (int)i);
+    const bool rf = i < c.n && np[r] < 0 && f[r] == (int)i;
+    lrf[i] = (uint8_t)rf;
+    // Per-trace services involved / root nodes: every span adds itself to
+    // its trace's LDS words (no-return atomics) instead of one lane per trace
+    // walking the trace.
+    if (span_par && i < c.n && !(ANOMOD_TS_ABL & 1)) {
+      const uint32_t ti = trace_in_chunk(Sm, r, lane);
+      const uint32_t sv = svc[r];
+      if (o.words == 1u) atomicOr(&ltm[ti], 1ull << sv);
+      else atomicOr(&o.svc_mask[(t0 + ti) * o.words + (sv >> 6)], 1ull << (sv & 63u));
+      if (rf) atomicAdd(&ltr[ti], 1u);
+    }
     nxt[r] = np[r] >= 0 ? (uint32_t)np[r] : (i | kDone);
     dst[r] = np[r] >= 0 ? 1u : 0u;
     lnxt[i] = nxt[r];
@@ -202,7 +227,7 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
   }
   // Pointer jumping: after round k every span points 2^k ancestors up (or at
   // its root, flagged kDone) and knows the distance; 8 rounds cover 256.
-  for (int round = 0; round < 8; ++round) {
+  for (int round = 0; round < ((ANOMOD_TS_ABL & 2) ? 0 : 8); ++round) {
     bool live = false;
 #pragma unroll
     for (int r = 0; r < kPer; ++r) live |= !(nxt[r] & kDone);
@@ -242,23 +267,27 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
                              (f[r] == (int)i ? ANOMOD_SPAN_FIRST : 0u));
     }
   }
-  // Per trace: lane l < k owns trace t0 + l = chunk positions [s, e).
-  const uint32_t next_start = (uint32_t)__shfl((int)c.start, (lane + 1) & (kWave - 1));
-  if ((uint32_t)lane < c.k) {
-    const uint32_t s = c.start;
-    const uint32_t e = (lane + 1 < (int)c.k) ? next_start : c.n;
+  // Per trace: lane l < k owns trace t0 + l.  Span-parallel words (complete:
+  // the wave_syncs above order every span's atomics before these reads), or,
+  // when the chunk holds an empty trace, a walk over the trace's positions.
+  if ((uint32_t)lane < c.k && !(ANOMOD_TS_ABL & 1)) {
     const uint64_t t = t0 + lane;
-    uint32_t roots = 0;
-    unsigned long long mask = 0;
-    for (uint32_t q = s; q < e; ++q) {
-      roots += lrf[q];
-      const uint32_t sv = lsvc[q];
-      if (o.words == 1u) mask |= 1ull << sv;
-      else
-        atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
+    if (span_par) {
+      o.n_roots[t] = ltr[lane];
+      if (o.words == 1u) o.svc_mask[t] = ltm[lane];
+    } else {
+      uint32_t roots = 0;
+      unsigned long long mask = 0;
+      for (uint32_t q = c.start; q < t_e; ++q) {
+        roots += lrf[q];
+        const uint32_t sv = lsvc[q];
+        if (o.words == 1u) mask |= 1ull << sv;
+        else
+          atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
+      }
+      o.n_roots[t] = roots;
+      if (o.words == 1u) o.svc_mask[t] = mask;
     }
-    o.n_roots[t] = roots;
-    if (o.words == 1u) o.svc_mask[t] = mask;
   }
   wave_sync();
 }
