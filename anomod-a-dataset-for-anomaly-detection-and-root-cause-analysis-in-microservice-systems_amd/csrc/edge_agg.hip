@@ -24,7 +24,7 @@
 //    <= 64 traces, so parent resolution is trace-local in that wave's LDS
 //    staging area (no inter-wave synchronisation inside the loop);
 //  * parent lookup: ordered scan of the trace's staged ids (first match, the
-//    reference rule), 8 ids per 4 x ds_read_b128 step (a per-wave LDS hash
+//    reference rule), 8 ids per 4 x ds_read2_b64 step (a per-wave LDS hash
 //    with ds_cmpst inserts measured 1.7x slower, and scanning a lane's 4
 //    slots in lockstep 1.1-1.4x slower: register pressure);
 //  * the E x 896 histogram does not fit LDS, so each workgroup privatises it
@@ -250,23 +250,21 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
   }
 }
 
-// First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read_b128
-// from a 16-B aligned start), matches folded into a bit mask.  First match in
-// trace order (the reference rule: jaeger_to_csv.py:34-38 /
+// First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read2_b64
+// from the trace start itself), matches folded into a bit mask.  First match
+// in trace order (the reference rule: jaeger_to_csv.py:34-38 /
 // trace_collector.py:424-443).
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
-  for (uint32_t q0 = a & ~1u; q0 < b; q0 += 8) {
-    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2*>(lsid + q0);
-    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 2);
-    const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 4);
-    const ulonglong2 v3 = *reinterpret_cast<const ulonglong2*>(lsid + q0 + 6);
-    uint32_t m = (v0.x == pid ? 1u : 0u) | (v0.y == pid ? 2u : 0u) | (v1.x == pid ? 4u : 0u) |
-                 (v1.y == pid ? 8u : 0u) | (v2.x == pid ? 16u : 0u) | (v2.y == pid ? 32u : 0u) |
-                 (v3.x == pid ? 64u : 0u) | (v3.y == pid ? 128u : 0u);
-    const uint32_t lo = a > q0 ? a - q0 : 0u;             // < 2
+  for (uint32_t q0 = a; q0 < b; q0 += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];  // 4 x ds_read2_b64
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m |= (v[j] == pid ? 1u : 0u) << j;
     const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;    // >= 1
-    m &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    m &= (1u << hi) - 1u;
     if (m) return (int)(q0 + __ffs(m) - 1u);
   }
   return -1;
