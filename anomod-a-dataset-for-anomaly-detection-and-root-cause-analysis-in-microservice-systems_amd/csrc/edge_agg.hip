@@ -305,6 +305,8 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
         trace_bounds(Sm, r, lane, c.n, a, b);
         const int q = find_parent(lsid, a, b, R.pid[r]);
         if (q >= 0) p = lsvc[q];
+      } else {  // ablation: a parent-like edge without the lookup (keeps key diversity)
+        p = ((R.sf[r] & 0xFFFFu) + 1u + (uint32_t)(R.pid[r] & 1u)) % S;
       }
     }
     if (i < c.n) record<LDS_HIST, LDS_STATS>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r],
