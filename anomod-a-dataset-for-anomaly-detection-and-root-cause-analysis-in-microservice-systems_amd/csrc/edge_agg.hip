@@ -24,7 +24,7 @@
 //    <= 64 traces, so parent resolution is trace-local in that wave's LDS
 //    staging area (no inter-wave synchronisation inside the loop);
 //  * parent lookup: ordered scan of the trace's staged ids (first match, the
-//    reference rule), 8 ids per 4 x ds_read2_b64 step (a per-wave LDS hash
+//    reference rule), 10 ids per 5 x ds_read2_b64 step (a per-wave LDS hash
 //    with ds_cmpst inserts measured 1.7x slower, and scanning a lane's 4
 //    slots in lockstep 1.1-1.4x slower: register pressure);
 //  * the E x 896 histogram does not fit LDS, so each workgroup privatises it
@@ -74,9 +74,9 @@ constexpr int kOffSum = kOffHc + (int)kHtSlots * 4;      // u64 [kLdsEdges][kSum
 constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs
 constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts
 constexpr int kOffWave = kOffErr + (int)kLdsEdges * 4;
-constexpr int kWSid = 0;                         // u64 span ids [kStage + 8]
-constexpr int kWSvc = kWSid + (kStage + 8) * 8;  // u16 services [kStage + 8]
-constexpr int kWFlag = kWSvc + (kStage + 8) * 2; // u8 trace-start flags [kStage]
+constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
+constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
+constexpr int kWFlag = kWSvc + (kStage + 8) * 2;  // u8 trace-start flags [kStage]
 constexpr int kWBytes = kWFlag + kStage;
 constexpr int kLdsBytes = kOffWave + kWavesPerWG * kWBytes;
 static_assert(kWBytes % 16 == 0, "wave staging must stay 16-B aligned");
@@ -250,20 +250,26 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
   }
 }
 
-// First span of [a, b) whose id equals pid: 8 ids per step (4 x ds_read2_b64
+// First span of [a, b) whose id equals pid: kScan ids per step (ds_read2_b64
 // from the trace start itself), matches folded into a bit mask.  First match
 // in trace order (the reference rule: jaeger_to_csv.py:34-38 /
 // trace_collector.py:424-443).
+#ifndef ANOMOD_SCAN_IDS
+#define ANOMOD_SCAN_IDS 10
+#endif
+constexpr uint32_t kScan = ANOMOD_SCAN_IDS;  // ids compared per step (kScan / 2 x ds_read2_b64)
+static_assert(kScan % 2 == 0 && kScan <= 16, "scan step");
+
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
-  for (uint32_t q0 = a; q0 < b; q0 += 8) {
-    uint64_t v[8];
+  for (uint32_t q0 = a; q0 < b; q0 += kScan) {
+    uint64_t v[kScan];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];  // 4 x ds_read2_b64
+    for (uint32_t j = 0; j < kScan; ++j) v[j] = lsid[q0 + j];
     uint32_t m = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m |= (v[j] == pid ? 1u : 0u) << j;
-    const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;    // >= 1
+    for (uint32_t j = 0; j < kScan; ++j) m |= (v[j] == pid ? 1u : 0u) << j;
+    const uint32_t hi = (b - q0) < kScan ? (b - q0) : kScan;  // >= 1
     m &= (1u << hi) - 1u;
     if (m) return (int)(q0 + __ffs(m) - 1u);
   }
