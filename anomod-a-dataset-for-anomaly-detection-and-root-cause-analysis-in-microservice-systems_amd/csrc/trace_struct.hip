@@ -53,9 +53,9 @@ constexpr int kTsThreads = kTsWaves * kWave;
 constexpr uint32_t kDone = 0x80000000u;  // pointer-jumping: chain reached a root
 
 // Per-wave LDS carve (bytes; 16-B aligned offsets).
-constexpr int kTSid = 0;                          // u64 span ids   [kStage + 8]
-constexpr int kTPid = kTSid + (kStage + 8) * 8;   // u64 parent refs [kStage + 8]
-constexpr int kTNxt = kTPid + (kStage + 8) * 8;   // u32 jump target | kDone [kStage]
+constexpr int kTSid = 0;                          // u64 span ids   [kStage + 16] (scan slack)
+constexpr int kTPid = kTSid + (kStage + 16) * 8;  // u64 parent refs [kStage]
+constexpr int kTNxt = kTPid + kStage * 8;         // u32 jump target | kDone [kStage]
 constexpr int kTDst = kTNxt + kStage * 4;         // u32 distance to the target [kStage]
 constexpr int kTCnt = kTDst + kStage * 4;         // u32 child counts [kStage]
 constexpr int kTPfl = kTCnt + kStage * 4;         // u32 (own parent pos + 1) | trace len << 16
@@ -80,25 +80,30 @@ struct TsOut {
   int* scr_pf;                   // big traces only: first span of its own parent ref
 };
 
-// One ordered pass over [a, b), 8 ids per step (4 x ds_read2_b64 from the
+// One ordered pass over [a, b), kTsScan ids per step (ds_read2_b64 from the
 // trace start itself), answering the three per-span id questions together:
 // f / l = first / last position whose id equals x (the span's own id: the
 // whole range is scanned for l), pf = first position whose id equals y (the
 // span's parent reference; -1 when y == 0).  -1 when none.
+#ifndef ANOMOD_TS_SCAN_IDS
+#define ANOMOD_TS_SCAN_IDS 10
+#endif
+constexpr uint32_t kTsScan = ANOMOD_TS_SCAN_IDS;  // ids per step (kTsScan / 2 x ds_read2_b64)
+
 __device__ __forceinline__ void scan_ids(const uint64_t* lsid, uint32_t a, uint32_t b, uint64_t x,
                                          uint64_t y, int& f, int& l, int& pf) {
   f = l = pf = -1;
-  for (uint32_t q0 = a; q0 < b; q0 += 8) {
-    uint64_t v[8];
+  for (uint32_t q0 = a; q0 < b; q0 += kTsScan) {
+    uint64_t v[kTsScan];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = lsid[q0 + j];  // 4 x ds_read2_b64
+    for (uint32_t j = 0; j < kTsScan; ++j) v[j] = lsid[q0 + j];
     uint32_t mx = 0, my = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (uint32_t j = 0; j < kTsScan; ++j) {
       mx |= (v[j] == x ? 1u : 0u) << j;
       my |= (v[j] == y ? 1u : 0u) << j;
     }
-    const uint32_t hi = (b - q0) < 8u ? (b - q0) : 8u;  // >= 1
+    const uint32_t hi = (b - q0) < kTsScan ? (b - q0) : kTsScan;  // >= 1
     const uint32_t rm = (1u << hi) - 1u;
     mx &= rm;
     my &= rm;
