@@ -74,6 +74,44 @@ def cpu_baseline(spec, n_traces: int, threads: int, min_seconds: float) -> dict:
                       f"passes in {el:.1f} s, C oracle, {threads} threads"}
 
 
+# Chaos targets of the TrainTicket runs (chaos-experiments/*.yaml target_service
+# labels, run_experiment.sh:299-345); None = the normal run (baseline).
+TT_FAULTS = [None, "ts-preserve-service", "ts-order-service", "ts-security-service",
+             "ts-travel-service", "ts-auth-service", "ts-basic-service", "ts-route-service",
+             "ts-seat-service", "ts-station-service", "ts-price-service",
+             "ts-train-service", "ts-user-service"]
+
+
+def tt_config2(ctx) -> dict:
+    """BASELINE config 2 on one GPU: the TrainTicket trace set of 13
+    experiments (~15k spans each, 46 services) + their metric matrices
+    (S = 5980 series x T = 480 steps @15 s), each taken through the product
+    call surface features() -> rank() (H2D of spans and series, edge table,
+    EWMA/z, PageRank, D2H and the host glue all inside the timed loop).
+    Inputs are synthetic and built in host memory before the clock starts."""
+    exps = [anomod.load_experiment(anomod.SynthSpec("TT", seed=20251103 + i, fault_service=f),
+                                   n_traces=650, series_per_service=130,
+                                   name=f"tt_{f or 'normal'}")
+            for i, f in enumerate(TT_FAULTS)]
+    base = anomod.features(exps[0], ctx)  # normal run: latency baseline (and warm-up)
+    for e in exps[1:3]:
+        anomod.rank(anomod.features(e, ctx, baseline=base), ctx=ctx)
+    t0 = time.perf_counter()
+    base = anomod.features(exps[0], ctx)
+    hits = []
+    for e in exps[1:]:
+        ranking = anomod.rank(anomod.features(e, ctx, baseline=base), ctx=ctx)
+        hits.append(anomod.hit_at(ranking, e.label, 3))
+    el = time.perf_counter() - t0
+    spans = sum(e.spans.n_spans for e in exps)
+    samples = sum(e.metrics.S * e.metrics.T for e in exps)
+    return {"experiments": len(exps), "spans": spans, "series": exps[0].metrics.S,
+            "steps": exps[0].metrics.T, "seconds": el, "ms_per_experiment": el / len(exps) * 1e3,
+            "spans_per_s": spans / el, "samples_per_s": samples / el,
+            "top3_hit_rate": float(np.mean(hits)),
+            "note": "end to end through features()/rank(): host-latency-bound at this size"}
+
+
 def load_traffic(n_spans: int) -> float | None:
     """HBM bytes per launch from the committed PMC profile of this workload."""
     p = ROOT / "profiles" / "edge_agg_pmc.json"
@@ -283,6 +321,9 @@ def main() -> int:
             "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
         }
         ser.free()
+
+    if not args.no_extras and world == 1:
+        result["tt_config2"] = tt_config2(ctx)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
