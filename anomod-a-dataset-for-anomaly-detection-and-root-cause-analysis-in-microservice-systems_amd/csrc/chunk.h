@@ -49,17 +49,22 @@ struct Chunk {
   uint32_t start;  // this lane's trace start relative to base (lanes < k)
 };
 
+// Lane `l` (wave-uniform) of a 64-bit value, through v_readlane (SALU side,
+// no LDS-pipe permute).
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+
 // lo/hi = trace_ptr[t + lane], trace_ptr[t + lane + 1] (see load_bounds).
 __device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane, uint64_t lo,
                                             uint64_t hi) {
   Chunk c;
   const bool valid = t + lane < t_end;
-  c.base = uniform64(__shfl(lo, 0));
+  c.base = readlane64(lo, 0);
   const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
   c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
-  const uint32_t n = c.k ? (uint32_t)(__shfl(hi, (int)c.k - 1) - c.base)
-                         : (uint32_t)(__shfl(hi, 0) - c.base);
-  c.n = (uint32_t)__builtin_amdgcn_readfirstlane(n);
+  c.n = (uint32_t)(readlane64(hi, c.k ? (int)c.k - 1 : 0) - c.base);
   c.start = (uint32_t)(lo - c.base);
   return c;
 }
