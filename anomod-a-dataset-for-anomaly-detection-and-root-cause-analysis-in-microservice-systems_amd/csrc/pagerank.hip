@@ -78,6 +78,31 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
+// Two block sums in one pass (two barriers instead of four), each with
+// block_sum's reduction tree, so the results are block_sum's bit for bit.
+// `red` holds 2 * waves doubles.  Results valid in thread 0.
+__device__ __forceinline__ void block_sum2(double a, double b, double* red, double& sa,
+                                           double& sb) {
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+  if (lane == 0) {
+    red[wid] = a;
+    red[nw + wid] = b;
+  }
+  __syncthreads();
+  sa = 0.0;
+  sb = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < nw; ++w) {
+      sa += red[w];
+      sb += red[nw + w];
+    }
+  __syncthreads();
+}
+
 // The per-row arithmetic, spelled out (explicit fma, no contraction left to
 // the compiler) so every kernel — per-launch, persistent, batched — rounds
 // identically and their vectors agree bit for bit.
@@ -110,6 +135,15 @@ __device__ __forceinline__ void ppr_iter_body(
     unsigned long long* e_zero, double* red, double* s_dsum, uint32_t block0 = 0) {
   const uint32_t gb = block0 + blockIdx.x;  // global row block (row shards start at one)
   const uint32_t r = gb * kRowsPerBlock + threadIdx.x;
+  // The row's own operands do not depend on the SpMV: issue them first so
+  // their latency overlaps the CSR chain (in_ptr -> in_col/in_w -> x gathers).
+  double pr = 0.0, xr = 0.0;
+  bool dg = false;
+  if (r < N) {
+    pr = p[r];
+    xr = x_in[r];
+    dg = dangling[r] != 0;
+  }
   double acc = 0.0;
   if (r < N) {
     const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
@@ -139,14 +173,13 @@ __device__ __forceinline__ void ppr_iter_body(
   const double dsum = *s_dsum;
   double dacc = 0.0, eacc = 0.0;
   if (r < N) {
-    const double pr = p[r];
     const double y = ppr_row(alpha, acc, dsum, pr);
     x_out[r] = y;
-    if (dangling[r]) dacc = y;
-    eacc = fabs(y - x_in[r]);
+    if (dg) dacc = y;
+    eacc = fabs(y - xr);
   }
-  const double ds = block_sum(dacc, red);
-  const double es = block_sum(eacc, red);
+  double ds, es;
+  block_sum2(dacc, eacc, red, ds, es);
   if (threadIdx.x == 0) {
     const int slot = gb & (kAccSlots - 1);
     atomicAdd(&d_out[slot], __double2ull_rn(ds * kDScale));
@@ -165,7 +198,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
     double* __restrict__ x_out, const unsigned long long* __restrict__ d_in,
     unsigned long long* d_out, unsigned long long* d_zero, unsigned long long* e_out,
     unsigned long long* e_zero, uint32_t block0) {
-  __shared__ double red[kPprThreads / 64];
+  __shared__ double red[2 * (kPprThreads / 64)];
   __shared__ double s_dsum;
   ppr_iter_body(N, in_ptr, in_col, in_w, dangling, p, alpha, x_in, x_out, d_in, d_out, d_zero,
                 e_out, e_zero, red, &s_dsum, block0);

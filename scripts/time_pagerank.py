@@ -15,9 +15,10 @@ import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
 with anomod.Context(0) as ctx:
-    g = anomod.DeviceGraph(ctx, synthetic=(100000, 10, 11))
+  for n_nodes in [int(v) for v in os.environ.get("PPR_NS", "100000").split(",")]:
+    g = anomod.DeviceGraph(ctx, synthetic=(n_nodes, 10, 11))
     p = np.random.default_rng(0).random(g.N)
-    for mode in ("0", "1", "2"):
+    for mode in os.environ.get("PPR_MODES", "0,1,2").split(","):
         os.environ["ANOMOD_PPR_MODE"] = mode
         for iters, tol in ((100, 0.0), (1000, 1e-10)):
             g.pagerank(p, iters=iters, tol=tol)
@@ -28,7 +29,7 @@ with anomod.Context(0) as ctx:
                 wall.append((time.perf_counter() - t) * 1e3)
                 ms.append(ctx.stage_ms(L.STAGE_PAGERANK))
             k = float(np.median(ms))
-            print(json.dumps({"mode": mode, "iters": its, "tol": tol, "kernel_ms": k,
+            print(json.dumps({"N": g.N, "mode": mode, "iters": its, "tol": tol, "kernel_ms": k,
                               "us_per_iter": k * 1e3 / its, "iters_per_s": its / k * 1e3,
                               "wall_ms": float(np.median(wall))}), flush=True)
     g.free()
