@@ -129,22 +129,32 @@ __device__ __attribute__((noinline)) void ht_insert(uint32_t* hk, uint32_t* hc, 
   atomicAdd(&ghist[key - 1u], 1ull);
 }
 
+using u32x2 = uint32_t __attribute__((ext_vector_type(2)));
+
+// The edge's current (min, max) in LDS (read before the span's histogram
+// update, so this read and the bucket read share one LDS round trip).
+template <bool LDS_STATS>
+__device__ __forceinline__ u32x2 stat_peek(const unsigned char* smem, uint32_t edge) {
+  if constexpr (LDS_STATS && !(ANOMOD_ABL & 1))
+    return *reinterpret_cast<const u32x2*>(smem + kOffMm + 8u * edge);
+  else
+    return u32x2{0u, 0u};
+}
+
 template <bool LDS_STATS>
 __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uint32_t d,
-                                         uint32_t fl, const Table& tab) {
+                                         uint32_t fl, const Table& tab, u32x2 mm) {
   if constexpr (ANOMOD_ABL & 1) return;
   if constexpr (LDS_STATS) {
     // Lanes of one wave-instruction share few edges, and same-address LDS
     // atomics serialise: the sum is spread over kSumReps replicas by lane,
-    // and min / max are read first (a broadcast read) and only updated when
-    // the span beats them — after warm-up almost never.  A stale read only
-    // costs a redundant atomic.
+    // and min / max (`mm`, read by stat_peek: a broadcast read) are only
+    // updated when the span beats them — after warm-up almost never.  A stale
+    // read only costs a redundant atomic.
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
     auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
     atomicAdd(&lsum[edge * kSumReps + (__lane_id() & (kSumReps - 1u))], (unsigned long long)d);
-    using u32x2 = uint32_t __attribute__((ext_vector_type(2)));
-    const u32x2 mm = *reinterpret_cast<const u32x2*>(lmm + 2u * edge);
     if (d < mm.x) atomicMin(&lmm[2u * edge], d);
     if (d > mm.y) atomicMax(&lmm[2u * edge + 1u], d);
     if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&lerr[edge], 1u);
@@ -160,6 +170,9 @@ __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uin
 template <bool LDS_HIST, bool LDS_STATS>
 __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
                                        const Table& tab) {
+  const u32x2 mm = stat_peek<LDS_STATS>(smem, edge);
+  bool miss = false;
+  uint32_t key = 0, s0 = 0;
   if constexpr (!(ANOMOD_ABL & 2)) {
     const uint32_t kidx = edge * kBins + hist_bin(d);
     if constexpr (LDS_HIST) {
@@ -167,7 +180,8 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
       // unconditional add (0 for lanes that miss, so no branch around it)
       auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
       auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
-      const uint32_t key = kidx + 1u, s0 = ht_bucket(key) * 4u;
+      key = kidx + 1u;
+      s0 = ht_bucket(key) * 4u;
       // a plain 16-B read (other waves insert concurrently; a stale empty
       // slot only sends the lane down the insert path, which re-reads)
       using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
@@ -175,11 +189,15 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
       const uint32_t j = bk.x == key ? 0u : bk.y == key ? 1u : bk.z == key ? 2u : 3u;
       const bool hit = (j < 3u) | (bk.w == key);
       atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
-      if (!hit) ht_insert(hk, hc, key, s0, tab.hist);
+      miss = !hit;
     } else
       atomicAdd(&tab.hist[kidx], 1ull);
   }
-  stat_add<LDS_STATS>(smem, edge, d, fl, tab);
+  stat_add<LDS_STATS>(smem, edge, d, fl, tab, mm);
+  if constexpr (LDS_HIST && !(ANOMOD_ABL & 2))
+    if (miss)
+      ht_insert(reinterpret_cast<uint32_t*>(smem + kOffHt),
+                reinterpret_cast<uint32_t*>(smem + kOffHc), key, s0, tab.hist);
 }
 
 // A trace longer than kStage: wave-cooperative scan of the trace's span ids,
