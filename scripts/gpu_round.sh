@@ -10,6 +10,9 @@ timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 > gpurun_out/bench.lo
 rc=$?; echo "bench rc=$rc" >> gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 OUT=gpurun_out/prof
+# rocprofv3 --kernel-trace crashes at process exit after any cooperative launch
+# (scripts/coop_exit_probe.py): profiled runs take the per-launch PageRank path.
+export ANOMOD_PPR_MODE=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_trace.log 2>&1 || exit $?
 PMC_ARGS="--steps 2 --warmup 0 --no-cpu-baseline --no-extras"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS > $OUT/pmc_fetch.log 2>&1 || exit $?

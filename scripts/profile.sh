@@ -3,6 +3,9 @@
 cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
+# rocprofv3 --kernel-trace crashes at process exit after any cooperative launch
+# (scripts/coop_exit_probe.py): profiled runs take the per-launch PageRank path.
+export ANOMOD_PPR_MODE=1
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $BENCH_ARGS > $OUT/bench_trace.log 2>&1 || exit $?
