@@ -37,6 +37,9 @@ struct anomod_ctx {
   // Cached device workspace for the edge table.
   void* d_table = nullptr;
   size_t table_bytes = 0;
+  // Pinned host staging for the edge table's small per-edge vectors (one D2H).
+  void* h_stage = nullptr;
+  size_t stage_bytes = 0;
 };
 
 struct anomod_spans {
@@ -89,6 +92,7 @@ int stage_begin(anomod_ctx* ctx, Stage s);
 int stage_end(anomod_ctx* ctx, Stage s);
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
+int ensure_host_stage(anomod_ctx* ctx, size_t bytes);
 
 // ---- integer latency histogram (ANOMOD_HIST_*) --------------------------
 __host__ __device__ inline uint32_t hist_bin(uint32_t v) {

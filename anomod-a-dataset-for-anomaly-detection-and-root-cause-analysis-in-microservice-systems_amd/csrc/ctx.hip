@@ -58,6 +58,23 @@ int ensure_table(anomod_ctx* ctx, size_t bytes) {
   return ANOMOD_OK;
 }
 
+int ensure_host_stage(anomod_ctx* ctx, size_t bytes) {
+  if (ctx->stage_bytes >= bytes) return ANOMOD_OK;
+  if (ctx->h_stage) {
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ANOMOD_HIP(ctx, hipHostFree(ctx->h_stage));
+    ctx->h_stage = nullptr;
+    ctx->stage_bytes = 0;
+  }
+  if (hipHostMalloc(&ctx->h_stage, bytes, hipHostMallocDefault) != hipSuccess) {
+    set_error(ctx, "hipHostMalloc(%zu) for the edge-table staging failed", bytes);
+    ctx->h_stage = nullptr;
+    return ANOMOD_ENOMEM;
+  }
+  ctx->stage_bytes = bytes;
+  return ANOMOD_OK;
+}
+
 }  // namespace anomod
 
 extern "C" {
@@ -118,6 +135,7 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   if (ctx->d_table) (void)hipFree(ctx->d_table);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (int s = 0; s < anomod::kNumStages; ++s) {
     if (ctx->ev_begin[s]) (void)hipEventDestroy(ctx->ev_begin[s]);
     if (ctx->ev_end[s]) (void)hipEventDestroy(ctx->ev_end[s]);

@@ -35,6 +35,7 @@
 //  * all merges are integer adds / min / max: results are bit-exact and
 //    independent of geometry, scheduling and shard count.
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 #include "chunk.h"
@@ -510,20 +511,22 @@ KernelFn pick_kernel(uint32_t E, const char** name) {
   return edge_agg_kernel<false, false>;
 }
 
-// Device table layout inside ctx->d_table.
+// Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
+// all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
+// count | p50 | p99 | mn.  [off_err, bytes) is copied to the host in one D2H.
 struct Layout {
   uint64_t E;
-  size_t off_hist, off_err, off_sum, off_count, off_p50, off_p99, off_mn, off_mx, bytes;
+  size_t off_hist, off_err, off_sum, off_mx, off_count, off_p50, off_p99, off_mn, bytes;
   explicit Layout(uint64_t e) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
     off_sum = off_err + E * 8;
-    off_count = off_sum + E * 8;
+    off_mx = off_sum + E * 8;
+    off_count = (off_mx + E * 4 + 7) & ~size_t(7);
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
-    off_mx = off_mn + E * 4;
-    bytes = off_mx + E * 4;
+    bytes = off_mn + E * 4;
   }
 };
 
@@ -560,9 +563,8 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
   auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
 
-  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum
+  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx
   ANOMOD_HIP(ctx, hipMemsetAsync(tab.mn, 0xFF, E * 4ull, ctx->stream));
-  ANOMOD_HIP(ctx, hipMemsetAsync(tab.mx, 0, E * 4ull, ctx->stream));
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
@@ -604,19 +606,27 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   ANOMOD_HIP(ctx, hipGetLastError());
   if (int rc = stage_end(ctx, kStageEdgeFinal)) return rc;
 
-  auto d2h = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-    if (!dst) return hipSuccess;
-    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
-  };
-  ANOMOD_HIP(ctx, d2h(out->count, count, E * 8ull));
-  ANOMOD_HIP(ctx, d2h(out->errors, tab.err, E * 8ull));
-  ANOMOD_HIP(ctx, d2h(out->sum_us, tab.sum, E * 8ull));
-  ANOMOD_HIP(ctx, d2h(out->min_us, tab.mn, E * 4ull));
-  ANOMOD_HIP(ctx, d2h(out->max_us, tab.mx, E * 4ull));
-  ANOMOD_HIP(ctx, d2h(out->hist, tab.hist, (size_t)E * kBins * 8ull));
-  ANOMOD_HIP(ctx, d2h(out->p50_us, p50, E * 8ull));
-  ANOMOD_HIP(ctx, d2h(out->p99_us, p99, E * 8ull));
+  // The per-edge vectors come back in one D2H into pinned staging, then
+  // fan out on the host; the histogram (when asked for) goes straight.
+  const size_t small = L.bytes - L.off_err;
+  if (int rc = ensure_host_stage(ctx, small)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, base + L.off_err, small, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  if (out->hist)
+    ANOMOD_HIP(ctx, hipMemcpyAsync(out->hist, tab.hist, (size_t)E * kBins * 8ull,
+                                   hipMemcpyDeviceToHost, ctx->stream));
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const char* hs = static_cast<const char*>(ctx->h_stage);
+  auto fan = [&](void* dst, size_t off, size_t bytes) {  // off: device layout offset
+    if (dst) memcpy(dst, hs + (off - L.off_err), bytes);
+  };
+  fan(out->count, L.off_count, E * 8ull);
+  fan(out->errors, L.off_err, E * 8ull);
+  fan(out->sum_us, L.off_sum, E * 8ull);
+  fan(out->min_us, L.off_mn, E * 4ull);
+  fan(out->max_us, L.off_mx, E * 4ull);
+  fan(out->p50_us, L.off_p50, E * 8ull);
+  fan(out->p99_us, L.off_p99, E * 8ull);
   return ANOMOD_OK;
 }
 
