@@ -149,15 +149,27 @@ def default_context() -> Context:
     return _default_ctx
 
 
-def _series_service(key, services: list[str]) -> int | None:
+def _series_service(key, services: list[str], memo: dict | None = None) -> int | None:
     """Map a metric series to a service by its label values (pod, container,
-    service, job ... carry the service name in both datasets)."""
+    service, job ... carry the service name in both datasets): the longest
+    service name contained in a label value, the first such in `services`
+    order on ties.  Service names hold no spaces, so this is decided value by
+    value; `memo` (one per call site) keeps each distinct value's answer."""
     labels = key[1] if len(key) > 1 else ()
-    text = " ".join(str(v) for _, v in labels)
     best = None
-    for i, s in enumerate(services):
-        if s and s in text and (best is None or len(s) > len(services[best])):
-            best = i
+    for _, v in labels:
+        v = str(v)
+        hit = memo.get(v, -2) if memo is not None else -2
+        if hit == -2:
+            hit = -1
+            for i, s in enumerate(services):
+                if s and s in v and (hit < 0 or len(s) > len(services[hit])):
+                    hit = i
+            if memo is not None:
+                memo[v] = hit
+        if hit >= 0 and (best is None or len(services[hit]) > len(services[best])
+                         or (len(services[hit]) == len(services[best]) and hit < best)):
+            best = hit
     return best
 
 
@@ -194,8 +206,9 @@ def features(exp: Experiment, ctx: Context | None = None, *, W: int = 60,
         # a single spike), then take the max over the series of a service
         k = max(1, Z.shape[0] // 20)
         top = np.sort(Z, axis=0)[-k:].mean(axis=0) if Z.shape[0] else np.zeros(Z.shape[1])
+        memo: dict = {}
         for j, key in enumerate(series):
-            i = _series_service(key, edges.services)
+            i = _series_service(key, edges.services, memo)
             if i is not None:
                 metric_score[i] = max(metric_score[i], float(top[j]))
     # error rate of the calls each service serves
