@@ -8,11 +8,16 @@
 #include "common.h"
 
 namespace anomod {
+namespace {  // internal linkage: a kernel file may pick its own chunk size
 namespace chunk {
 
+#ifndef ANOMOD_STAGE
+#define ANOMOD_STAGE 256
+#endif
 constexpr int kWave = 64;
-constexpr int kStage = 256;  // spans staged per wave chunk
+constexpr int kStage = ANOMOD_STAGE;  // spans staged per wave chunk
 constexpr int kPer = kStage / kWave;
+static_assert(kStage % kWave == 0 && kStage <= 1024, "chunk size");
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -84,7 +89,7 @@ __device__ __forceinline__ void load_bounds(const uint64_t* __restrict__ trace_p
 // 64*r + l starts a trace.  lflag is the wave's u8[kStage] LDS scratch.
 __device__ __forceinline__ void start_masks(uint8_t* lflag, const Chunk& c, int lane,
                                             uint64_t (&Sm)[kPer]) {
-  reinterpret_cast<uint32_t*>(lflag)[lane] = 0u;
+  for (int w = lane; w < kStage / 4; w += kWave) reinterpret_cast<uint32_t*>(lflag)[w] = 0u;
   wave_sync();
   if ((uint32_t)lane < c.k && c.start < c.n) lflag[c.start] = 1;
   wave_sync();
@@ -129,4 +134,5 @@ __device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], i
 }
 
 }  // namespace chunk
+}  // namespace
 }  // namespace anomod
