@@ -104,6 +104,30 @@ def test_ewma_synthetic_fill_same_in_both_layouts(ctx, monkeypatch):
     np.testing.assert_array_equal(out[0], out[1])
 
 
+def test_ewma_dense_blocks_equal_general_step(ctx, monkeypatch):
+    """The tiled kernel takes a select-free step for 64-step blocks in which
+    every lane of the wave has started and no sample is NaN.  Waves that are
+    wholly dense, that hold one NaN, that start late in one lane, or that hold
+    +-inf (sum NaN -> general path; a lone inf stays on the dense path) must
+    equal the row kernel (general step only) bit for bit."""
+    rng = np.random.default_rng(23)
+    T, S, W = 1980, 640, 60  # 10 waves; T % 64 != 0: a partial last block
+    X = (1000 + 30 * rng.standard_normal((T, S))).astype(np.float32)
+    X[777, 64 + 5] = np.nan                 # wave 1: one NaN in one block
+    X[:100, 128 + 9] = np.nan               # wave 2: one lane starts at step 100
+    X[1500, 192 + 1] = np.inf               # wave 3: a lone inf (dense path)
+    X[300, 256 + 2], X[301, 256 + 3] = np.inf, -np.inf  # wave 4: inf - inf in the sum
+    X[:, 320 + 4] = np.nan                  # wave 5: a lane that never starts
+    out = []
+    for mode in ("1", "3"):
+        monkeypatch.setenv("ANOMOD_EWMA_MODE", mode)
+        out.append(ctx.ewma_z(X, 2 / 61, W))
+    np.testing.assert_array_equal(out[0], out[1])
+    fin = np.r_[0:192, 320:640]  # lanes of the waves without inf, against the oracle
+    np.testing.assert_allclose(out[0][:, fin], native.ewma_z(X[:, fin], 2 / 61, W),
+                               rtol=Z_RTOL, atol=Z_ATOL)
+
+
 def test_pagerank_matches_networkx_golden(ctx, golden):
     g = np.load(golden / "pagerank_networkx.npz")
     x, it = ctx.pagerank(g["row_ptr"], g["col"], g["w"], g["p"], float(g["alpha"]),
