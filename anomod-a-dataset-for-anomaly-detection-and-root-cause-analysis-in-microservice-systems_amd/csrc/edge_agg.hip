@@ -89,6 +89,7 @@ struct Table {
   unsigned long long* sum;   // [E]
   unsigned int* mn;          // [E]
   unsigned int* mx;          // [E]
+  unsigned long long* ctr;   // trace-segment counter of the dynamic tail (zeroed per launch)
 };
 
 struct Cols {
@@ -376,9 +377,21 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   unsigned char* wsm = smem + kOffWave + wid * kWBytes;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-  const uint64_t t_begin = uniform64(n_traces * gw / nw);
-  const uint64_t t_end = uniform64(n_traces * (gw + 1) / nw);
+#ifndef ANOMOD_DYN
+#define ANOMOD_DYN 4
+#endif
+  // Static share: the first n_static traces split evenly over the waves; with
+  // ANOMOD_DYN = d > 0 the last 1/d of the traces are handed out in segments
+  // of kDynSeg from a global counter, so waves that finish early take the tail.
+#ifndef ANOMOD_DYN_SEG
+#define ANOMOD_DYN_SEG 512
+#endif
+  constexpr uint64_t kDynSeg = ANOMOD_DYN_SEG;
+  const uint64_t n_static = ANOMOD_DYN ? n_traces - n_traces / (ANOMOD_DYN ? ANOMOD_DYN : 1) : n_traces;
+  uint64_t t_begin = uniform64(n_static * gw / nw);
+  uint64_t t_end = uniform64(n_static * (gw + 1) / nw);
 
+  while (true) {
   if (t_begin < t_end) {
     // Pipeline: the bounds of chunk c+2 and the span columns of chunk c+1 are
     // in flight while chunk c is resolved and recorded.
@@ -408,6 +421,14 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       cur = nxt;
       R = Rn;
     }
+  }
+  if (!ANOMOD_DYN || n_static == n_traces) break;
+  unsigned long long g = 0;
+  if (lane == 0) g = atomicAdd(tab.ctr, (unsigned long long)kDynSeg);
+  g = __shfl(g, 0);
+  t_begin = uniform64(n_static + g);
+  if (t_begin >= n_traces) break;
+  t_end = uniform64(t_begin + kDynSeg < n_traces ? t_begin + kDynSeg : n_traces);
   }
   __syncthreads();
 
@@ -513,16 +534,17 @@ KernelFn pick_kernel(uint32_t E, const char** name) {
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
 // all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
-// count | p50 | p99 | mn.  [off_err, bytes) is copied to the host in one D2H.
+// ctr (u64, zeroed with them) | count | p50 | p99 | mn.  [off_err, bytes) is copied to the host in one D2H.
 struct Layout {
   uint64_t E;
-  size_t off_hist, off_err, off_sum, off_mx, off_count, off_p50, off_p99, off_mn, bytes;
+  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_count, off_p50, off_p99, off_mn, bytes;
   explicit Layout(uint64_t e) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
     off_sum = off_err + E * 8;
     off_mx = off_sum + E * 8;
-    off_count = (off_mx + E * 4 + 7) & ~size_t(7);
+    off_ctr = (off_mx + E * 4 + 7) & ~size_t(7);
+    off_count = off_ctr + 8;
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
@@ -559,11 +581,12 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.sum = reinterpret_cast<unsigned long long*>(base + L.off_sum);
   tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
   tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
+  tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
   auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
   auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
   auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
 
-  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx
+  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx|ctr
   ANOMOD_HIP(ctx, hipMemsetAsync(tab.mn, 0xFF, E * 4ull, ctx->stream));
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
