@@ -78,6 +78,7 @@ struct TsOut {
   uint32_t words;                // ceil(S / 64)
   int* scr_f;                    // big traces only: node (first span) of each span
   int* scr_pf;                   // big traces only: first span of its own parent ref
+  unsigned long long* ctr;       // trace-segment counter of the dynamic tail (zeroed per launch)
 };
 
 // One ordered pass over [a, b), kTsScan ids per step (ds_read2_b64 from the
@@ -410,9 +411,7 @@ __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4)))
   unsigned char* wsm = smem + wid * kTBytes;
   const uint64_t gw = (uint64_t)blockIdx.x * kTsWaves + wid;
   const uint64_t nw = (uint64_t)gridDim.x * kTsWaves;
-  const uint64_t t_end = uniform64(n_traces * (gw + 1) / nw);
-  const uint64_t t_begin = uniform64(n_traces * gw / nw);
-  if (t_begin >= t_end) return;
+  auto run = [&](const uint64_t t_begin, const uint64_t t_end) __attribute__((always_inline)) {
   // Software pipeline (as the edge kernel): the bounds of chunk c+2 and the
   // span columns of chunk c+1 are in flight while chunk c is resolved.
   auto load_cols = [&](const Chunk& c, uint64_t (&sid)[kPer], uint64_t (&pid)[kPer],
@@ -462,6 +461,30 @@ __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4)))
       svc[r] = svc_n[r];
     }
   }
+  };
+#ifndef ANOMOD_TS_DYN
+#define ANOMOD_TS_DYN 2
+#endif
+#ifndef ANOMOD_TS_DYN_SEG
+#define ANOMOD_TS_DYN_SEG 512
+#endif
+  // As the edge kernel: a static share per wave, then the last 1/ANOMOD_TS_DYN
+  // of the traces in segments of kDynSeg from a global counter.
+  constexpr uint64_t kDynSeg = ANOMOD_TS_DYN_SEG;
+  const uint64_t n_static =
+      ANOMOD_TS_DYN ? n_traces - n_traces / (ANOMOD_TS_DYN ? ANOMOD_TS_DYN : 1) : n_traces;
+  uint64_t t_begin = uniform64(n_static * gw / nw);
+  uint64_t t_end = uniform64(n_static * (gw + 1) / nw);
+  while (true) {
+    if (t_begin < t_end) run(t_begin, t_end);
+    if (!ANOMOD_TS_DYN || n_static == n_traces) break;
+    unsigned long long g = 0;
+    if (lane == 0) g = atomicAdd(o.ctr, (unsigned long long)kDynSeg);
+    g = __shfl(g, 0);
+    t_begin = uniform64(n_static + g);
+    if (t_begin >= n_traces) break;
+    t_end = uniform64(t_begin + kDynSeg < n_traces ? t_begin + kDynSeg : n_traces);
+  }
 }
 
 }  // namespace
@@ -489,7 +512,8 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   const size_t off_mask = (off_roots + nt * 4 + 7) & ~(size_t)7;
   // + scratch for traces longer than a chunk: (own node, parent's node) per span
   const size_t off_scr = (off_mask + nt * words * 8 + 15) & ~(size_t)15;
-  const size_t bytes = off_scr + n * 8 + 8;
+  const size_t off_ctr = off_scr + n * 8 + 8;
+  const size_t bytes = off_ctr + 8;
   char* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) {
     set_error(ctx, "hipMalloc(%zu) for trace-structure outputs failed", bytes);
@@ -502,6 +526,7 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   };
   hipError_t e = hipMemsetAsync(d + off_cnt, 0, n * 4, ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(d + off_mask, 0, nt * words * 8, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d + off_ctr, 0, 8, ctx->stream);
   if (e != hipSuccess) return fail(e, "hipMemsetAsync");
   TsOut o;
   o.parent_pos = reinterpret_cast<uint32_t*>(d);
@@ -513,6 +538,7 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   o.words = words;
   o.scr_f = reinterpret_cast<int*>(d + off_scr);
   o.scr_pf = reinterpret_cast<int*>(d + off_scr + n * 4);
+  o.ctr = reinterpret_cast<unsigned long long*>(d + off_ctr);
   if (int rc = stage_begin(ctx, kStageTraceStruct)) {
     (void)hipFree(d);
     return rc;
