@@ -73,6 +73,19 @@ def test_random_sets_bit_exact(ctx, S, n_traces, max_len):
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
 
 
+@pytest.mark.parametrize("n_traces", [1, 511, 513, 16387, (1 << 20) + 1])
+def test_dynamic_tail_segments_bit_exact(ctx, n_traces):
+    """The kernel splits the first 3/4 of the traces statically over its waves
+    and hands the last 1/4 out in 512-trace segments from a device counter:
+    every trace is counted exactly once at counts around those boundaries
+    (fewer traces than waves, one segment and a bit, many segments)."""
+    rng = np.random.default_rng(n_traces)
+    sp = _random_spanset(rng, 12, n_traces, 6, dup=0.01)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+    again = ctx.edge_aggregate(sp)  # the counter is re-zeroed per launch
+    assert_table_equal(again, native.edge_aggregate(sp))
+
+
 @pytest.mark.parametrize("S,max_len", [(12, 40), (46, 60)])
 def test_low_word_aliases(ctx, S, max_len):
     """Span ids sharing their low 32-bit word inside a trace: the kernel scans

@@ -129,6 +129,16 @@ def test_gpu_random_sets_bit_exact(ctx, S, n_traces, max_len):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_traces", [1, 513, (1 << 19) + 3])
+def test_gpu_dynamic_tail_segments_bit_exact(ctx, n_traces):
+    """The second half of the traces goes out in 512-trace segments from a
+    device counter (re-zeroed per call): each trace resolved exactly once."""
+    sp = _random_set(np.random.default_rng(n_traces), 12, n_traces, 6)
+    _gpu_equal(ctx, sp)
+    _gpu_equal(ctx, sp)
+
+
+@pytest.mark.gpu
 def test_gpu_big_traces_and_empty(ctx):
     rng = np.random.default_rng(9)
     parts = [_random_set(rng, 12, 40, 10), _random_set(rng, 12, 2, 900),
