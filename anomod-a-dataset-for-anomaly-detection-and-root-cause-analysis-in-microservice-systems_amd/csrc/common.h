@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "../../include/anomod.h"
 
@@ -34,6 +35,10 @@ struct anomod_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1;
   int rank = 0;
+  bool comm_aborted = false;   // set once the communicator was aborted
+  double comm_timeout_s = 300; // ANOMOD_RCCL_TIMEOUT_S
+  int* d_status = nullptr;     // device word of the status agreement
+  int* h_status = nullptr;     // pinned host twin
   // Cached device workspace for the edge table.
   void* d_table = nullptr;
   size_t table_bytes = 0;
@@ -47,6 +52,8 @@ struct anomod_spans {
   uint64_t n_spans = 0;
   uint64_t n_traces = 0;
   uint32_t max_svc = 0;      // largest service index present (host-validated)
+  bool grouped = true;       // false: spans in arrival order, trace_ptr = NULL
+                             // (anomod_spans_upload_ungrouped; group first)
   uint64_t* trace_hash = nullptr;
   uint64_t* span_id = nullptr;
   uint64_t* parent_span_id = nullptr;
@@ -83,6 +90,17 @@ struct anomod_spans {
     }                                                                                       \
   } while (0)
 
+// ANOMOD_REQUIRE for the checks before a collective: instead of returning,
+// record the first failure in `local` (passed to comm_agree afterwards, so
+// the other ranks learn of it instead of waiting in the collective).
+#define ANOMOD_CHECK_LOCAL(ctx, local, cond, ...)                                           \
+  do {                                                                                      \
+    if ((local) == ANOMOD_OK && !(cond)) {                                                  \
+      anomod::set_error((ctx), __VA_ARGS__);                                                \
+      (local) = ANOMOD_EINVAL;                                                              \
+    }                                                                                       \
+  } while (0)
+
 namespace anomod {
 
 // Make ctx's device current on this host thread.
@@ -90,6 +108,22 @@ int bind(anomod_ctx* ctx);
 // hipEvent bracketing of a stage on the ctx stream.
 int stage_begin(anomod_ctx* ctx, Stage s);
 int stage_end(anomod_ctx* ctx, Stage s);
+// Wait for the ctx stream.  With a communicator attached, RCCL's async
+// error state is polled while waiting and the communicator is aborted on an
+// error or after ctx->comm_timeout_s (a dead peer must not hang the rank).
+int stream_wait(anomod_ctx* ctx);
+// Status agreement before a collective: every rank passes its local status
+// (ANOMOD_OK or an error it would otherwise return early with) and gets back
+// ANOMOD_OK only when every rank is OK — so either all ranks enter the data
+// collective or none does.  A no-op returning local_rc without a communicator.
+int comm_agree(anomod_ctx* ctx, int local_rc);
+// Trace cut points 0 = c_0 < ... < c_k = n_traces of a span set such that
+// every range [c_i, c_{i+1}) holds at most max_spans spans or is a single
+// trace (kernels with per-workgroup u32 counters launch once per range).
+// 2^31, or ANOMOD_MAX_LAUNCH_SPANS (tests: forces the multi-launch path).
+uint64_t max_launch_spans();
+int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
+                     std::vector<uint64_t>& cuts);
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
 int ensure_host_stage(anomod_ctx* ctx, size_t bytes);

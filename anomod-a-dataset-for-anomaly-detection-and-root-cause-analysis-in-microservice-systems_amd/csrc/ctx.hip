@@ -4,8 +4,11 @@
 // backend: None"; its only concurrency is the HTTP ThreadPoolExecutor of
 // trace_collector.py:519-531).  Here one process drives one GPU and the
 // integer edge tables of all ranks are summed with RCCL over xGMI.
+#include <chrono>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "common.h"
 
@@ -38,6 +41,125 @@ int stage_begin(anomod_ctx* ctx, Stage s) {
 int stage_end(anomod_ctx* ctx, Stage s) {
   ANOMOD_HIP(ctx, hipEventRecord(ctx->ev_end[s], ctx->stream));
   ctx->stage_recorded[s] = true;
+  return ANOMOD_OK;
+}
+
+namespace {
+void abort_comm(anomod_ctx* ctx) {
+  if (ctx->comm && !ctx->comm_aborted) {
+    ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;  // an aborted communicator is not destroyed again
+    ctx->comm_aborted = true;
+  }
+}
+}  // namespace
+
+int stream_wait(anomod_ctx* ctx) {
+  if (!ctx->comm) {
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return ANOMOD_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 0;; ++spin) {
+    const hipError_t q = hipStreamQuery(ctx->stream);
+    if (q == hipSuccess) return ANOMOD_OK;
+    if (q != hipErrorNotReady) {
+      set_error(ctx, "stream failed while waiting on a collective: %s", hipGetErrorString(q));
+      abort_comm(ctx);
+      return ANOMOD_EHIP;
+    }
+    ncclResult_t ar = ncclSuccess;
+    const ncclResult_t qr = ncclCommGetAsyncError(ctx->comm, &ar);
+    if (qr != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress)) {
+      set_error(ctx, "RCCL async error on rank %d of %d: %s; communicator aborted", ctx->rank,
+                ctx->nranks, ncclGetErrorString(qr != ncclSuccess ? qr : ar));
+      abort_comm(ctx);
+      return ANOMOD_ERCCL;
+    }
+    const double el =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > ctx->comm_timeout_s) {
+      set_error(ctx, "collective on rank %d of %d did not finish within %.0f s "
+                "(ANOMOD_RCCL_TIMEOUT_S): a peer is gone or stuck; communicator aborted",
+                ctx->rank, ctx->nranks, ctx->comm_timeout_s);
+      abort_comm(ctx);
+      return ANOMOD_ERCCL;
+    }
+    if (spin > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+int comm_agree(anomod_ctx* ctx, int local_rc) {
+  if (!ctx->comm) {
+    if (ctx->comm_aborted && local_rc == ANOMOD_OK) {
+      set_error(ctx, "the communicator of this context was aborted after an earlier failure");
+      return ANOMOD_ERCCL;
+    }
+    return local_rc;
+  }
+  const std::string local_msg = ctx->err;
+  *ctx->h_status = local_rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->d_status, ctx->h_status, sizeof(int),
+                                 hipMemcpyHostToDevice, ctx->stream));
+  // statuses are <= 0: the minimum is an error whenever any rank has one
+  ANOMOD_RCCL(ctx, ncclAllReduce(ctx->d_status, ctx->d_status, 1, ncclInt32, ncclMin, ctx->comm,
+                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_status, ctx->d_status, sizeof(int),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+  if (int rc = stream_wait(ctx)) return rc;
+  const int agreed = *ctx->h_status;
+  if (local_rc != ANOMOD_OK) {
+    ctx->err = local_msg;  // this rank's own reason
+    return local_rc;
+  }
+  if (agreed != ANOMOD_OK) {
+    set_error(ctx, "another rank failed before the collective (status %d); "
+              "this rank skipped it too", agreed);
+    return agreed;
+  }
+  return ANOMOD_OK;
+}
+
+uint64_t max_launch_spans() {  // read per call: tests lower it at run time
+  const char* e = getenv("ANOMOD_MAX_LAUNCH_SPANS");
+  const unsigned long long x = e ? strtoull(e, nullptr, 10) : 0ull;
+  return x > 0 && x < (1ull << 31) ? (uint64_t)x : (uint64_t)(1ull << 31);
+}
+
+int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
+                     std::vector<uint64_t>& cuts) {
+  cuts.assign(1, 0);
+  if (s->n_spans <= max_spans) {
+    cuts.push_back(s->n_traces);
+    return ANOMOD_OK;
+  }
+  // Binary searches over the device trace_ptr, one u64 read back per probe
+  // (only sets of >= 2^31 spans get here).
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  auto at = [&](uint64_t t, uint64_t* v) -> int {
+    ANOMOD_HIP(ctx, hipMemcpy(v, s->trace_ptr + t, 8, hipMemcpyDeviceToHost));
+    return ANOMOD_OK;
+  };
+  uint64_t cur = 0, pcur = 0;
+  while (cur < s->n_traces) {
+    uint64_t lo = cur + 1, hi = s->n_traces;  // largest t in [lo, hi] with ptr[t] - pcur <= max
+    uint64_t v = 0;
+    if (int rc = at(lo, &v)) return rc;
+    if (v - pcur > max_spans) {  // one trace alone exceeds the bound
+      ANOMOD_REQUIRE(ctx, v - pcur < (1ull << 32), "trace %llu holds %llu >= 2^32 spans",
+                     (unsigned long long)cur, (unsigned long long)(v - pcur));
+      hi = lo;
+    } else {
+      while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo + 1) / 2;
+        if (int rc = at(mid, &v)) return rc;
+        if (v - pcur <= max_spans) lo = mid; else hi = mid - 1;
+      }
+    }
+    cuts.push_back(hi);
+    if (int rc = at(hi, &pcur)) return rc;
+    cur = hi;
+  }
   return ANOMOD_OK;
 }
 
@@ -134,6 +256,8 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->d_status) (void)hipFree(ctx->d_status);
+  if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->d_table) (void)hipFree(ctx->d_table);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (int s = 0; s < anomod::kNumStages; ++s) {
@@ -190,8 +314,17 @@ int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks
   ANOMOD_REQUIRE(nullptr, ctx && unique_id, "anomod_ctx_attach_comm: NULL argument");
   ANOMOD_REQUIRE(ctx, nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d of %d", rank,
                  nranks);
-  ANOMOD_REQUIRE(ctx, ctx->comm == nullptr, "ctx already has a communicator");
+  ANOMOD_REQUIRE(ctx, ctx->comm == nullptr && !ctx->comm_aborted,
+                 "ctx already has (or had) a communicator");
   if (int rc = anomod::bind(ctx)) return rc;
+  if (!ctx->d_status) ANOMOD_HIP(ctx, hipMalloc(&ctx->d_status, sizeof(int)));
+  if (!ctx->h_status)
+    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_status), sizeof(int),
+                                  hipHostMallocDefault));
+  if (const char* t = getenv("ANOMOD_RCCL_TIMEOUT_S")) {
+    const double v = atof(t);
+    if (v > 0) ctx->comm_timeout_s = v;
+  }
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
   ANOMOD_RCCL(ctx, ncclCommInitRank(&ctx->comm, nranks, id, rank));

@@ -562,18 +562,27 @@ extern "C" {
 int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S,
                                 anomod_edge_table* out) {
   ANOMOD_REQUIRE(nullptr, ctx && spans && out, "anomod_edge_aggregate_spans: NULL argument");
-  ANOMOD_REQUIRE(ctx, S >= 1 && S <= 4096, "n_services=%u out of range [1, 4096]", S);
-  ANOMOD_REQUIRE(ctx, out->n_services == S, "out->n_services=%u != n_services=%u",
-                 out->n_services, S);
-  ANOMOD_REQUIRE(ctx, out->n_bins == kBins, "out->n_bins=%u != ANOMOD_HIST_BINS=%u", out->n_bins,
-                 kBins);
-  ANOMOD_REQUIRE(ctx, spans->device == ctx->device, "span set lives on another device");
-  ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < S,
-                 "span service index %u >= n_services %u", spans->max_svc, S);
-  if (int rc = bind(ctx)) return rc;
+  // Every check that can fail on one rank only (a shard's data, memory)
+  // feeds the status agreement instead of returning early: with a
+  // communicator attached the other ranks would otherwise wait in the
+  // all-reduce below forever.
+  int local = ANOMOD_OK;
+  ANOMOD_CHECK_LOCAL(ctx, local, S >= 1 && S <= 4096, "n_services=%u out of range [1, 4096]", S);
+  ANOMOD_CHECK_LOCAL(ctx, local, out->n_services == S, "out->n_services=%u != n_services=%u",
+                     out->n_services, S);
+  ANOMOD_CHECK_LOCAL(ctx, local, out->n_bins == kBins, "out->n_bins=%u != ANOMOD_HIST_BINS=%u",
+                     out->n_bins, kBins);
+  ANOMOD_CHECK_LOCAL(ctx, local, spans->device == ctx->device, "span set lives on another device");
+  ANOMOD_CHECK_LOCAL(ctx, local, spans->grouped, "span set is not grouped by trace: "
+                     "anomod_spans_group first (or anomod_edge_aggregate_ungrouped)");
+  ANOMOD_CHECK_LOCAL(ctx, local, spans->n_spans == 0 || spans->max_svc < S,
+                     "span service index %u >= n_services %u", spans->max_svc, S);
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
   const Layout L(E);
-  if (int rc = ensure_table(ctx, L.bytes)) return rc;
+  if (local == ANOMOD_OK) local = bind(ctx);
+  if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
+  if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.bytes - L.off_err);
+  if (int rc = comm_agree(ctx, local)) return rc;
   char* base = static_cast<char*>(ctx->d_table);
   Table tab;
   tab.hist = reinterpret_cast<unsigned long long*>(base + L.off_hist);
@@ -593,19 +602,24 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   if (spans->n_traces > 0) {
     const char* kname = nullptr;
     KernelFn fn = pick_kernel(E, &kname);
-    // As many workgroups as are resident at once (LDS / registers decide:
-    // one or two per CU); more only to keep a workgroup's u32 LDS counters
-    // (errors, min, max) far from 2^32 spans.
+    // As many workgroups as are resident at once (LDS / registers decide).
     int per_cu = 0;
     ANOMOD_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
                         &per_cu, reinterpret_cast<const void*>(fn), kThreads, 0));
-    uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
-    const uint64_t per_wg_cap = 1ull << 30;
-    if (spans->n_spans / grid > per_wg_cap) grid = (spans->n_spans + per_wg_cap - 1) / per_wg_cap;
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
-                       spans->parent_span_id, spans->svc_flags, spans->dur_us, spans->trace_ptr,
-                       spans->n_traces, S, E, tab);
-    ANOMOD_HIP(ctx, hipGetLastError());
+    const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
+    // A workgroup's LDS counters (histogram slots, errors) are u32 and the
+    // dynamic tail may hand one workgroup any share of a launch, so a launch
+    // covers < 2^32 spans: larger sets run as several launches over whole
+    // trace ranges (split on the device trace_ptr; one launch below 2^31).
+    std::vector<uint64_t> cuts;
+    if (int rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts)) return rc;
+    for (size_t k = 0; k + 1 < cuts.size(); ++k) {
+      if (k > 0) ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
+      hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
+                         spans->parent_span_id, spans->svc_flags, spans->dur_us,
+                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tab);
+      ANOMOD_HIP(ctx, hipGetLastError());
+    }
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
 
@@ -632,13 +646,12 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   // The per-edge vectors come back in one D2H into pinned staging, then
   // fan out on the host; the histogram (when asked for) goes straight.
   const size_t small = L.bytes - L.off_err;
-  if (int rc = ensure_host_stage(ctx, small)) return rc;
   ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, base + L.off_err, small, hipMemcpyDeviceToHost,
                                  ctx->stream));
   if (out->hist)
     ANOMOD_HIP(ctx, hipMemcpyAsync(out->hist, tab.hist, (size_t)E * kBins * 8ull,
                                    hipMemcpyDeviceToHost, ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = stream_wait(ctx)) return rc;
   const char* hs = static_cast<const char*>(ctx->h_stage);
   auto fan = [&](void* dst, size_t off, size_t bytes) {  // off: device layout offset
     if (dst) memcpy(dst, hs + (off - L.off_err), bytes);

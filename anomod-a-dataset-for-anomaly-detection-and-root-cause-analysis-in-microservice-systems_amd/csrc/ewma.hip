@@ -708,10 +708,36 @@ int anomod_ewma_z(anomod_ctx* ctx, const float* X, uint64_t T, uint64_t S, float
   ANOMOD_REQUIRE(ctx, W >= 1 && T % W == 0, "T=%llu must be a multiple of W=%u",
                  (unsigned long long)T, W);
   if (T == 0 || S == 0) return ANOMOD_OK;
+  if (int rc = bind(ctx)) return rc;
+  // X may exceed HBM (config 4: 10^5 series x 10^6 steps = 400 GB on a
+  // 288 GB GPU): stream it through one device series in chunks of Tc steps
+  // with the (m, v, n) state carried — Tc a multiple of 16 (tiles) and of the
+  // time-parallel sub-chunk U (a multiple of W), so the chunked scores equal
+  // the one-pass scores bit for bit.
+  const uint32_t cap = W <= 64 ? 64u : 128u;
+  const uint64_t U = W <= 128 ? (uint64_t)W * (cap / W) : (uint64_t)W;
+  uint64_t q = U;
+  while (q % kTile) q += U;  // lcm(U, 16)
+  size_t free_b = 0, total_b = 0;
+  ANOMOD_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  // X, a possible re-layout copy of X and the window scores must fit, plus
+  // 2 GiB for the upload staging and everything else
+  const double per_step = (double)S * 4.0 * 2.0 + (double)S * 4.0 / W;
+  const double avail = (double)free_b - (double)(2ull << 30);
+  uint64_t Tc = avail > per_step * q ? (uint64_t)(avail / per_step) / q * q : q;
+  if (const char* e = getenv("ANOMOD_EWMA_CHUNK_STEPS")) {  // tests: force chunking
+    const unsigned long long f = strtoull(e, nullptr, 10);
+    if (f > 0) Tc = ((f + q - 1) / q) * q;
+  }
+  if (Tc >= T) Tc = T;
   anomod_series* ser = nullptr;
-  if (int rc = anomod_series_create(ctx, T, S, &ser)) return rc;
-  int rc = anomod_series_upload(ctx, ser, X);
-  if (rc == ANOMOD_OK) rc = anomod_series_ewma_z(ctx, ser, alpha, W, eps, Z);
+  if (int rc = anomod_series_create(ctx, Tc, S, &ser)) return rc;
+  int rc = ANOMOD_OK;
+  for (uint64_t t0 = 0; t0 < T && rc == ANOMOD_OK; t0 += Tc) {
+    ser->T = T - t0 < Tc ? T - t0 : Tc;  // the last chunk reuses the allocation
+    rc = anomod_series_upload(ctx, ser, X + t0 * S);
+    if (rc == ANOMOD_OK) rc = anomod_series_ewma_z(ctx, ser, alpha, W, eps, Z + (t0 / W) * S);
+  }
   free_series(ser);
   return rc;
 }

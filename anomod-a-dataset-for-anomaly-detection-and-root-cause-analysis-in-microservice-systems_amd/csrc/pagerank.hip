@@ -845,22 +845,31 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
   ANOMOD_REQUIRE(ctx, alpha > 0.0 && alpha < 1.0, "alpha=%g outside (0, 1)", alpha);
   ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
   ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
-  const bool ranks = ctx->comm != nullptr;
+  const bool ranks = ctx->comm != nullptr || ctx->comm_aborted;
   ANOMOD_REQUIRE(ctx, !ranks || virtual_shards <= 1,
                  "virtual_shards=%u needs a context without a communicator", virtual_shards);
   const uint32_t G = ranks ? (uint32_t)ctx->nranks : (virtual_shards ? virtual_shards : 1u);
   ANOMOD_REQUIRE(ctx, G <= 4096, "%u shards", G);
   const uint32_t N = g->N;
+  // Checks that can fail on one rank only go through the status agreement
+  // (the other ranks would otherwise wait in the first exchange forever).
+  int local = ANOMOD_OK;
   double psum = 0.0;
-  for (uint32_t i = 0; i < N; ++i) {
-    ANOMOD_REQUIRE(ctx, std::isfinite(p[i]) && p[i] >= 0.0, "personalization[%u] invalid", i);
+  for (uint32_t i = 0; i < N && local == ANOMOD_OK; ++i) {
+    ANOMOD_CHECK_LOCAL(ctx, local, std::isfinite(p[i]) && p[i] >= 0.0,
+                       "personalization[%u] invalid", i);
     psum += p[i];
   }
-  ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
+  ANOMOD_CHECK_LOCAL(ctx, local, psum > 0.0, "personalization sums to zero");
   std::vector<double> pn(p, p + N);
   for (double& v : pn) v /= psum;
-  if (int rc = bind(ctx)) return rc;
-  if (int rc = ensure_shard_x(ctx, g, G)) return rc;
+  if (local == ANOMOD_OK) local = bind(ctx);
+  if (local == ANOMOD_OK) local = ensure_shard_x(ctx, g, G);
+  if (ranks) {
+    if (int rc = comm_agree(ctx, local)) return rc;
+  } else if (local != ANOMOD_OK) {
+    return local;
+  }
   ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, pn.data(), N * 8ull, hipMemcpyHostToDevice, ctx->stream));
   for (unsigned long long& v : g->host_acc) v = 0ull;
   g->host_acc[0] = (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
@@ -909,7 +918,7 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
       unsigned long long* eh = g->host_acc.data() + (3 + w) * S;
       ANOMOD_HIP(ctx, hipMemcpyAsync(eh, A + (3 + w) * S, S * 8, hipMemcpyDeviceToHost,
                                      ctx->stream));
-      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      if (int rc = stream_wait(ctx)) return rc;
       unsigned long long et = 0;
       for (int i = 0; i < S; ++i) et += eh[i];
       if ((double)et * (1.0 / kEScale) < (double)N * tol) {
@@ -921,7 +930,7 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
   if (int rc = stage_end(ctx, kStagePagerank)) return rc;
   ANOMOD_HIP(ctx, hipMemcpyAsync(x_out, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
                                  ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = stream_wait(ctx)) return rc;
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;
 }

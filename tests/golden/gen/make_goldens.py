@@ -31,6 +31,10 @@ inputs and the outputs the reference computed from them are written.
       synthetic Prometheus query_range results -> TT_collection-scripts/
       T-Dataset/metric_collector.py MetricCollector.collect_experiment_metrics_csv
       (the HTTP query, boot-time probe and sleeps replaced by stubs; TZ=UTC)
+  prom_dir/*.csv / prom_results.json
+      synthetic Prometheus query_range results -> SN_collection-scripts/
+      Dataset/metric_data/fetch_prometheus_metrics.py fetch_prometheus_metrics
+      (requests.get stubbed) -> df.to_csv as its main() writes it (TZ=UTC)
   ewma_pandas.npz        pandas Series.ewm(alpha, adjust=False) mean/var
   pagerank_networkx.npz  networkx.pagerank (3.4.2, scipy backend)
 
@@ -530,9 +534,118 @@ def metric_long_golden(results: dict, out_csv: Path) -> None:
         Path(out_csv).write_bytes(Path(path).read_bytes())
 
 
+# ---------------------------------------------------------------------------
+# SN metric directory (fetch_prometheus_metrics.py:9-80 + main :92-102,
+# one CSV per query as collect_metric.sh:24-125 names them)
+# ---------------------------------------------------------------------------
+def sn_prometheus_results(seed: int = 31) -> dict:
+    """Synthetic query_range answers for SN queries (file stem -> result
+    list): several series per query with differing label sets, fractional
+    timestamps, 'NaN' / '+Inf' / '-Inf' samples, tiny and huge values, a
+    series with an empty label dict, label values holding commas and quotes,
+    series of different lengths and offsets, and a no-data query (no file)."""
+    rng = random.Random(seed)
+    t0 = 1762207375.0  # 2025-11-03 22:02:55 UTC
+
+    def values(n, start=0, frac=0.0, nan_p=0.05, scale=1.0, specials=()):
+        out = []
+        for k in range(n):
+            ts = t0 + 15 * (start + k) + frac
+            r = rng.random()
+            if r < nan_p:
+                v = "NaN"
+            else:
+                v = repr(round(rng.uniform(0, 100) * scale, 9))
+            out.append([ts, v])
+        for k, v in specials:
+            out[k][1] = v
+        return out
+
+    svc = "container_label_com_docker_compose_service"
+    res = {}
+    res["socialnet_container_cpu"] = [
+        {"metric": {svc: s}, "values": values(20, nan_p=0.1, scale=0.01)}
+        for s in ("compose-post-service", "media-service", "user-timeline-service")]
+    res["socialnet_container_memory"] = [
+        {"metric": {"__name__": "container_memory_usage_bytes", svc: "post-storage-mongodb",
+                    "container_label_com_docker_compose_project": "socialnetwork",
+                    "id": "/docker/1f2e", "image": "mongo:4.4.6", "instance": "cadvisor:8080",
+                    "job": "cadvisor", "name": "socialnetwork-post-storage-mongodb-1"},
+         "values": values(20, scale=1e7, specials=((3, "+Inf"), (4, "-Inf")))},
+        {"metric": {"__name__": "container_memory_usage_bytes", svc: "text-service",
+                    "instance": "cadvisor:8080", "job": "cadvisor"},
+         "values": values(12, start=5, scale=1e7)},
+    ]
+    # fractional timestamps (a window not aligned to whole seconds)
+    res["socialnet_container_network_receive"] = [
+        {"metric": {svc: "nginx-thrift"}, "values": values(16, frac=0.5, scale=1e3)},
+        {"metric": {svc: "home-timeline-service"}, "values": values(16, frac=0.5, nan_p=0.3)},
+    ]
+    # an aggregate without labels ('metric' = '') and label values with
+    # commas and quotes
+    res["mongodb_operations_rate"] = [
+        {"metric": {}, "values": values(10, scale=1e-6)},
+        {"metric": {"type": "query,insert", "note": 'say "hi"'}, "values": values(10, start=3)},
+    ]
+    res["microservice_request_rate"] = []  # no data -> no file (fetch_prometheus_metrics.py:101-102)
+    return res
+
+
+def sn_prometheus_golden(results: dict, out_dir: Path) -> None:
+    """Run the reference fetch_prometheus_metrics() with requests.get stubbed
+    and write each DataFrame as its main() does (df.to_csv(index=False))."""
+    os.environ["TZ"] = "UTC"
+    import time
+    time.tzset()
+    sys.path.insert(0, str(REF / "SN_collection-scripts/Dataset/metric_data"))
+    try:
+        import fetch_prometheus_metrics as fpm  # noqa: E402  (reference, run time only)
+    finally:
+        sys.path.pop(0)
+
+    class _Resp:
+        def __init__(self, payload):
+            self.payload = payload
+
+        def raise_for_status(self):
+            return None
+
+        def json(self):
+            return self.payload
+
+    current = {}
+
+    def fake_get(url, params=None, **kw):
+        return _Resp({"status": "success",
+                      "data": {"resultType": "matrix", "result": current["result"]}})
+
+    out_dir.mkdir(parents=True, exist_ok=True)
+    for old in out_dir.glob("*.csv"):
+        old.unlink()
+    real_requests = fpm.requests
+    fpm.requests = types.SimpleNamespace(get=fake_get, exceptions=real_requests.exceptions)
+    try:
+        for stem, result in results.items():
+            current["result"] = result
+            df = fpm.fetch_prometheus_metrics(stem, int(t0_of(result)), int(t0_of(result)) + 3600,
+                                              "15s", "http://prometheus.invalid:9090")
+            if df is not None:
+                df.to_csv(out_dir / f"{stem}.csv", index=False)
+    finally:
+        fpm.requests = real_requests
+
+
+def t0_of(result) -> float:
+    return min((v[0][0] for r in result for v in [r["values"]] if v), default=0.0)
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only in (None, "prom"):
+        res = sn_prometheus_results()
+        (OUT / "prom_results.json").write_text(json.dumps(res))
+        sn_prometheus_golden(res, OUT / "prom_dir")
     if only in (None, "metric"):
         res = prometheus_results()
         (OUT / "metric_results.json").write_text(json.dumps(res))

@@ -133,3 +133,46 @@ def test_metric_long_csv_dedup_and_nan():
     assert col[0] == 10 and np.isnan(col[1]) and col[2] == 40
     padded = mm.pad_to_multiple(2)
     assert padded.T == 4 and np.isnan(padded.X[3]).all()
+
+
+def _prom_expected(results: dict):
+    """Series of the SN metric directory derived from the stubbed Prometheus
+    answers themselves: key (file stem, label string as
+    fetch_prometheus_metrics.py:51 renders it) -> {epoch: value}."""
+    exp = {}
+    for stem, result in results.items():
+        for r in result:
+            labels = ",".join(f'{k}="{v}"' for k, v in r.get("metric", {}).items())
+            exp[(stem, (("metric", labels),))] = {float(t): float(v) for t, v in r["values"]}
+    return exp
+
+
+def test_prometheus_dir_matches_reference_csvs(golden, monkeypatch):
+    """decode_prometheus_csv_dir on the CSVs the reference's
+    fetch_prometheus_metrics() + to_csv wrote (tests/golden/prom_dir, TZ=UTC)
+    is column-equal to the query answers that produced them."""
+    import time
+    monkeypatch.setenv("TZ", "UTC")
+    time.tzset()
+    try:
+        results = json.loads((golden / "prom_results.json").read_text())
+        files = sorted(p.stem for p in (golden / "prom_dir").glob("*.csv"))
+        # the no-data query writes no file (fetch_prometheus_metrics.py:101-102)
+        assert files == sorted(s for s, r in results.items() if r)
+        mm = anomod.decode_prometheus_csv_dir(golden / "prom_dir")
+        exp = _prom_expected(results)
+        assert sorted(mm.series) == sorted(exp) and list(mm.series) == sorted(mm.series)
+        want_ts = sorted({t for d in exp.values() for t in d})
+        np.testing.assert_allclose(mm.timestamps, want_ts, rtol=0, atol=1e-6)
+        col_of = {t: i for i, t in enumerate(want_ts)}
+        for j, key in enumerate(mm.series):
+            want = np.full(mm.T, np.nan, np.float32)
+            for t, v in exp[key].items():
+                want[col_of[t]] = np.float32(v)
+            np.testing.assert_array_equal(mm.X[:, j], want)
+        # specials survive the CSV round trip
+        assert np.isposinf(mm.X).any() and np.isneginf(mm.X).any() and np.isnan(mm.X).any()
+        assert any(k[1][0][1] == "" for k in mm.series)  # empty label set
+    finally:
+        monkeypatch.undo()
+        time.tzset()

@@ -187,3 +187,21 @@ def test_large_synthetic_full_parity(ctx):
     np.testing.assert_array_equal(t1.hist.sum(axis=1), t1.count)
     host = dev.download()
     assert_table_equal(t1, native.edge_aggregate(host))
+
+
+@pytest.mark.parametrize("cap", [1000, 4096])
+def test_multi_launch_split_bit_exact(ctx, monkeypatch, cap):
+    """Span sets above the per-launch span bound (2^31: a workgroup's u32 LDS
+    counters must not wrap) run as several launches over whole trace ranges;
+    ANOMOD_MAX_LAUNCH_SPANS lowers the bound so the split runs here: cuts
+    inside runs of short traces, a trace longer than the bound alone, empty
+    traces at the cuts."""
+    rng = np.random.default_rng(cap)
+    parts = [_random_spanset(rng, 12, 3000, 12, dup=0.01), _random_spanset(rng, 12, 2, 5000),
+             _random_spanset(rng, 12, 700, 3), _random_spanset(rng, 12, 1, 1)]
+    sp = anomod.SpanSet.concat(parts)
+    ref = native.edge_aggregate(sp)
+    monkeypatch.setenv("ANOMOD_MAX_LAUNCH_SPANS", str(cap))
+    assert_table_equal(ctx.edge_aggregate(sp), ref)
+    monkeypatch.delenv("ANOMOD_MAX_LAUNCH_SPANS")
+    assert_table_equal(ctx.edge_aggregate(sp), ref)

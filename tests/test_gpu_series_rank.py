@@ -244,3 +244,33 @@ def test_features_and_rank_find_injected_fault(ctx):
     assert fe.window_scores is not None and fe.window_scores.shape[0] == 480 // 60
     ranking = anomod.rank(fe, ctx=ctx)
     assert anomod.hit_at(ranking, fault, 3) == 1.0
+
+
+@pytest.mark.parametrize("W", [1, 4, 15])
+def test_ewma_on_decoded_prometheus_dir(ctx, golden, ewma_mode, W):
+    """§8 row a8 end to end: the SN metric directory the reference wrote
+    (tests/golden/prom_dir: NaN gaps, ragged series, +/-inf) -> decoded
+    matrix -> EWMA/z kernel == the C oracle on the same matrix."""
+    mm = anomod.decode_prometheus_csv_dir(golden / "prom_dir").pad_to_multiple(W)
+    assert mm.S == 9 and mm.T >= 30
+    a = 2.0 / (W + 1) if W > 1 else 0.3
+    np.testing.assert_allclose(ctx.ewma_z(mm.X, a, W), native.ewma_z(mm.X, a, W),
+                               rtol=Z_RTOL, atol=Z_ATOL)
+
+
+@pytest.mark.parametrize("T,S,W,chunk", [(1920, 300, 60, 500), (4800, 77, 16, 1000),
+                                         (960, 5000, 96, 100), (1200, 40, 150, 7)])
+def test_one_shot_ewma_chunked_equals_one_pass(ctx, ewma_mode, monkeypatch, T, S, W, chunk):
+    """anomod_ewma_z streams X through HBM in T-chunks when it exceeds free
+    HBM (config 4 on one GPU); ANOMOD_EWMA_CHUNK_STEPS forces the chunking
+    here.  Cuts fall on multiples of lcm(16, U), so every kernel's chunked
+    scores equal its one-pass scores bit for bit."""
+    rng = np.random.default_rng(T * S)
+    X = (rng.uniform(0, 1e3, S) + rng.standard_normal((T, S))).astype(np.float32)
+    X[rng.random((T, S)) < 0.02] = np.nan
+    X[: T // 3, : S // 4] = np.nan  # series that start late, across chunk cuts
+    a = 2.0 / (W + 1)
+    one = ctx.ewma_z(X, a, W)
+    monkeypatch.setenv("ANOMOD_EWMA_CHUNK_STEPS", str(chunk))
+    np.testing.assert_array_equal(ctx.ewma_z(X, a, W), one)
+    np.testing.assert_allclose(one, native.ewma_z(X, a, W), rtol=Z_RTOL, atol=Z_ATOL)
