@@ -14,7 +14,7 @@ import numpy as np
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("ANOMOD_LIB", _HERE / "libanomod.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 HIST_SUB_BITS = 5
 HIST_BINS = 896
 ROOT_ROWS = 2
@@ -27,7 +27,7 @@ OK, EINVAL, EHIP, ERCCL, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
 _STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", ESTATE: "ESTATE"}
 
 (STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK,
- STAGE_TRACE_STRUCT, STAGE_SEGMENTS, STAGE_SUMMARY) = range(8)
+ STAGE_TRACE_STRUCT, STAGE_SEGMENTS, STAGE_SUMMARY, STAGE_GROUP) = range(9)
 NO_PARENT = 0xFFFFFFFF
 SPAN_ROOT, SPAN_FIRST = 0x1, 0x2
 
@@ -151,6 +151,11 @@ _SIGS = {
     "anomod_spans_info": (_i32, [_vp, _P(_u64), _P(_u64)]),
     "anomod_spans_download": (_i32, [_vp, _vp, _P(SpanSoA), _P(_u64)]),
     "anomod_spans_free": (_i32, [_vp]),
+    "anomod_spans_upload_ungrouped": (_i32, [_vp, _P(SpanSoA), _u64, _P(_vp)]),
+    "anomod_spans_grouped": (_i32, [_vp, _P(_i32)]),
+    "anomod_spans_group": (_i32, [_vp, _vp, _P(_vp)]),
+    "anomod_spans_shuffle": (_i32, [_vp, _vp, _u64, _u64, _P(_vp)]),
+    "anomod_edge_aggregate_ungrouped": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
     "anomod_synth_n_services": (_i32, [_u32, _P(_u32)]),
     "anomod_synth_service_name": (C.c_char_p, [_u32, _u32]),
     "anomod_synth_count_host": (_i32, [_P(SynthSpec), _u64, _u64, _P(_u64)]),

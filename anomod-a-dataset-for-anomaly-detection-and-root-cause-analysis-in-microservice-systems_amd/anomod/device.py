@@ -89,9 +89,11 @@ class DeviceSpans:
 
     def __init__(self, ctx: "Context", handle: C.c_void_p, services: list[str]):
         self.ctx, self.handle, self.services = ctx, handle, list(services)
-        ns, nt = C.c_uint64(), C.c_uint64()
+        ns, nt, g = C.c_uint64(), C.c_uint64(), C.c_int()
         L.check(L.lib().anomod_spans_info(handle, C.byref(ns), C.byref(nt)))
+        L.check(L.lib().anomod_spans_grouped(handle, C.byref(g)))
         self.n_spans, self.n_traces = ns.value, nt.value
+        self.grouped = bool(g.value)  # False: arrival order, traces known by trace_hash only
 
     def download(self) -> SpanSet:
         n = self.n_spans
@@ -175,6 +177,31 @@ class Context:
                                                   spans.n_traces, C.byref(h)))
         return DeviceSpans(self, h, spans.services)
 
+    def upload_ungrouped(self, spans: SpanSet) -> DeviceSpans:
+        """Upload spans in arrival order: the trace of a span is its trace_hash
+        alone (spans.trace_ptr is ignored)."""
+        h = C.c_void_p()
+        soa = spans.soa()
+        self._check(self._lib.anomod_spans_upload_ungrouped(self.handle, C.byref(soa),
+                                                            spans.n_spans, C.byref(h)))
+        return DeviceSpans(self, h, spans.services)
+
+    def group(self, spans: DeviceSpans) -> DeviceSpans:
+        """Group an ungrouped device span set by trace (segmented radix sort
+        on the GPU): traces by mix64(trace_hash), spans in arrival order."""
+        h = C.c_void_p()
+        self._check(self._lib.anomod_spans_group(self.handle, spans.handle, C.byref(h)))
+        return DeviceSpans(self, h, spans.services)
+
+    def shuffle(self, spans: DeviceSpans, seed: int, window_traces: int = 0) -> DeviceSpans:
+        """Synthetic arrival order of a grouped set: window_traces = 0 shuffles
+        spans inside each trace (stays grouped); W > 0 interleaves the spans
+        of every W consecutive traces (ungrouped result)."""
+        h = C.c_void_p()
+        self._check(self._lib.anomod_spans_shuffle(self.handle, spans.handle, seed, window_traces,
+                                                   C.byref(h)))
+        return DeviceSpans(self, h, spans.services)
+
     def generate(self, spec: SynthSpec, n_traces: int, shard: int = 0) -> DeviceSpans:
         h = C.c_void_p()
         cs = spec.c_struct()
@@ -190,8 +217,9 @@ class Context:
         try:
             table = EdgeTable.empty(spans.services, with_hist)
             cs = table.c_struct()
-            self._check(self._lib.anomod_edge_aggregate_spans(
-                self.handle, spans.handle, len(spans.services), C.byref(cs)))
+            fn = (self._lib.anomod_edge_aggregate_spans if spans.grouped
+                  else self._lib.anomod_edge_aggregate_ungrouped)
+            self._check(fn(self.handle, spans.handle, len(spans.services), C.byref(cs)))
             if table.hist is not None:
                 table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
             return table

@@ -92,6 +92,12 @@ class SpanSet:
         h[nz] = self.trace_hash[first[nz]]
         return self.select_traces((h % np.uint64(nshards)) == np.uint64(rank))
 
+    def take(self, order: np.ndarray, trace_ptr: np.ndarray) -> "SpanSet":
+        """The spans in `order`, split into traces by `trace_ptr`."""
+        return SpanSet(self.services, trace_ptr, self.trace_hash[order], self.span_id[order],
+                       self.parent_span_id[order], self.svc[order], self.flags[order],
+                       self.dur_us[order])
+
     @staticmethod
     def concat(sets: list["SpanSet"]) -> "SpanSet":
         if not sets:

@@ -17,9 +17,11 @@ namespace anomod {
 // otherwise (anomod_last_error).
 void set_error(anomod_ctx* ctx, const char* fmt, ...);
 
+struct GroupWs;  // group.hip
+
 enum Stage { kStageEdgeAgg = 0, kStageEdgeFinal = 1, kStageEdgeReduce = 2, kStageEwma = 3,
              kStagePagerank = 4, kStageTraceStruct = 5, kStageSegments = 6, kStageSummary = 7,
-             kNumStages = 8 };
+             kStageGroup = 8, kNumStages = 9 };
 
 }  // namespace anomod
 
@@ -39,6 +41,8 @@ struct anomod_ctx {
   double comm_timeout_s = 300; // ANOMOD_RCCL_TIMEOUT_S
   int* d_status = nullptr;     // device word of the status agreement
   int* h_status = nullptr;     // pinned host twin
+  // Trace-grouping workspace (segmented radix sort of ungrouped span sets).
+  anomod::GroupWs* group_ws = nullptr;
   // Cached device workspace for the edge table.
   void* d_table = nullptr;
   size_t table_bytes = 0;
@@ -124,6 +128,13 @@ int comm_agree(anomod_ctx* ctx, int local_rc);
 uint64_t max_launch_spans();
 int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
                      std::vector<uint64_t>& cuts);
+// Span-set storage (synth.hip): every array of a set of n_spans spans /
+// n_traces traces (trace_hash optional), and its release.
+int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_hash,
+                anomod_spans** out);
+void free_spans(anomod_spans* s);
+// Trace-grouping workspace (group.hip), released with the ctx.
+void free_group_ws(anomod_ctx* ctx);
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
 int ensure_host_stage(anomod_ctx* ctx, size_t bytes);

@@ -256,6 +256,7 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  anomod::free_group_ws(ctx);
   if (ctx->d_status) (void)hipFree(ctx->d_status);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->d_table) (void)hipFree(ctx->d_table);

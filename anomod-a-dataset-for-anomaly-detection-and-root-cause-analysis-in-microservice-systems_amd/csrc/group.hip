@@ -1,0 +1,834 @@
+// Ungrouped span sets -> grouped by trace: the segmented radix sort of
+// BASELINE.json north_star (2) ("segmented radix sort by (traceId, ...)").
+//
+// Every span kernel of this library reads spans grouped by trace (the
+// order jaeger_to_csv.py:21-32 and trace_collector.py:539-546 emit).  Spans
+// that arrive interleaved across traces — the Elasticsearch path pulls
+// sw_segment-* hits sorted by start_time over all traces
+// (TT_collection-scripts/T-Dataset/enhanced_trace_collector.py:80-90,
+// 109-110) — are grouped here first.  Trace membership is the trace_hash
+// (equal hash = same trace).  Output order: traces by k = mix64(trace_hash)
+// ascending (mix64 = the SplitMix64 finaliser, a bijection, so any hash
+// distribution gives even buckets), spans of a trace in arrival order (the
+// sort is stable), so parent resolution sees the trace's spans in the order
+// the reference would (first match, trace_collector.py:424-443).
+//
+// Design (MI355X):
+//  * one histogram pass over trace_hash (8 B/span) gives the digit counts of
+//    every radix pass;
+//  * P LSD passes over 8-bit digits of the top 8P bits of k, each ONE kernel
+//    (onesweep): a 4096-record tile is ranked stably with wave ballots (8
+//    ballots give each lane its same-digit peers; rank = popc of the lower
+//    peers; a per-wave LDS counter per digit carries the running count down
+//    the wave's 4 rows), the tile's digit totals are published with a
+//    decoupled look-back over tiles (tile ids from an atomic ticket, so a
+//    tile only ever waits on running predecessors; state words carry an
+//    8-bit epoch so the array is never cleared between passes), the tile is
+//    staged in LDS in digit order and written as coalesced digit runs of
+//    32-B records (AoS: hash, span_id, parent, svc|flags, dur);
+//  * with P = ceil(log2(n) / 8) the top 8P bits nearly always separate
+//    traces; a copy pass writes the grouped SoA columns and lists every key
+//    change inside a bucket of equal top bits; one wave per such bucket
+//    sorts it in LDS by (k, arrival) — rank = #{smaller k} + #{equal k
+//    earlier} — and rewrites its rows; a list overflow or a mixed bucket
+//    larger than the wave's LDS reruns the sort with P + 1 (at P = 8 no
+//    bucket is mixed), so the output never depends on P;
+//  * trace_ptr: one pass over the grouped hashes, trace starts compacted
+//    with a block scan and a decoupled look-back over 4096-span tiles.
+// Bytes per span: 8 (histogram) + 64 per radix pass + 64 (copy) + 8
+// (trace_ptr) + 8 per trace.
+#include <algorithm>
+#include <cmath>
+
+#include "chunk.h"
+#include "common.h"
+
+namespace anomod {
+
+struct __attribute__((aligned(16))) GRec {
+  uint64_t h, sid, pid;
+  uint32_t sf, dur;
+};
+static_assert(sizeof(GRec) == 32, "32-B records");
+
+struct GroupWs {
+  uint64_t cap = 0;                   // spans the buffers hold
+  GRec* aos[2] = {nullptr, nullptr};  // ping-pong records; the other one holds the SoA output
+  uint64_t* tptr = nullptr;           // [cap + 1]
+  uint64_t* state = nullptr;          // look-back words
+  uint64_t state_words = 0;
+  unsigned long long* misc = nullptr; // hist | tickets | counters
+  unsigned long long* list = nullptr; // key changes inside buckets
+  uint64_t list_cap = 0;
+  uint32_t epoch = 0;
+  unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
+};
+
+namespace {
+
+using chunk::wave_sync;
+constexpr int kWv = 64;
+constexpr int kSThreads = 1024;              // scatter workgroup
+constexpr int kSWaves = kSThreads / kWv;
+constexpr int kSPer = 4;                     // records per thread
+constexpr int kSTile = kSThreads * kSPer;    // 4096 records per tile
+constexpr int kRowsPerWave = kSTile / kSWaves / kWv;  // 4
+constexpr int kDig = 256;
+constexpr int kMaxPasses = 8;
+constexpr int kTThreads = 256;               // trace_ptr workgroup
+constexpr int kTPer = 16;
+constexpr int kTTile = kTThreads * kTPer;    // 4096 spans
+constexpr int kFixCap = 1024;                // records of a mixed bucket one wave sorts
+constexpr int kFixWaves = 4;
+constexpr uint64_t kValMask = (1ull << 54) - 1;
+constexpr uint32_t kSpinLimit = 1u << 26;
+
+// misc layout (u64 words)
+constexpr int kMiscHist = 0;                          // [kMaxPasses][256]
+constexpr int kMiscTicket = kMiscHist + kMaxPasses * kDig;  // [kMaxPasses + 1]
+constexpr int kMiscListCnt = kMiscTicket + kMaxPasses + 1;
+constexpr int kMiscOver = kMiscListCnt + 1;           // oversized mixed buckets
+constexpr int kMiscTraces = kMiscOver + 1;            // n_traces
+constexpr int kMiscErr = kMiscTraces + 1;             // look-back timeout
+constexpr int kMiscWords = kMiscErr + 1;
+constexpr int kMiscRead = kMiscListCnt;               // [kMiscRead, kMiscWords) read back
+
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ inline uint64_t pack_state(uint32_t epoch, uint32_t flag, uint64_t v) {
+  return ((uint64_t)epoch << 56) | ((uint64_t)flag << 54) | (v & kValMask);
+}
+
+__device__ inline void publish(uint64_t* w, uint64_t v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sum of the predecessors' totals of one look-back lane (state words
+// strided by `stride` per tile): aggregates (flag 1) are added and the walk
+// continues, an inclusive prefix (flag 2) ends it.  A bounded spin: a
+// predecessor that never publishes sets the error word instead of hanging.
+__device__ uint64_t look_back(uint64_t* state, uint64_t stride, uint64_t tile, uint32_t lane,
+                              uint32_t epoch, unsigned long long* err) {
+  uint64_t excl = 0;
+  int64_t j = (int64_t)tile - 1;
+  uint32_t spins = 0;
+  while (j >= 0) {
+    const uint64_t w = __hip_atomic_load(&state[(uint64_t)j * stride + lane], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ep = (uint32_t)(w >> 56), fl = (uint32_t)(w >> 54) & 3u;
+    if (ep != epoch || fl == 0u) {
+      if (++spins > kSpinLimit) {
+        atomicAdd(err, 1ull);
+        return excl;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += w & kValMask;
+    if (fl == 2u) break;
+    --j;
+  }
+  return excl;
+}
+
+struct SoaIn {
+  const uint64_t* __restrict__ h;
+  const uint64_t* __restrict__ sid;
+  const uint64_t* __restrict__ pid;
+  const uint32_t* __restrict__ sf;
+  const uint32_t* __restrict__ dur;
+};
+
+struct SoaOut {
+  uint64_t* __restrict__ h;
+  uint64_t* __restrict__ sid;
+  uint64_t* __restrict__ pid;
+  uint32_t* __restrict__ sf;
+  uint32_t* __restrict__ dur;
+};
+
+// ---- digit histograms of every pass (one read of trace_hash) -------------
+__global__ __launch_bounds__(256) void group_hist_kernel(const uint64_t* __restrict__ h,
+                                                         uint64_t n, int passes, int shift0,
+                                                         unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t lh[kMaxPasses * kDig];
+  for (int i = threadIdx.x; i < passes * kDig; i += 256) lh[i] = 0u;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = mix64(h[i]);
+    for (int p = 0; p < passes; ++p)
+      atomicAdd(&lh[p * kDig + (uint32_t)((k >> (shift0 + 8 * p)) & 255u)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * kDig; i += 256)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+
+// ---- one stable LSD pass (onesweep) ---------------------------------------
+template <bool SOA_IN>
+__global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
+    SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
+    const unsigned long long* __restrict__ hist, uint64_t* __restrict__ state, uint32_t epoch,
+    unsigned long long* __restrict__ ticket, unsigned long long* __restrict__ err) {
+  __shared__ GRec stage[kSTile];                 // 128 KiB
+  __shared__ uint16_t wcnt[kSWaves][kDig];       // per-wave digit counts, then wave offsets
+  __shared__ uint8_t sdig[kSTile];
+  __shared__ uint32_t tstart[kDig];              // tile-local start of each digit
+  __shared__ unsigned long long gbase[kDig];     // global start of each digit's run
+  __shared__ unsigned long long hbase[kDig];
+  __shared__ uint32_t wsum_t[kDig / kWv];
+  __shared__ unsigned long long wsum_h[kDig / kWv];
+  __shared__ unsigned long long s_tile;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1ull);
+  for (int i = tid; i < kSWaves * kDig / 2; i += kSThreads)
+    reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0u;
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t base = tile * kSTile;
+
+  // a record as two 16-B halves: (h, sid) and (pid, sf | dur << 32)
+  uint4 ra[kSPer], rb[kSPer];
+  uint32_t d[kSPer];
+  bool v[kSPer];
+#pragma unroll
+  for (int k = 0; k < kSPer; ++k) {
+    const uint64_t i = base + (uint64_t)(w * (kRowsPerWave * kWv) + k * kWv + lane);
+    v[k] = i < n;
+    ra[k] = make_uint4(0, 0, 0, 0);
+    rb[k] = make_uint4(0, 0, 0, 0);
+    if (v[k]) {
+      if constexpr (SOA_IN) {
+        const uint64_t h = sin.h[i], sid = sin.sid[i], pid = sin.pid[i];
+        ra[k] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)sid, (uint32_t)(sid >> 32));
+        rb[k] = make_uint4((uint32_t)pid, (uint32_t)(pid >> 32), sin.sf[i], sin.dur[i]);
+      } else {
+        const uint4* q = reinterpret_cast<const uint4*>(ain + i);
+        ra[k] = q[0];
+        rb[k] = q[1];
+      }
+    }
+    d[k] = (uint32_t)(mix64(((uint64_t)ra[k].y << 32) | ra[k].x) >> shift) & 255u;
+  }
+
+  // Wave multisplit, rows in order: peers = lanes of the row with the same
+  // digit (8 ballots); rank = lower peers + the wave's running digit count.
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t off[kSPer];
+#pragma unroll
+  for (int k = 0; k < kSPer; ++k) {
+    uint64_t peers = __ballot(v[k]);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d[k] >> b) & 1u;
+      const uint64_t bb = __ballot(v[k] && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    off[k] = 0;
+    if (v[k]) {
+      const uint64_t lower = peers & lt_mask;
+      const uint32_t b0 = wcnt[w][d[k]];
+      off[k] = b0 + (uint32_t)__popcll(lower);
+      if (lower == 0ull) wcnt[w][d[k]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
+    }
+    wave_sync();
+  }
+  __syncthreads();
+
+  // Per digit (threads 0..255): wave offsets + tile total, then the tile's
+  // digit starts and the pass's global digit starts (two block scans).
+  uint32_t total = 0;
+  if (tid < kDig) {
+    uint32_t run = 0;
+    for (int ww = 0; ww < kSWaves; ++ww) {
+      const uint32_t c = wcnt[ww][tid];
+      wcnt[ww][tid] = (uint16_t)run;
+      run += c;
+    }
+    total = run;
+    const unsigned long long hcount = hist[tid];
+    uint32_t inc = total;
+    unsigned long long hinc = hcount;
+#pragma unroll
+    for (int o = 1; o < kWv; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      const unsigned long long hy = __shfl_up(hinc, o);
+      if (lane >= o) {
+        inc += y;
+        hinc += hy;
+      }
+    }
+    tstart[tid] = inc - total;
+    hbase[tid] = hinc - hcount;
+    if (lane == kWv - 1) {
+      wsum_t[w] = inc;
+      wsum_h[w] = hinc;
+    }
+  }
+  __syncthreads();
+  if (tid < kDig) {
+    for (int ww = 0; ww < w; ++ww) {
+      tstart[tid] += wsum_t[ww];
+      hbase[tid] += wsum_h[ww];
+    }
+    uint64_t* st = state + tile * kDig + tid;
+    uint64_t excl = 0;
+    if (tile == 0) {
+      publish(st, pack_state(epoch, 2u, total));
+    } else {
+      publish(st, pack_state(epoch, 1u, total));
+      excl = look_back(state, kDig, tile, (uint32_t)tid, epoch, err);
+      publish(st, pack_state(epoch, 2u, excl + total));
+    }
+    gbase[tid] = hbase[tid] + excl;
+  }
+  __syncthreads();
+
+  // Stage the tile in digit order.
+#pragma unroll
+  for (int k = 0; k < kSPer; ++k) {
+    if (v[k]) {
+      const uint32_t lp = tstart[d[k]] + wcnt[w][d[k]] + off[k];
+      uint4* q = reinterpret_cast<uint4*>(&stage[lp]);
+      q[0] = ra[k];
+      q[1] = rb[k];
+      sdig[lp] = (uint8_t)d[k];
+    }
+  }
+  __syncthreads();
+  const uint64_t nvalid = n - base < (uint64_t)kSTile ? n - base : (uint64_t)kSTile;
+#pragma unroll
+  for (int k = 0; k < kSPer; ++k) {
+    const uint32_t p = (uint32_t)(tid + k * kSThreads);
+    if (p < nvalid) {
+      const uint32_t dd = sdig[p];
+      const uint4* q = reinterpret_cast<const uint4*>(&stage[p]);
+      uint4* o = reinterpret_cast<uint4*>(aout + gbase[dd] + (p - tstart[dd]));
+      const uint4 x0 = q[0], x1 = q[1];
+      o[0] = x0;
+      o[1] = x1;
+    }
+  }
+}
+
+// ---- copy to SoA columns + list key changes inside buckets ----------------
+__global__ __launch_bounds__(256) void group_copy_kernel(const GRec* __restrict__ a, uint64_t n,
+                                                         int top_shift, SoaOut out,
+                                                         unsigned long long* __restrict__ list,
+                                                         uint64_t list_cap,
+                                                         unsigned long long* __restrict__ cnt) {
+  const int lane = threadIdx.x & (kWv - 1);
+  const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWv;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 256 / kWv;
+  for (uint64_t b = wave * kWv; b < n; b += nwaves * kWv) {
+    const uint64_t i = b + lane;
+    const bool v = i < n;
+    GRec r = v ? a[i] : GRec{0, 0, 0, 0, 0};
+    const uint64_t k = mix64(r.h);
+    uint64_t kp = __shfl_up(k, 1);
+    if (lane == 0) kp = (i > 0 && v) ? mix64(a[i - 1].h) : k;
+    const bool change = v && i > 0 && k != kp && (k >> top_shift) == (kp >> top_shift);
+    const uint64_t bal = __ballot(change);
+    if (bal) {
+      unsigned long long at = 0;
+      if (lane == 0) at = atomicAdd(cnt, (unsigned long long)__popcll(bal));
+      at = __shfl(at, 0);
+      const uint64_t pos = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+      if (change && pos < list_cap) list[pos] = i;
+    }
+    if (v) {
+      out.h[i] = r.h;
+      out.sid[i] = r.sid;
+      out.pid[i] = r.pid;
+      out.sf[i] = r.sf;
+      out.dur[i] = r.dur;
+    }
+  }
+}
+
+// ---- one wave per mixed bucket: sort it by (k, arrival) in LDS ------------
+__global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
+    const GRec* __restrict__ a, uint64_t n, int top_shift, SoaOut out,
+    const unsigned long long* __restrict__ list, uint64_t list_cap,
+    const unsigned long long* __restrict__ cnt, unsigned long long* __restrict__ over) {
+  __shared__ uint64_t lk[kFixWaves][kFixCap];
+  const int lane = threadIdx.x & (kWv - 1), w = threadIdx.x / kWv;
+  uint64_t m_list = *cnt;
+  if (m_list > list_cap) m_list = list_cap;  // overflow: the host reruns with more passes
+  uint64_t* keys = lk[w];
+  for (uint64_t e = (uint64_t)blockIdx.x * kFixWaves + w; e < m_list;
+       e += (uint64_t)gridDim.x * kFixWaves) {
+    const uint64_t i = list[e];
+    const uint64_t ki = mix64(a[i].h), kprev = mix64(a[i - 1].h);
+    const uint64_t top = ki >> top_shift;
+    // bucket start: walk back from i - 1; this entry owns the bucket only if
+    // it is the bucket's first key change (everything before it = kprev)
+    uint64_t bs = 0;
+    bool owner = true;
+    for (uint64_t s0 = 0;; s0 += kWv) {
+      const uint64_t off = s0 + lane + 1;  // position i - off
+      const bool valid = off <= i;
+      const uint64_t kj = valid ? mix64(a[i - off].h) : 0;
+      const bool same_top = valid && (kj >> top_shift) == top;
+      const uint64_t end_m = __ballot(!same_top);
+      const uint64_t bad_m = __ballot(same_top && kj != kprev);
+      if (end_m) {
+        const int f = __ffsll((long long)end_m) - 1;  // first lane past the bucket
+        if (bad_m & ((1ull << f) - 1ull)) owner = false;
+        bs = i - (s0 + (uint64_t)f);
+        break;
+      }
+      if (bad_m) {
+        owner = false;
+        break;
+      }
+    }
+    if (!owner) continue;
+    uint64_t be = n;
+    for (uint64_t j0 = i + 1; j0 < n; j0 += kWv) {
+      const uint64_t j = j0 + lane;
+      const bool same_top = j < n && (mix64(a[j].h) >> top_shift) == top;
+      const uint64_t end_m = __ballot(!same_top);
+      if (end_m) {
+        be = j0 + (uint64_t)(__ffsll((long long)end_m) - 1);
+        break;
+      }
+    }
+    const uint64_t m = be - bs;
+    if (m > (uint64_t)kFixCap) {
+      if (lane == 0) atomicAdd(over, 1ull);
+      continue;
+    }
+    for (uint32_t q = lane; q < m; q += kWv) keys[q] = mix64(a[bs + q].h);
+    wave_sync();
+    for (uint32_t q0 = 0; q0 < m; q0 += kWv) {
+      const uint32_t q = q0 + lane;
+      const bool act = q < m;
+      const uint64_t kq = act ? keys[q] : 0;
+      uint32_t rank = 0;
+      for (uint32_t t = 0; t < m; ++t) {
+        const uint64_t kt = keys[t];
+        rank += (kt < kq || (kt == kq && t < q)) ? 1u : 0u;
+      }
+      if (act) {
+        const GRec r = a[bs + q];
+        const uint64_t p = bs + rank;
+        out.h[p] = r.h;
+        out.sid[p] = r.sid;
+        out.pid[p] = r.pid;
+        out.sf[p] = r.sf;
+        out.dur[p] = r.dur;
+      }
+    }
+    wave_sync();
+  }
+}
+
+// ---- trace_ptr from the grouped hashes --------------------------------------
+__global__ __launch_bounds__(kTThreads) void group_tptr_kernel(
+    const uint64_t* __restrict__ h, uint64_t n, uint64_t* __restrict__ tptr,
+    uint64_t* __restrict__ state, uint32_t epoch, unsigned long long* __restrict__ ticket,
+    unsigned long long* __restrict__ n_traces, unsigned long long* __restrict__ err) {
+  __shared__ unsigned long long s_tile, s_excl;
+  __shared__ uint32_t wtot[kTThreads / kWv];
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1ull);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t p0 = tile * kTTile + (uint64_t)tid * kTPer;
+  uint32_t starts = 0;
+  uint64_t prev = p0 > 0 && p0 - 1 < n ? h[p0 - 1] : ~0ull;
+#pragma unroll
+  for (int j = 0; j < kTPer; ++j) {
+    const uint64_t p = p0 + j;
+    if (p < n) {
+      const uint64_t x = h[p];
+      if (p == 0 || x != prev) starts |= 1u << j;
+      prev = x;
+    }
+  }
+  const uint32_t c = (uint32_t)__popc(starts);
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < kWv; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWv - 1) wtot[w] = inc;
+  __syncthreads();
+  uint32_t wadd = 0, tot = 0;
+  for (int ww = 0; ww < kTThreads / kWv; ++ww) {
+    if (ww < w) wadd += wtot[ww];
+    tot += wtot[ww];
+  }
+  if (tid == 0) {
+    uint64_t* st = state + tile;
+    uint64_t excl = 0;
+    if (tile == 0) {
+      publish(st, pack_state(epoch, 2u, tot));
+    } else {
+      publish(st, pack_state(epoch, 1u, tot));
+      excl = look_back(state, 1, tile, 0u, epoch, err);
+      publish(st, pack_state(epoch, 2u, excl + tot));
+    }
+    s_excl = excl;
+    if ((tile + 1) * kTTile >= n) {  // the last tile closes trace_ptr
+      *n_traces = excl + tot;
+      tptr[excl + tot] = n;
+    }
+  }
+  __syncthreads();
+  uint64_t idx = s_excl + wadd + inc - c;
+#pragma unroll
+  for (int j = 0; j < kTPer; ++j)
+    if ((starts >> j) & 1u) tptr[idx++] = p0 + j;
+}
+
+// ---- synthetic arrival orders (bench / tests; not a product path) --------
+// Keyed bijection of [0, m) (4-round Feistel over the next power of 4,
+// cycle-walking back into range).
+__device__ inline uint64_t feistel_perm(uint64_t x, uint64_t m, uint64_t key) {
+  if (m <= 1) return 0;
+  int bits = 64 - __clzll((long long)(m - 1));
+  if (bits & 1) ++bits;
+  const int half = bits / 2;
+  const uint64_t mask = (1ull << half) - 1ull;
+  do {
+    uint64_t l = x >> half, r = x & mask;
+    for (int round = 0; round < 4; ++round) {
+      const uint64_t f = mix64(r ^ (key + 0x9E3779B97F4A7C15ull * (round + 1))) & mask;
+      const uint64_t nl = r;
+      r = l ^ f;
+      l = nl;
+    }
+    x = (l << half) | r;
+  } while (x >= m);
+  return x;
+}
+
+// Window w (traces [w*W, (w+1)*W)) gathers its span range in a random order.
+__global__ __launch_bounds__(256) void shuffle_window_kernel(SoaIn in, SoaOut out,
+                                                             const uint64_t* __restrict__ tptr,
+                                                             uint64_t n_traces, uint64_t W,
+                                                             uint64_t seed) {
+  const uint64_t nwin = (n_traces + W - 1) / W;
+  for (uint64_t win = blockIdx.x; win < nwin; win += gridDim.x) {
+    const uint64_t a = tptr[win * W];
+    const uint64_t b = tptr[(win + 1) * W < n_traces ? (win + 1) * W : n_traces];
+    const uint64_t m = b - a, key = mix64(seed ^ (win * 0xD1B54A32D192ED03ull));
+    for (uint64_t q = threadIdx.x; q < m; q += 256) {
+      const uint64_t src = a + feistel_perm(q, m, key);
+      out.h[a + q] = in.h[src];
+      out.sid[a + q] = in.sid[src];
+      out.pid[a + q] = in.pid[src];
+      out.sf[a + q] = in.sf[src];
+      out.dur[a + q] = in.dur[src];
+    }
+  }
+}
+
+// One thread per trace: its spans in a random order (stays grouped).
+__global__ __launch_bounds__(256) void shuffle_in_trace_kernel(SoaIn in, SoaOut out,
+                                                               const uint64_t* __restrict__ tptr,
+                                                               uint64_t n_traces, uint64_t seed) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n_traces; t += stride) {
+    const uint64_t a = tptr[t], m = tptr[t + 1] - a, key = mix64(seed ^ (t * 0xA24BAED4963EE407ull));
+    for (uint64_t q = 0; q < m; ++q) {
+      const uint64_t src = a + feistel_perm(q, m, key);
+      if (out.h) out.h[a + q] = in.h[src];
+      out.sid[a + q] = in.sid[src];
+      out.pid[a + q] = in.pid[src];
+      out.sf[a + q] = in.sf[src];
+      out.dur[a + q] = in.dur[src];
+    }
+  }
+}
+
+int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
+  GroupWs* ws = ctx->group_ws;
+  if (ws && ws->cap >= n) return ANOMOD_OK;
+  free_group_ws(ctx);
+  ws = new GroupWs();
+  ctx->group_ws = ws;
+  const uint64_t cap = n ? n : 1;
+  const uint64_t tiles = (cap + kSTile - 1) / kSTile;
+  ws->cap = cap;
+  ws->state_words = std::max<uint64_t>(tiles * kDig, (cap + kTTile - 1) / kTTile);
+  ws->list_cap = cap / 8 + 65536;
+  bool ok = hipMalloc(&ws->aos[0], cap * sizeof(GRec)) == hipSuccess;
+  ok = ok && hipMalloc(&ws->aos[1], cap * sizeof(GRec)) == hipSuccess;
+  ok = ok && hipMalloc(&ws->tptr, (cap + 1) * 8) == hipSuccess;
+  ok = ok && hipMalloc(&ws->state, ws->state_words * 8) == hipSuccess;
+  ok = ok && hipMalloc(&ws->misc, kMiscWords * 8) == hipSuccess;
+  ok = ok && hipMalloc(&ws->list, ws->list_cap * 8) == hipSuccess;
+  ok = ok && hipHostMalloc(reinterpret_cast<void**>(&ws->h_misc), kMiscWords * 8,
+                           hipHostMallocDefault) == hipSuccess;
+  if (!ok) {
+    free_group_ws(ctx);
+    set_error(ctx, "hipMalloc failed for the trace-grouping workspace of %llu spans "
+              "(~%llu GB)", (unsigned long long)n,
+              (unsigned long long)((cap * 81ull) >> 30));
+    return ANOMOD_ENOMEM;
+  }
+  ANOMOD_HIP(ctx, hipMemsetAsync(ws->state, 0, ws->state_words * 8, ctx->stream));
+  ws->epoch = 0;
+  return ANOMOD_OK;
+}
+
+uint32_t next_epoch(anomod_ctx* ctx) {
+  GroupWs* ws = ctx->group_ws;
+  if (ws->epoch >= 255u) {  // the 8-bit tag wraps: clear the look-back words once
+    (void)hipMemsetAsync(ws->state, 0, ws->state_words * 8, ctx->stream);
+    ws->epoch = 0;
+  }
+  return ++ws->epoch;
+}
+
+// The grouped view of the workspace after a run.
+struct GroupResult {
+  SoaOut cols;
+  uint64_t n_traces = 0;
+  uint64_t* tptr = nullptr;
+  int passes = 0;
+};
+
+int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
+  const uint64_t n = in->n_spans;
+  if (int rc = ensure_group_ws(ctx, n)) return rc;
+  GroupWs* ws = ctx->group_ws;
+  int P = 1;
+  while (P < kMaxPasses && (1ull << (8 * P)) < n) ++P;  // 2^(8P) >= n
+  const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
+  const uint64_t tiles = (n + kSTile - 1) / kSTile;
+  for (;; ++P) {
+    ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc, 0, kMiscWords * 8, ctx->stream));
+    const int shift0 = 64 - 8 * P;
+    GRec* src = nullptr;
+    GRec* dst = ws->aos[0];
+    if (n > 0) {
+      hipLaunchKernelGGL(group_hist_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
+                         in->trace_hash, n, P, shift0, ws->misc + kMiscHist);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      for (int p = 0; p < P; ++p) {
+        dst = ws->aos[p & 1];
+        const uint32_t ep = next_epoch(ctx);
+        auto fn = p == 0 ? group_scatter_kernel<true> : group_scatter_kernel<false>;
+        hipLaunchKernelGGL(fn, dim3((unsigned)tiles), dim3(kSThreads), 0, ctx->stream, sin, src,
+                           dst, n, shift0 + 8 * p, ws->misc + kMiscHist + p * kDig, ws->state, ep,
+                           ws->misc + kMiscTicket + p, ws->misc + kMiscErr);
+        ANOMOD_HIP(ctx, hipGetLastError());
+        src = dst;
+      }
+    }
+    // SoA output carved from the other record buffer
+    char* ob = reinterpret_cast<char*>(ws->aos[P & 1]);
+    const uint64_t cap = ws->cap;
+    SoaOut cols{reinterpret_cast<uint64_t*>(ob), reinterpret_cast<uint64_t*>(ob + 8 * cap),
+                reinterpret_cast<uint64_t*>(ob + 16 * cap), reinterpret_cast<uint32_t*>(ob + 24 * cap),
+                reinterpret_cast<uint32_t*>(ob + 28 * cap)};
+    if (n > 0) {
+      const int top_shift = 64 - 8 * P;  // 0 at P = 8: every bucket is one key
+      const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256,
+                                                         (uint64_t)ctx->num_cus * 16);
+      hipLaunchKernelGGL(group_copy_kernel, dim3(grid), dim3(256), 0, ctx->stream, src, n,
+                         top_shift, cols, ws->list, ws->list_cap,
+                         ws->misc + kMiscListCnt);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      hipLaunchKernelGGL(group_fix_kernel, dim3(ctx->num_cus * 4), dim3(kFixWaves * kWv), 0,
+                         ctx->stream, src, n, top_shift, cols, ws->list, ws->list_cap,
+                         ws->misc + kMiscListCnt, ws->misc + kMiscOver);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      const uint32_t ep = next_epoch(ctx);
+      hipLaunchKernelGGL(group_tptr_kernel, dim3((unsigned)((n + kTTile - 1) / kTTile)),
+                         dim3(kTThreads), 0, ctx->stream, cols.h, n, ws->tptr, ws->state, ep,
+                         ws->misc + kMiscTicket + kMaxPasses, ws->misc + kMiscTraces,
+                         ws->misc + kMiscErr);
+      ANOMOD_HIP(ctx, hipGetLastError());
+    } else {
+      ANOMOD_HIP(ctx, hipMemsetAsync(ws->tptr, 0, 8, ctx->stream));
+    }
+    ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
+                                   (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const unsigned long long* hm = ws->h_misc;
+    if (hm[kMiscErr]) {
+      set_error(ctx, "trace grouping: a look-back wait timed out (%llu lanes)", hm[kMiscErr]);
+      return ANOMOD_EHIP;
+    }
+    if (n > 0 && P < kMaxPasses && (hm[kMiscListCnt] > ws->list_cap || hm[kMiscOver] > 0))
+      continue;  // too many traces share their top 8P bits: one more pass
+    res->cols = cols;
+    res->n_traces = n > 0 ? hm[kMiscTraces] : 0;
+    res->tptr = ws->tptr;
+    res->passes = P;
+    return ANOMOD_OK;
+  }
+}
+
+anomod_spans view_of(const anomod_spans* in, const GroupResult& g) {
+  anomod_spans v;
+  v.device = in->device;
+  v.n_spans = in->n_spans;
+  v.n_traces = g.n_traces;
+  v.max_svc = in->max_svc;
+  v.grouped = true;
+  v.trace_hash = g.cols.h;
+  v.span_id = g.cols.sid;
+  v.parent_span_id = g.cols.pid;
+  v.svc_flags = g.cols.sf;
+  v.dur_us = g.cols.dur;
+  v.trace_ptr = g.tptr;
+  return v;
+}
+
+}  // namespace
+
+void free_group_ws(anomod_ctx* ctx) {
+  GroupWs* ws = ctx->group_ws;
+  if (!ws) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  void* p[] = {ws->aos[0], ws->aos[1], ws->tptr, ws->state, ws->misc, ws->list};
+  for (void* q : p)
+    if (q) (void)hipFree(q);
+  if (ws->h_misc) (void)hipHostFree(ws->h_misc);
+  delete ws;
+  ctx->group_ws = nullptr;
+}
+
+}  // namespace anomod
+
+using namespace anomod;
+
+extern "C" {
+
+int anomod_spans_upload_ungrouped(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                                  anomod_spans** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && soa && out, "anomod_spans_upload_ungrouped: NULL argument");
+  ANOMOD_REQUIRE(ctx, n_spans == 0 || soa->trace_hash,
+                 "an ungrouped span set needs trace_hash (it defines the traces)");
+  if (int rc = anomod_spans_upload(ctx, soa, n_spans, nullptr, 0, out)) return rc;
+  (*out)->grouped = false;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_grouped(const anomod_spans* spans, int* grouped) {
+  ANOMOD_REQUIRE(nullptr, spans && grouped, "anomod_spans_grouped: NULL argument");
+  *grouped = spans->grouped ? 1 : 0;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* in, anomod_spans** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && in && out, "anomod_spans_group: NULL argument");
+  *out = nullptr;
+  ANOMOD_REQUIRE(ctx, in->device == ctx->device, "span set lives on another device");
+  ANOMOD_REQUIRE(ctx, in->n_spans == 0 || in->trace_hash, "span set has no trace_hash");
+  if (int rc = bind(ctx)) return rc;
+  if (int rc = stage_begin(ctx, kStageGroup)) return rc;
+  GroupResult g;
+  if (int rc = group_run(ctx, in, &g)) return rc;
+  if (int rc = stage_end(ctx, kStageGroup)) return rc;
+  anomod_spans* s = nullptr;
+  if (int rc = alloc_spans(ctx, in->n_spans, g.n_traces, true, &s)) return rc;
+  s->max_svc = in->max_svc;
+  const uint64_t n = in->n_spans;
+  hipError_t e = hipSuccess;
+  auto cp = [&](void* d, const void* src, size_t bytes) {
+    if (e == hipSuccess && bytes)
+      e = hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
+  };
+  cp(s->trace_hash, g.cols.h, n * 8);
+  cp(s->span_id, g.cols.sid, n * 8);
+  cp(s->parent_span_id, g.cols.pid, n * 8);
+  cp(s->svc_flags, g.cols.sf, n * 4);
+  cp(s->dur_us, g.cols.dur, n * 4);
+  cp(s->trace_ptr, g.tptr, (g.n_traces + 1) * 8);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    free_spans(s);
+    set_error(ctx, "copying the grouped span set failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
+  *out = s;
+  return ANOMOD_OK;
+}
+
+int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
+                                    uint32_t n_services, anomod_edge_table* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && spans && out, "anomod_edge_aggregate_ungrouped: NULL argument");
+  if (spans->grouped) return anomod_edge_aggregate_spans(ctx, spans, n_services, out);
+  int rc = ANOMOD_OK;
+  if (spans->device != ctx->device) {
+    set_error(ctx, "span set lives on another device");
+    rc = ANOMOD_EINVAL;
+  } else if (spans->n_spans && !spans->trace_hash) {
+    set_error(ctx, "span set has no trace_hash");
+    rc = ANOMOD_EINVAL;
+  }
+  GroupResult g;
+  if (rc == ANOMOD_OK) rc = bind(ctx);
+  if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
+  if (rc == ANOMOD_OK) rc = group_run(ctx, spans, &g);
+  if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
+  if (rc != ANOMOD_OK) return comm_agree(ctx, rc);  // peers learn of it before their reduce
+  const anomod_spans view = view_of(spans, g);
+  return anomod_edge_aggregate_spans(ctx, &view, n_services, out);
+}
+
+int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* in, uint64_t seed,
+                         uint64_t window_traces, anomod_spans** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && in && out, "anomod_spans_shuffle: NULL argument");
+  *out = nullptr;
+  ANOMOD_REQUIRE(ctx, in->grouped, "anomod_spans_shuffle needs a grouped span set");
+  ANOMOD_REQUIRE(ctx, window_traces == 0 || in->n_spans == 0 || in->trace_hash,
+                 "interleaving traces needs trace_hash");
+  ANOMOD_REQUIRE(ctx, in->device == ctx->device, "span set lives on another device");
+  if (int rc = bind(ctx)) return rc;
+  const bool keep = window_traces == 0;  // in-trace shuffle: stays grouped
+  anomod_spans* s = nullptr;
+  if (int rc = alloc_spans(ctx, in->n_spans, keep ? in->n_traces : 0, in->trace_hash != nullptr,
+                           &s))
+    return rc;
+  s->max_svc = in->max_svc;
+  s->grouped = keep;
+  const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
+  const SoaOut sout{s->trace_hash, s->span_id, s->parent_span_id, s->svc_flags, s->dur_us};
+  hipError_t e = hipSuccess;
+  if (keep) {
+    e = hipMemcpyAsync(s->trace_ptr, in->trace_ptr, (in->n_traces + 1) * 8,
+                       hipMemcpyDeviceToDevice, ctx->stream);
+    if (e == hipSuccess && in->trace_hash && in->n_spans)
+      e = hipMemcpyAsync(s->trace_hash, in->trace_hash, in->n_spans * 8,
+                         hipMemcpyDeviceToDevice, ctx->stream);  // constant within a trace
+    if (e == hipSuccess && in->n_traces) {
+      SoaOut o = sout;
+      o.h = nullptr;
+      hipLaunchKernelGGL(shuffle_in_trace_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
+                         ctx->stream, sin, o, in->trace_ptr, in->n_traces, seed);
+      e = hipGetLastError();
+    }
+  } else {
+    if (e == hipSuccess) e = hipMemsetAsync(s->trace_ptr, 0, 8, ctx->stream);
+    if (e == hipSuccess && in->n_traces) {
+      hipLaunchKernelGGL(shuffle_window_kernel, dim3(ctx->num_cus * 16), dim3(256), 0, ctx->stream,
+                         sin, sout, in->trace_ptr, in->n_traces, window_traces, seed);
+      e = hipGetLastError();
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    free_spans(s);
+    set_error(ctx, "span shuffle failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
+  *out = s;
+  return ANOMOD_OK;
+}
+
+}  // extern "C"

@@ -351,6 +351,8 @@ __global__ void synth_fill_kernel(TopoView tp, SynthParams sp, uint64_t shard, u
   }
 }
 
+}  // namespace
+
 void free_spans(anomod_spans* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
@@ -385,7 +387,6 @@ int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_
   return ANOMOD_OK;
 }
 
-}  // namespace
 }  // namespace anomod
 
 using namespace anomod;

@@ -500,6 +500,7 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   ANOMOD_REQUIRE(ctx, out->n_services >= 1 && out->n_services <= 4096,
                  "n_services=%u out of range [1, 4096]", out->n_services);
   ANOMOD_REQUIRE(ctx, spans->device == ctx->device, "span set lives on another device");
+  ANOMOD_REQUIRE(ctx, spans->grouped, "span set is not grouped by trace: anomod_spans_group first");
   ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < out->n_services,
                  "span service index %u >= n_services %u", spans->max_svc, out->n_services);
   if (int rc = bind(ctx)) return rc;

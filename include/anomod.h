@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ANOMOD_ABI_VERSION 1
+#define ANOMOD_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 #define ANOMOD_OK 0
@@ -118,7 +118,8 @@ int anomod_ctx_synchronize(anomod_ctx* ctx);
  * ctx stream.  stage: 0 = edge aggregation kernel, 1 = edge finalize kernel,
  * 2 = edge all-reduce, 3 = ewma kernel, 4 = pagerank iterations,
  * 5 = trace-structure kernel, 6 = segment-summary kernel,
- * 7 = value summary (select + sort + sum + picks).                        */
+ * 7 = value summary (select + sort + sum + picks),
+ * 8 = trace grouping of an ungrouped span set (radix passes + copy + trace_ptr). */
 int anomod_ctx_stage_ms(const anomod_ctx* ctx, int stage, double* ms);
 
 /* ---- histogram helpers (host) ------------------------------------------- */
@@ -135,6 +136,26 @@ int anomod_spans_info(const anomod_spans* spans, uint64_t* n_spans, uint64_t* n_
 int anomod_spans_download(anomod_ctx* ctx, const anomod_spans* spans,
                           const anomod_span_soa_out* dst, uint64_t* trace_ptr);
 int anomod_spans_free(anomod_spans* spans);
+
+/* ---- ungrouped span sets (BASELINE.json north_star (2)) ------------------
+ * Spans that arrive interleaved across traces — the Elasticsearch path of
+ * enhanced_trace_collector.py:80-90,109-110 pulls sw_segment-* hits sorted by
+ * start_time over all traces — carry their trace only in trace_hash (equal
+ * hash = same trace).  anomod_spans_group groups them on the device with a
+ * segmented radix sort: traces ordered by mix64(trace_hash) ascending (the
+ * SplitMix64 finaliser), the spans of a trace in arrival order (stable), so
+ * every grouped-set kernel then sees each trace's spans in the order they
+ * arrived (first-match parent rule, trace_collector.py:424-443).            */
+int anomod_spans_upload_ungrouped(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                                  anomod_spans** out);
+int anomod_spans_grouped(const anomod_spans* spans, int* grouped);
+int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* ungrouped, anomod_spans** grouped);
+/* Rearranged copies of a grouped set (synthetic arrival orders for tests
+ * and benchmarks): window_traces = 0 shuffles the spans inside every trace
+ * (the result stays grouped); window_traces = W interleaves the spans of
+ * every W consecutive traces in a random order (the result is ungrouped).  */
+int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* grouped, uint64_t seed,
+                         uint64_t window_traces, anomod_spans** out);
 
 /* ---- synthetic workload ----------------------*/
 #define ANOMOD_TOPO_SN 0 /* DeathStarBench SocialNetwork, 12 services        */
@@ -203,6 +224,10 @@ uint64_t anomod_hash64(const char* s, uint64_t len);
  * (RCCL all-reduce) before quantiles are taken.                            */
 int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
                                 anomod_edge_table* out);
+/* Edge table of an ungrouped set: group (anomod_spans_group, into a
+ * workspace the ctx keeps) then aggregate; a grouped set is aggregated as is. */
+int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
+                                    uint32_t n_services, anomod_edge_table* out);
 /* One-shot host convenience: upload + aggregate + download.               */
 int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
                           const uint64_t* trace_ptr, uint64_t n_traces, anomod_edge_table* out);

@@ -269,3 +269,27 @@ def window_scores_from_state(X: np.ndarray, M: np.ndarray, V: np.ndarray, W: int
             # carry state across NaNs: M/V at t-1 already hold the last state
             Z[t // W, s] = max(Z[t // W, s], abs(z))
     return Z
+
+
+# ---- ungrouped span sets: the grouping rule of anomod_spans_group ----------
+# (no reference counterpart: the reference's collectors hand spans over per
+# trace, trace_collector.py:539-546; the ES path enhanced_trace_collector.py:
+# 80-90,109-110 pulls hits sorted by start_time across traces)
+def mix64(h) -> np.ndarray:
+    """SplitMix64 finaliser (a bijection of u64), elementwise."""
+    z = np.array(h, dtype=np.uint64, copy=True).reshape(-1)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def group_by_trace(trace_hash) -> tuple[np.ndarray, np.ndarray]:
+    """(order, trace_ptr): spans taken in `order` are grouped by trace —
+    traces by mix64(trace_hash) ascending, spans of a trace in arrival order
+    (a stable sort)."""
+    k = mix64(trace_hash)
+    order = np.argsort(k, kind="stable")
+    ks = k[order]
+    n = ks.shape[0]
+    starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]]) if n else np.zeros(0, np.int64)
+    return order, np.r_[starts, n].astype(np.uint64)

@@ -23,8 +23,11 @@ def assert_table_equal(gpu: anomod.EdgeTable, ref: dict):
 
 
 def _random_spanset(rng, S, n_traces, max_len, orphan=0.05, dup=0.0, wide_dur=True,
-                    lo_alias=False):
-    lens = rng.integers(0, max_len + 1, n_traces)
+                    lo_alias=False, lens=None):
+    if lens is None:
+        lens = rng.integers(0, max_len + 1, n_traces)
+    lens = np.asarray(lens, np.int64)
+    n_traces = lens.shape[0]
     ptr = np.zeros(n_traces + 1, np.uint64)
     np.cumsum(lens, out=ptr[1:])
     n = int(ptr[-1])

@@ -1,0 +1,184 @@
+"""GPU parity: grouping of ungrouped span sets (the segmented radix sort,
+csrc/group.hip) against the oracle's stable grouping (oracle/spec.py
+group_by_trace), and the edge table / trace structure of interleaved input
+against the C oracle on the oracle-grouped spans, bit for bit."""
+import numpy as np
+import pytest
+
+import anomod
+from oracle import native, spec
+
+from test_gpu_edge import _random_spanset, assert_table_equal
+
+pytestmark = pytest.mark.gpu
+
+COLS = ("trace_hash", "span_id", "parent_span_id", "svc", "flags", "dur_us")
+
+
+def _interleave(sp: anomod.SpanSet, rng, mode: str) -> anomod.SpanSet:
+    """Arrival orders: 'random' (uniform permutation), 'time' (traces start in
+    order, each span lands at its trace's start + a random delay: the
+    ES start_time order of enhanced_trace_collector.py:80-90 across
+    concurrent traces), 'reverse'."""
+    n = sp.n_spans
+    if mode == "random":
+        order = rng.permutation(n)
+    elif mode == "reverse":
+        order = np.arange(n)[::-1]
+    else:
+        t_of = np.repeat(np.arange(sp.n_traces), np.diff(sp.trace_ptr).astype(np.int64))
+        when = t_of * 10.0 + rng.exponential(200.0, n)
+        order = np.argsort(when, kind="stable")
+    return anomod.SpanSet(sp.services, np.zeros(1, np.uint64), sp.trace_hash[order],
+                          sp.span_id[order], sp.parent_span_id[order], sp.svc[order],
+                          sp.flags[order], sp.dur_us[order])
+
+
+def _with_trace_hashes(sp: anomod.SpanSet, rng, hashes=None) -> anomod.SpanSet:
+    nt = sp.n_traces
+    th = rng.integers(0, 2**64, nt, dtype=np.uint64) if hashes is None else hashes
+    sp.trace_hash = np.repeat(th, np.diff(sp.trace_ptr).astype(np.int64)).astype(np.uint64)
+    return sp
+
+
+def _oracle_grouped(flat: anomod.SpanSet) -> anomod.SpanSet:
+    order, tptr = spec.group_by_trace(flat.trace_hash)
+    return flat.take(order, tptr)
+
+
+def _assert_grouped_equal(got: anomod.SpanSet, want: anomod.SpanSet):
+    np.testing.assert_array_equal(got.trace_ptr, want.trace_ptr, err_msg="trace_ptr")
+    for k in COLS:
+        np.testing.assert_array_equal(getattr(got, k), getattr(want, k), err_msg=k)
+
+
+@pytest.mark.parametrize("n_traces,max_len,mode", [
+    (1, 1, "random"), (3, 5, "reverse"), (200, 12, "random"), (5000, 20, "time"),
+    (40000, 12, "random"), (300000, 14, "time"),
+])
+def test_group_matches_oracle(ctx, n_traces, max_len, mode):
+    rng = np.random.default_rng(n_traces + max_len)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, n_traces, max_len, dup=0.02), rng)
+    flat = _interleave(sp, rng, mode)
+    dev = ctx.upload_ungrouped(flat)
+    assert not dev.grouped
+    g = ctx.group(dev)
+    assert g.grouped
+    _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+    g.free()
+    dev.free()
+
+
+def test_group_empty(ctx):
+    sp = anomod.SpanSet(["a"], np.zeros(1, np.uint64), *(np.zeros(0, t) for t in (
+        np.uint64, np.uint64, np.uint64, np.uint16, np.uint16, np.uint32)))
+    dev = ctx.upload_ungrouped(sp)
+    g = ctx.group(dev)
+    assert g.n_spans == 0 and g.n_traces == 0
+    t = ctx.edge_aggregate(dev)
+    assert t.count.sum() == 0
+
+
+def _unmix64(k: np.ndarray) -> np.ndarray:
+    """Inverse of spec.mix64 (hashes with chosen mixed keys)."""
+    M = 2**64
+
+    def unxorshift(y, s):
+        x = y.copy()
+        for _ in range(64 // s + 1):
+            x = y ^ (x >> np.uint64(s))
+        return x
+
+    z = unxorshift(np.asarray(k, np.uint64), 31)
+    z = z * np.uint64(pow(0x94D049BB133111EB, -1, M))
+    z = unxorshift(z, 27)
+    z = z * np.uint64(pow(0xBF58476D1CE4E5B9, -1, M))
+    return unxorshift(z, 30)
+
+
+def test_mixed_buckets_and_pass_retry(ctx):
+    """Traces whose mixed keys share their top 40 bits land in one bucket at
+    every pass count below 6: buckets of two or three traces take the
+    in-LDS fix-up, a 1800-span mixed bucket exceeds it and forces reruns with
+    more radix passes; the output is the same stable grouping."""
+    rng = np.random.default_rng(3)
+    k = rng.integers(0, 2**64, 10, dtype=np.uint64)
+    assert (spec.mix64(_unmix64(k)) == k).all()
+    base = rng.integers(0, 2**64, 1, dtype=np.uint64)[0] & np.uint64(0xFFFFFFFFFF000000)
+    keys = []
+    keys += [base | np.uint64(x) for x in rng.integers(0, 2**24, 3, dtype=np.uint64)]  # big mix
+    for _ in range(50):  # pairs sharing 40 top bits elsewhere
+        b = rng.integers(0, 2**64, 1, dtype=np.uint64)[0] & np.uint64(0xFFFFFFFFFF000000)
+        keys += [b | np.uint64(x) for x in rng.integers(0, 2**24, 2, dtype=np.uint64)]
+    keys = np.asarray(keys, np.uint64)
+    hashes = _unmix64(keys)
+    lens = np.r_[np.full(3, 600), rng.integers(1, 30, len(keys) - 3)]
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02, lens=lens), rng, hashes)
+    extra = _with_trace_hashes(_random_spanset(rng, 12, 2000, 10), rng)
+    sp = anomod.SpanSet.concat([sp, extra])
+    flat = _interleave(sp, rng, "random")
+    g = ctx.group(ctx.upload_ungrouped(flat))
+    _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+
+
+@pytest.mark.parametrize("mode", ["random", "time"])
+def test_edge_aggregate_ungrouped_bit_exact(ctx, mode):
+    """Interleaved spans with duplicate ids and orphans: the edge table of
+    the ungrouped set equals the oracle's on the stably grouped spans (the
+    first-match parent rule sees each trace in arrival order)."""
+    rng = np.random.default_rng(11)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 30000, 24, dup=0.05), rng)
+    big = _with_trace_hashes(_random_spanset(rng, 12, 3, 900, dup=0.05), rng)
+    flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, mode)
+    dev = ctx.upload_ungrouped(flat)
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(_oracle_grouped(flat)))
+
+
+def test_trace_structure_of_grouped_ungrouped(ctx):
+    rng = np.random.default_rng(5)
+    sp = _with_trace_hashes(_random_spanset(rng, 20, 8000, 30, dup=0.03), rng)
+    flat = _interleave(sp, rng, "time")
+    g = ctx.group(ctx.upload_ungrouped(flat))
+    got = ctx.trace_structure(g)
+    want = native.trace_structure(_oracle_grouped(flat))
+    for k in ("parent_pos", "depth", "n_children", "span_flags", "n_roots", "svc_mask"):
+        np.testing.assert_array_equal(getattr(got, k), want[k], err_msg=k)
+
+
+def test_device_shuffles(ctx):
+    """Window interleave and in-trace shuffle of a device-generated SN set:
+    ungrouped edge table == the oracle on the regrouped download; in-trace
+    shuffle keeps trace_ptr and each trace's multiset of spans."""
+    spec_ = anomod.SynthSpec("SN", seed=21, p_orphan_ppm=2000)
+    dev = ctx.generate(spec_, 60000)
+    host = dev.download()
+    inter = ctx.shuffle(dev, seed=7, window_traces=4096)
+    assert not inter.grouped and inter.n_spans == dev.n_spans
+    flat = inter.download()
+    assert sorted(flat.span_id.tolist()) == sorted(host.span_id.tolist())
+    assert_table_equal(ctx.edge_aggregate(inter), native.edge_aggregate(_oracle_grouped(flat)))
+    intra = ctx.shuffle(dev, seed=9, window_traces=0)
+    assert intra.grouped
+    ih = intra.download()
+    np.testing.assert_array_equal(ih.trace_ptr, host.trace_ptr)
+    assert not np.array_equal(ih.span_id, host.span_id)
+    for t in range(0, host.n_traces, 997):
+        a, b = int(host.trace_ptr[t]), int(host.trace_ptr[t + 1])
+        assert sorted(ih.span_id[a:b].tolist()) == sorted(host.span_id[a:b].tolist())
+    assert_table_equal(ctx.edge_aggregate(intra), native.edge_aggregate(ih))
+
+
+@pytest.mark.slow
+def test_large_interleaved_conservation(ctx):
+    """2^23 SN traces (~72 M spans) interleaved in 4096-trace windows: the
+    grouped edge table equals the table of the original grouped set (span
+    ids are unique, so the table does not depend on in-trace order)."""
+    dev = ctx.generate(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=500), 1 << 23)
+    want = ctx.edge_aggregate(dev)
+    inter = ctx.shuffle(dev, seed=1, window_traces=4096)
+    dev.free()
+    got = ctx.edge_aggregate(inter)
+    for k in ("count", "errors", "sum_us", "min_us", "max_us", "hist"):
+        np.testing.assert_array_equal(getattr(got, k), getattr(want, k), err_msg=k)
+    g = ctx.group(inter)
+    assert g.n_traces == 1 << 23 and g.n_spans == inter.n_spans

@@ -165,3 +165,22 @@ def test_native_edge_aggregate_matches_python():
         h = {(int(e), int(b)): int(tab["hist"][e, b]) for e, b in zip(*np.nonzero(tab["hist"]))}
         assert h == py["hist"]
         assert int(tab["count"].sum()) == sp.n_spans
+
+
+def test_group_by_trace_is_a_stable_grouping():
+    """oracle/spec.py group_by_trace (the rule anomod_spans_group follows)
+    against a dict-based restatement: traces by mix64(hash), arrival order
+    inside a trace."""
+    rng = np.random.default_rng(4)
+    th = rng.integers(0, 50, 3000).astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    order, tptr = spec.group_by_trace(th)
+    groups: dict = {}
+    for i, h in enumerate(th.tolist()):
+        groups.setdefault(h, []).append(i)
+    keys = sorted(groups, key=lambda h: int(spec.mix64([h])[0]))
+    want = [i for h in keys for i in groups[h]]
+    assert order.tolist() == want
+    assert np.diff(tptr).tolist() == [len(groups[h]) for h in keys]
+    assert spec.group_by_trace(np.zeros(0, np.uint64))[1].tolist() == [0]
+    # mix64 is the SplitMix64 finaliser
+    assert int(spec.mix64([1])[0]) == 0x5692161D100B05E5
