@@ -50,9 +50,15 @@ using namespace chunk;
 #endif
 constexpr int kWavesPerWG = ANOMOD_WAVES;
 constexpr int kThreads = kWave * kWavesPerWG;
-constexpr int kHtBucketLog2 = 11;  // 2048 buckets of 4 slots
-constexpr uint32_t kHtSlots = 4u << kHtBucketLog2;
-constexpr int kMaxProbe = 48;
+// LDS histogram table, two forms in the same 64 KiB (see ht_* below).
+enum HistForm { kHtHbm = 0, kHtPair = 1, kHtCompact = 2 };
+constexpr int kPairBucketLog2 = 11;  // pair: 2048 buckets of 4 slots, keys | counts
+constexpr uint32_t kPairSlots = 4u << kPairBucketLog2;
+constexpr int kPairMaxProbe = 48;
+constexpr int kCmpBucketLog2 = 12;   // compact: 4096 buckets of 4 (key | count << kb) slots
+constexpr uint32_t kCmpSlots = 4u << kCmpBucketLog2;
+constexpr int kHtBytes = 65536;
+static_assert(kPairSlots * 8 == kHtBytes && kCmpSlots * 4 == kHtBytes, "64 KiB table");
 #ifndef ANOMOD_LDS_EDGES
 #define ANOMOD_LDS_EDGES 512
 #endif
@@ -65,16 +71,27 @@ constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 #endif
 
 // LDS carve (bytes, every offset a multiple of 16).
-constexpr int kOffHt = 0;                                // u32 slot keys (0 = empty)
-constexpr int kOffHc = kOffHt + (int)kHtSlots * 4;       // u32 slot counts
+constexpr int kOffHt = 0;                      // u32 keys (pair) | u32 slots (compact); 0 = empty
+constexpr int kOffHc = kOffHt + (int)kPairSlots * 4;  // u32 counts (pair form)
 #ifndef ANOMOD_SUM_REPS
 #define ANOMOD_SUM_REPS 8
 #endif
 constexpr uint32_t kSumReps = ANOMOD_SUM_REPS;           // u64 sum replicas per edge
-constexpr int kOffSum = kOffHc + (int)kHtSlots * 4;      // u64 [kLdsEdges][kSumReps]
-constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs
-constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts
-constexpr int kOffWave = kOffErr + (int)kLdsEdges * 4;
+constexpr int kOffSum = kOffHt + kHtBytes;               // u64 [kLdsEdges][kSumReps]
+// Per-edge stats in LDS, two forms.  Direct (E <= kLdsEdges: every SN-width
+// table): (min, max) pairs and error counts indexed by edge.  Slot-hashed
+// (wider tables, e.g. TrainTicket: E = 48 * 46 = 2208): kSlotEdges 16-B
+// entries {edge + 1, min, max, errors} found by hashing the edge (linear
+// probing, ds_cmpst inserts), the sum replicas indexed by slot — a trace set
+// touches far fewer edges than E.
+constexpr uint32_t kSlotEdges = 512;
+static_assert(kSlotEdges <= kLdsEdges, "slot sums reuse the direct sum replicas");
+constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs | slots
+constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts (direct form)
+constexpr int kStatsBytes = (int)(kLdsEdges * 12 > kSlotEdges * 16 ? kLdsEdges * 12
+                                                                  : kSlotEdges * 16);
+constexpr int kOffWave = kOffMm + kStatsBytes;
+enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2 };
 constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
 constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2;  // u8 trace-start flags [kStage]
@@ -90,6 +107,7 @@ struct Table {
   unsigned int* mn;          // [E]
   unsigned int* mx;          // [E]
   unsigned long long* ctr;   // trace-segment counter of the dynamic tail (zeroed per launch)
+  uint32_t kb;               // key bits of a histogram slot (count in the 32 - kb above)
 };
 
 struct Cols {
@@ -99,24 +117,32 @@ struct Cols {
   const uint32_t* __restrict__ dur;
 };
 
-// Histogram increment of key = edge*kBins + bin + 1 in the workgroup's LDS
-// hash table: 2048 buckets of 4 slots, keys and counts in separate u32
-// arrays, so one ds_read_b128 fetches a key's whole home bucket.  A key
-// resident in its home bucket costs that read + one fire-and-forget
-// ds_add_u32 (0 for lanes that miss, so no branch around it).  With the SN
-// mix a workgroup holds ~3.6 k keys in 8 Ki slots and 0.02 % of spans miss
-// their home bucket (1-slot linear probing at the same size: 3.1 %, which
-// sent 87 % of wave-instructions down the insert loop).  A workgroup sees
-// < 2^32 spans, so u32 counts do not wrap.  New keys take the first empty slot
-// in probe order from the bucket start (ds_cmpst; a key never moves); a
-// saturated probe chain counts in HBM directly.
-__device__ __forceinline__ uint32_t ht_bucket(uint32_t key) {
-  return (key * 0x9E3779B1u) >> (32 - kHtBucketLog2);
-}
+// Histogram increment of key = edge*kBins + bin + 1 in the workgroup's LDS.
+//
+// Pair form (E <= kLdsEdges, SN width): 2048 buckets of 4 slots, keys and u32
+// counts in separate arrays, so one ds_read_b128 fetches a key's home
+// bucket; a resident key costs that read + one fire-and-forget ds_add_u32 (0
+// for lanes that miss, so no branch around it).  With the SN mix a
+// workgroup holds ~3.6 k keys in 8 Ki slots and 0.02 % of spans miss their
+// home bucket.  A launch covers < 2^32 spans, so u32 counts do not wrap.
+//
+// Compact form (wider tables: TrainTicket E = 2208, ~21 k keys per
+// workgroup): 16 Ki u32 slots = key | count << kb (kb = the key's bit width,
+// 21 for TrainTicket) in 4096 buckets; a key lives in its home bucket or the
+// next one, both fetched by two ds_read_b128 in one round trip (95 % / 3.3 %
+// of TrainTicket spans, simulated).  The add returns the old slot: a count
+// field that was all ones wrapped, and that lane moves 2^(32-kb) counts to
+// HBM (exact: one lane per wrap).  When both buckets are full of other keys
+// the span counts in HBM at once (1.7 %), so no lane walks a probe chain.
+//
+// New keys take the first empty slot in probe order from the bucket start
+// (ds_cmpst; a key never moves).
+__device__ __forceinline__ uint32_t ht_hash(uint32_t key) { return key * 0x9E3779B1u; }
 
-__device__ __attribute__((noinline)) void ht_insert(uint32_t* hk, uint32_t* hc, uint32_t key, uint32_t s,
-                                          unsigned long long* __restrict__ ghist) {
-  for (int probe = 0; probe < kMaxProbe; ++probe) {
+__device__ __attribute__((noinline)) void ht_insert_pair(uint32_t* hk, uint32_t* hc, uint32_t key,
+                                                         uint32_t s,
+                                                         unsigned long long* __restrict__ ghist) {
+  for (int probe = 0; probe < kPairMaxProbe; ++probe) {
     uint32_t cur = __hip_atomic_load(&hk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == 0u) {
       const uint32_t prev = atomicCAS(&hk[s], 0u, key);
@@ -126,86 +152,182 @@ __device__ __attribute__((noinline)) void ht_insert(uint32_t* hk, uint32_t* hc, 
       atomicAdd(&hc[s], 1u);
       return;
     }
-    s = (s + 1u) & (kHtSlots - 1u);
+    s = (s + 1u) & (kPairSlots - 1u);
+  }
+  atomicAdd(&ghist[key - 1u], 1ull);
+}
+
+__device__ __forceinline__ void ht_wrap(uint32_t old, uint32_t key, uint32_t kb,
+                                        unsigned long long* __restrict__ ghist) {
+  if ((old >> kb) == (0xFFFFFFFFu >> kb)) atomicAdd(&ghist[key - 1u], 1ull << (32u - kb));
+}
+
+// Compact form, key not in its two buckets but one of them had room: claim
+// the first empty slot of the 8 (or count where another lane just put it).
+__device__ __attribute__((noinline)) void ht_insert_cmp(uint32_t* hk, uint32_t key, uint32_t b0,
+                                                        uint32_t b1, uint32_t kb,
+                                                        unsigned long long* __restrict__ ghist) {
+  const uint32_t kmask = 0xFFFFFFFFu >> (32u - kb);
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t s = (q < 4 ? b0 : b1) + (uint32_t)(q & 3);
+    uint32_t cur = __hip_atomic_load(&hk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0u) {
+      const uint32_t prev = atomicCAS(&hk[s], 0u, key | (1u << kb));
+      if (prev == 0u) return;  // new slot, count 1
+      cur = prev;
+    }
+    if ((cur & kmask) == key) {
+      ht_wrap(atomicAdd(&hk[s], 1u << kb), key, kb, ghist);
+      return;
+    }
   }
   atomicAdd(&ghist[key - 1u], 1ull);
 }
 
 using u32x2 = uint32_t __attribute__((ext_vector_type(2)));
+using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
 
-// The edge's current (min, max) in LDS (read before the span's histogram
-// update, so this read and the bucket read share one LDS round trip).
-template <bool LDS_STATS>
-__device__ __forceinline__ u32x2 stat_peek(const unsigned char* smem, uint32_t edge) {
-  if constexpr (LDS_STATS && !(ANOMOD_ABL & 1))
-    return *reinterpret_cast<const u32x2*>(smem + kOffMm + 8u * edge);
-  else
-    return u32x2{0u, 0u};
+__device__ __forceinline__ uint32_t slot_home(uint32_t edge) {
+  return (edge * 0x9E3779B1u) >> (32 - 9);  // kSlotEdges = 512
 }
 
-template <bool LDS_STATS>
+// The slot of `key` = edge + 1 past its home (linear probing; inserted on
+// first sight); UINT32_MAX when kSlotProbe slots are taken by other edges
+// (that span's stats then go to HBM).
+constexpr int kSlotProbe = 32;
+__device__ __attribute__((noinline)) uint32_t slot_find(uint32_t* st4, uint32_t key) {
+  uint32_t s = slot_home(key - 1u);
+  for (int probe = 0; probe < kSlotProbe; ++probe) {
+    uint32_t cur = __hip_atomic_load(&st4[4u * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0u) {
+      const uint32_t prev = atomicCAS(&st4[4u * s], 0u, key);
+      cur = prev == 0u ? key : prev;
+    }
+    if (cur == key) return s;
+    s = (s + 1u) & (kSlotEdges - 1u);
+  }
+  return 0xFFFFFFFFu;
+}
+
+// The edge's stats position and current (min, max) in LDS, read before the
+// span's histogram update so this read and the bucket read share one LDS
+// round trip.  slot: the edge itself (direct), its table slot (slot form;
+// UINT32_MAX = not at home, resolved by slot_find after the bucket read).
+struct StatPeek {
+  u32x2 mm;
+  uint32_t slot;
+};
+
+template <int ST>
+__device__ __forceinline__ StatPeek stat_peek(const unsigned char* smem, uint32_t edge) {
+  if constexpr (ST == kStDirect && !(ANOMOD_ABL & 1)) {
+    return {*reinterpret_cast<const u32x2*>(smem + kOffMm + 8u * edge), edge};
+  } else if constexpr (ST == kStSlot && !(ANOMOD_ABL & 1)) {
+    const uint32_t s = slot_home(edge);
+    const u32x4 e = *reinterpret_cast<const u32x4*>(smem + kOffMm + 16u * s);
+    return {u32x2{e.y, e.z}, e.x == edge + 1u ? s : 0xFFFFFFFFu};
+  } else {
+    return {u32x2{0u, 0u}, edge};
+  }
+}
+
+template <int ST>
 __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uint32_t d,
-                                         uint32_t fl, const Table& tab, u32x2 mm) {
+                                         uint32_t fl, const Table& tab, StatPeek pk) {
   if constexpr (ANOMOD_ABL & 1) return;
-  if constexpr (LDS_STATS) {
+  auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+  if constexpr (ST == kStDirect) {
     // Lanes of one wave-instruction share few edges, and same-address LDS
     // atomics serialise: the sum is spread over kSumReps replicas by lane,
     // and min / max (`mm`, read by stat_peek: a broadcast read) are only
     // updated when the span beats them — after warm-up almost never.  A stale
     // read only costs a redundant atomic.
-    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
     auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
     atomicAdd(&lsum[edge * kSumReps + (__lane_id() & (kSumReps - 1u))], (unsigned long long)d);
-    if (d < mm.x) atomicMin(&lmm[2u * edge], d);
-    if (d > mm.y) atomicMax(&lmm[2u * edge + 1u], d);
+    if (d < pk.mm.x) atomicMin(&lmm[2u * edge], d);
+    if (d > pk.mm.y) atomicMax(&lmm[2u * edge + 1u], d);
     if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&lerr[edge], 1u);
-  } else {
-    atomicAdd(&tab.sum[edge], (unsigned long long)d);
-    atomicMin(&tab.mn[edge], d);
-    atomicMax(&tab.mx[edge], d);
-    if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&tab.err[edge], 1ull);
+    return;
   }
+  if constexpr (ST == kStSlot) {
+    uint32_t s = pk.slot;
+    u32x2 mm = pk.mm;
+    auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    if (s == 0xFFFFFFFFu) {
+      s = slot_find(st4, edge + 1u);
+      mm = u32x2{0xFFFFFFFFu, 0u};  // unknown: the atomics below decide
+    }
+    if (s != 0xFFFFFFFFu) {
+      atomicAdd(&lsum[s * kSumReps + (__lane_id() & (kSumReps - 1u))], (unsigned long long)d);
+      if (d < mm.x) atomicMin(&st4[4u * s + 1u], d);
+      if (d > mm.y) atomicMax(&st4[4u * s + 2u], d);
+      if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&st4[4u * s + 3u], 1u);
+      return;
+    }
+  }
+  atomicAdd(&tab.sum[edge], (unsigned long long)d);
+  atomicMin(&tab.mn[edge], d);
+  atomicMax(&tab.mx[edge], d);
+  if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&tab.err[edge], 1ull);
 }
 
-// One span (big-trace path).
-template <bool LDS_HIST, bool LDS_STATS>
+// One span.
+template <int HT, int ST>
 __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint32_t d, uint32_t fl,
                                        const Table& tab) {
-  const u32x2 mm = stat_peek<LDS_STATS>(smem, edge);
-  bool miss = false;
-  uint32_t key = 0, s0 = 0;
-  if constexpr (!(ANOMOD_ABL & 2)) {
-    const uint32_t kidx = edge * kBins + hist_bin(d);
-    if constexpr (LDS_HIST) {
-      // fast path: the key is resident in its home slot -> one read and an
-      // unconditional add (0 for lanes that miss, so no branch around it)
-      auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
-      auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
-      key = kidx + 1u;
-      s0 = ht_bucket(key) * 4u;
-      // a plain 16-B read (other waves insert concurrently; a stale empty
-      // slot only sends the lane down the insert path, which re-reads)
-      using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
-      const u32x4 bk = *reinterpret_cast<const u32x4*>(hk + s0);
-      const uint32_t j = bk.x == key ? 0u : bk.y == key ? 1u : bk.z == key ? 2u : 3u;
-      const bool hit = (j < 3u) | (bk.w == key);
-      atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
-      miss = !hit;
-    } else
-      atomicAdd(&tab.hist[kidx], 1ull);
+  const StatPeek pk = stat_peek<ST>(smem, edge);
+  const uint32_t key = edge * kBins + hist_bin(d) + 1u;
+  if constexpr ((ANOMOD_ABL & 2) || HT == kHtHbm) {
+    if constexpr (!(ANOMOD_ABL & 2)) atomicAdd(&tab.hist[key - 1u], 1ull);
+    stat_add<ST>(smem, edge, d, fl, tab, pk);
+  } else if constexpr (HT == kHtPair) {
+    // plain 16-B read (other waves insert concurrently; a stale empty slot
+    // only sends the lane down the insert path, which re-reads)
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
+    const uint32_t s0 = (ht_hash(key) >> (32 - kPairBucketLog2)) * 4u;
+    const u32x4 bk = *reinterpret_cast<const u32x4*>(hk + s0);
+    const uint32_t j = bk.x == key ? 0u : bk.y == key ? 1u : bk.z == key ? 2u : 3u;
+    const bool hit = (j < 3u) | (bk.w == key);
+    atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
+    stat_add<ST>(smem, edge, d, fl, tab, pk);
+    if (!hit) ht_insert_pair(hk, hc, key, s0, tab.hist);
+  } else {  // kHtCompact
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
+    const uint32_t b = ht_hash(key) >> (32 - kCmpBucketLog2);
+    const uint32_t s0 = b * 4u, s1 = ((b + 1u) & ((1u << kCmpBucketLog2) - 1u)) * 4u;
+    const u32x4 x = *reinterpret_cast<const u32x4*>(hk + s0);
+    const u32x4 y = *reinterpret_cast<const u32x4*>(hk + s1);
+    const uint32_t j = (x.x & kmask) == key   ? s0
+                       : (x.y & kmask) == key ? s0 + 1u
+                       : (x.z & kmask) == key ? s0 + 2u
+                       : (x.w & kmask) == key ? s0 + 3u
+                       : (y.x & kmask) == key ? s1
+                       : (y.y & kmask) == key ? s1 + 1u
+                       : (y.z & kmask) == key ? s1 + 2u
+                       : (y.w & kmask) == key ? s1 + 3u
+                                              : 0xFFFFFFFFu;
+    const bool hit = j != 0xFFFFFFFFu;
+    const uint32_t old = atomicAdd(&hk[hit ? j : s0], hit ? (1u << tab.kb) : 0u);
+    const bool room = (x.x == 0u) | (x.y == 0u) | (x.z == 0u) | (x.w == 0u) | (y.x == 0u) |
+                      (y.y == 0u) | (y.z == 0u) | (y.w == 0u);
+    stat_add<ST>(smem, edge, d, fl, tab, pk);
+    if (hit) {
+      ht_wrap(old, key, tab.kb, tab.hist);
+    } else if (room) {
+      ht_insert_cmp(hk, key, s0, s1, tab.kb, tab.hist);
+    } else {
+      atomicAdd(&tab.hist[key - 1u], 1ull);
+    }
   }
-  stat_add<LDS_STATS>(smem, edge, d, fl, tab, mm);
-  if constexpr (LDS_HIST && !(ANOMOD_ABL & 2))
-    if (miss)
-      ht_insert(reinterpret_cast<uint32_t*>(smem + kOffHt),
-                reinterpret_cast<uint32_t*>(smem + kOffHc), key, s0, tab.hist);
 }
 
 // A trace longer than kStage: wave-cooperative scan of the trace's span ids,
 // staged kStage at a time through the wave's LDS area (O(L^2 / 64) per trace;
 // rare — real traces are tens of spans).
-template <bool LDS_HIST, bool LDS_STATS>
+template <int HT, int ST>
 __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uint64_t lo,
                           uint64_t hi, const Cols& col, uint32_t S, const Table& tab) {
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
@@ -243,7 +365,7 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
       }
       wave_sync();
     }
-    if (active) record<LDS_HIST, LDS_STATS>(smem, p * S + c, d, fl, tab);
+    if (active) record<HT, ST>(smem, p * S + c, d, fl, tab);
   }
 }
 
@@ -296,7 +418,7 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   return -1;
 }
 
-template <bool LDS_HIST, bool LDS_STATS>
+template <int HT, int ST>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
                                               const Chunk& c, const Regs& R, uint32_t S,
                                               const Table& tab) {
@@ -335,13 +457,13 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
         p = ((R.sf[r] & 0xFFFFu) + 1u + (uint32_t)(R.pid[r] & 1u)) % S;
       }
     }
-    if (i < c.n) record<LDS_HIST, LDS_STATS>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r],
+    if (i < c.n) record<HT, ST>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r],
                                              R.sf[r] >> 16, tab);
   }
   wave_sync();
 }
 
-template <bool LDS_HIST, bool LDS_STATS>
+template <int HT, int ST>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
@@ -354,13 +476,9 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
 
   // ---- init LDS tables
   {
-    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
-    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
-    for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
-      hk[s] = 0u;
-      hc[s] = 0u;
-    }
-    if constexpr (LDS_STATS) {
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);  // both forms: 64 KiB of zeros
+    for (uint32_t s = tid; s < (uint32_t)kHtBytes / 4u; s += kThreads) hk[s] = 0u;
+    if constexpr (ST == kStDirect) {
       auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
       auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
       auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
@@ -369,6 +487,17 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         lerr[e] = 0u;
         lmm[2u * e] = 0xFFFFFFFFu;
         lmm[2u * e + 1u] = 0u;
+      }
+    }
+    if constexpr (ST == kStSlot) {
+      auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+      auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
+      for (uint32_t e = tid; e < kSlotEdges * kSumReps; e += kThreads) lsum[e] = 0ull;
+      for (uint32_t e = tid; e < kSlotEdges; e += kThreads) {
+        st4[4u * e] = 0u;
+        st4[4u * e + 1u] = 0xFFFFFFFFu;
+        st4[4u * e + 2u] = 0u;
+        st4[4u * e + 3u] = 0u;
       }
     }
   }
@@ -413,9 +542,9 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
       }
       if (cur.k == 0) {
-        big_trace<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur.base, cur.base + cur.n, col, S, tab);
+        big_trace<HT, ST>(smem, wsm, lane, cur.base, cur.base + cur.n, col, S, tab);
       } else {
-        process_chunk<LDS_HIST, LDS_STATS>(smem, wsm, lane, cur, R, S, tab);
+        process_chunk<HT, ST>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
@@ -433,15 +562,39 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   __syncthreads();
 
   // ---- flush the workgroup's private tables (integer atomics, order-free)
-  if constexpr (LDS_HIST) {
+  if constexpr (HT == kHtPair) {
     auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
     auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
-    for (uint32_t s = tid; s < kHtSlots; s += kThreads) {
+    for (uint32_t s = tid; s < kPairSlots; s += kThreads) {
       const uint32_t cnt = hc[s];
       if (cnt) atomicAdd(&tab.hist[hk[s] - 1u], (unsigned long long)cnt);
     }
   }
-  if constexpr (LDS_STATS) {
+  if constexpr (HT == kHtCompact) {
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
+    for (uint32_t s = tid; s < kCmpSlots; s += kThreads) {
+      const uint32_t w = hk[s];
+      if (w >> tab.kb) atomicAdd(&tab.hist[(w & kmask) - 1u], (unsigned long long)(w >> tab.kb));
+    }
+  }
+  if constexpr (ST == kStSlot) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    for (uint32_t s = tid; s < kSlotEdges; s += kThreads) {
+      const uint32_t key = st4[4u * s];
+      if (key) {
+        const uint32_t e = key - 1u;
+        unsigned long long sum = 0;
+        for (uint32_t k = 0; k < kSumReps; ++k) sum += lsum[s * kSumReps + k];
+        atomicAdd(&tab.sum[e], sum);
+        if (st4[4u * s + 3u]) atomicAdd(&tab.err[e], (unsigned long long)st4[4u * s + 3u]);
+        atomicMin(&tab.mn[e], st4[4u * s + 1u]);
+        atomicMax(&tab.mx[e], st4[4u * s + 2u]);
+      }
+    }
+  }
+  if constexpr (ST == kStDirect) {
     auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
     auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
     auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
@@ -518,18 +671,17 @@ using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, con
 
 KernelFn pick_kernel(uint32_t E, const char** name) {
   const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
-  const bool lds_hist = keys < (1ull << 32);
-  const bool lds_stats = E <= kLdsEdges;
-  if (lds_hist && lds_stats) {
+  const bool lds_hist = keys < (1ull << 31);  // >= 1 count bit above the key
+  if (lds_hist && E <= kLdsEdges) {
     *name = "edge_agg_kernel<lds_hist,lds_stats>";
-    return edge_agg_kernel<true, true>;
+    return edge_agg_kernel<kHtPair, kStDirect>;
   }
   if (lds_hist) {
-    *name = "edge_agg_kernel<lds_hist,hbm_stats>";
-    return edge_agg_kernel<true, false>;
+    *name = "edge_agg_kernel<lds_compact_hist,slot_stats>";
+    return edge_agg_kernel<kHtCompact, kStSlot>;
   }
   *name = "edge_agg_kernel<hbm_hist,hbm_stats>";
-  return edge_agg_kernel<false, false>;
+  return edge_agg_kernel<kHtHbm, kStHbm>;
 }
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
@@ -591,6 +743,8 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
   tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
   tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
+  tab.kb = 1;
+  while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
   auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
   auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
   auto* p99 = reinterpret_cast<double*>(base + L.off_p99);

@@ -21,7 +21,8 @@ def one(traces: int, steps: int):
     from anomod import _lib as L
 
     with anomod.Context(0) as ctx:
-        sp = ctx.generate(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100), traces)
+        topo = os.environ.get("ABL_TOPO", "SN")
+        sp = ctx.generate(anomod.SynthSpec(topo, seed=20251103, p_orphan_ppm=100), traces)
         for _ in range(2):
             ctx.edge_aggregate(sp, with_hist=False)
         ms = []
