@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "common.h"
@@ -49,6 +50,7 @@ struct anomod_graph {
   // persistent solve: [0] barrier arrivals, [1] timeout flag, [2] iterations done
   unsigned int* bar = nullptr;
   int coop_blocks = -1;  // co-resident blocks of ppr_persistent_kernel (-1: not queried)
+  double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
   uint32_t exec_iters = 0;
@@ -117,6 +119,18 @@ __global__ __launch_bounds__(kPprThreads) void ppr_init_kernel(uint32_t N, doubl
                                                                double* __restrict__ x) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
     x[i] = x0;
+}
+
+// x = x0 everywhere and p /= psum in place (the same IEEE division the host
+// did before: identical bits).
+__global__ __launch_bounds__(kPprThreads) void ppr_init_norm_kernel(uint32_t N, double x0,
+                                                                    double* __restrict__ x,
+                                                                    double* __restrict__ p,
+                                                                    double psum) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    x[i] = x0;
+    p[i] = p[i] / psum;
+  }
 }
 
 // One power iteration x_in -> x_out for the block's rows (the body of both
@@ -462,6 +476,7 @@ void free_graph(anomod_graph* g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  if (g->h_pin) (void)hipHostFree(g->h_pin);
   void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,    g->x[0], g->x[1],
                 g->acc,    g->bp,     g->bx[0], g->bx[1],    g->bacc, g->bar};
   for (void* q : ps)
@@ -641,18 +656,23 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     psum += p[i];
   }
   ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
-  std::vector<double> pn(p, p + N);
-  for (double& v : pn) v /= psum;
   if (int rc = bind(ctx)) return rc;
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, pn.data(), N * 8ull, hipMemcpyHostToDevice, ctx->stream));
+  // p goes up raw through pinned staging and is normalised on the device
+  // (the host-side copy, division and pageable DMA were ~30 % of a
+  // 100-iteration solve at N = 10^5)
+  if (!g->h_pin)
+    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&g->h_pin), N * 8ull,
+                                  hipHostMallocDefault));
+  memcpy(g->h_pin, p, N * 8ull);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, g->h_pin, N * 8ull, hipMemcpyHostToDevice, ctx->stream));
   // x0 = 1/N; its dangling mass n_dangling/N seeds iteration 0 (slot 0); the
   // slots iteration 0 adds into must start at zero.
   for (unsigned long long& v : g->host_acc) v = 0ull;
   g->host_acc[0] = (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
   ANOMOD_HIP(ctx, hipMemcpyAsync(g->acc, g->host_acc.data(), g->host_acc.size() * 8,
                                  hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(ppr_init_kernel, dim3(std::min<uint32_t>(g->grid, 1024)), dim3(kPprThreads),
-                     0, ctx->stream, N, 1.0 / N, g->x[0]);
+  hipLaunchKernelGGL(ppr_init_norm_kernel, dim3(std::min<uint32_t>(g->grid, 1024)),
+                     dim3(kPprThreads), 0, ctx->stream, N, 1.0 / N, g->x[0], g->p, psum);
   ANOMOD_HIP(ctx, hipGetLastError());
   uint32_t done = 0;
   // Tolerance mode: one cooperative launch for the whole solve when every
@@ -663,11 +683,20 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   // grid barrier costs what a graph launch does).  ANOMOD_PPR_MODE=1 forces
   // the per-launch path, 2 the persistent one (tests: same bits).
   if (g->coop_blocks < 0) {
+    // Blocks resident at once.  The persistent solve is a PLAIN launch: the
+    // cooperative launch API only adds a launch-time check of this same
+    // bound (MI355X_MICROARCH.md, coop-launch row), and a process that made
+    // one segfaulted at exit under rocprofv3 --kernel-trace (r01,
+    // scripts/coop_exit_probe.py) — so the bound is checked here, one block
+    // per CU below the occupancy answer (the hardware may admit one fewer
+    // than the API reports for 256-thread blocks), and the grid barrier's
+    // bounded spin turns a block that never became resident into an error,
+    // not a hang.
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ppr_persistent_kernel, kPprThreads,
                                                      0) != hipSuccess)
       per_cu = 0;
-    g->coop_blocks = per_cu * ctx->num_cus;
+    g->coop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
   }
   const char* mode_env = getenv("ANOMOD_PPR_MODE");
   const int mode = mode_env ? atoi(mode_env) : 0;
@@ -678,13 +707,10 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     ANOMOD_HIP(ctx, hipMemsetAsync(g->bar, 0, kBarWords * sizeof(unsigned int), ctx->stream));
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
-    void* args[] = {(void*)&g->N,     (void*)&g->in_ptr, (void*)&g->in_col, (void*)&g->in_w,
-                    (void*)&g->dangling, (void*)&g->p,  (void*)&alpha,     (void*)&x0v,
-                    (void*)&g->x[0],  (void*)&g->x[1],   (void*)&g->acc,    (void*)&iters,
-                    (void*)&ntol,     (void*)&g->bar};
-    ANOMOD_HIP(ctx, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ppr_persistent_kernel),
-                                               dim3(g->grid), dim3(kPprThreads), args, 0,
-                                               ctx->stream));
+    hipLaunchKernelGGL(ppr_persistent_kernel, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream,
+                       g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, x0v,
+                       g->x[0], g->x[1], g->acc, iters, ntol, g->bar);
+    ANOMOD_HIP(ctx, hipGetLastError());
   } else if (tol > 0.0) {
     // Convergence mode: host reads the L1 change after every iteration.
     for (uint32_t it = 0; it < iters; ++it) {
@@ -729,9 +755,10 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     }
     done = hb[2];
   }
-  ANOMOD_HIP(ctx, hipMemcpyAsync(x_out, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
                                  ctx->stream));
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(x_out, g->h_pin, N * 8ull);
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;
 }

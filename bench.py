@@ -33,6 +33,8 @@ import numpy as np  # noqa: E402
 import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
+LEGS = ("trace_structure", "in_trace_shuffled", "ungrouped", "tt_width", "pagerank", "ewma",
+        "tt_config2")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
 
@@ -147,6 +149,54 @@ def tt_config2(ctx) -> dict:
             "note": "end to end through features()/rank(): host-latency-bound at this size"}
 
 
+def edge_leg(ctx, spans, reps: int, what: str) -> dict:
+    """Edge-kernel time of a resident span set (hipEvents, ctx stream)."""
+    ctx.edge_aggregate(spans, with_hist=False)
+    ms = []
+    for _ in range(reps):
+        ctx.edge_aggregate(spans, with_hist=False)
+        ms.append(ctx.stage_ms(L.STAGE_EDGE_AGG))
+    k = float(np.mean(ms))
+    b = algorithmic_bytes(spans.n_spans, spans.n_traces)
+    return {"what": what, "spans": spans.n_spans, "traces": spans.n_traces, "kernel_ms": k,
+            "spans_per_s": spans.n_spans / (k * 1e-3), "bytes_per_launch": b,
+            "achieved_GBps": b / (k * 1e-3) / 1e9, "frac": b / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
+def group_passes(n: int) -> int:
+    """Radix passes anomod_spans_group starts with (csrc/group.hip: 2^(8P) >= n)."""
+    p = 1
+    while p < 8 and (1 << (8 * p)) < n:
+        p += 1
+    return p
+
+
+def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
+    """Grouping + edge aggregation of an ungrouped resident set (n_traces:
+    the traces it holds, all non-empty)."""
+    ctx.edge_aggregate(inter, with_hist=False)
+    g, e, wall = [], [], []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ctx.edge_aggregate(inter, with_hist=False)
+        wall.append(time.perf_counter() - t0)
+        g.append(ctx.stage_ms(L.STAGE_GROUP))
+        e.append(ctx.stage_ms(L.STAGE_EDGE_AGG))
+    n, P = inter.n_spans, group_passes(inter.n_spans)
+    # bytes the grouping moves: trace_hash read by the histogram pass, each
+    # radix pass reads and writes 32-B records, the copy reads records and
+    # writes the 32-B SoA columns, trace_ptr reads the hashes + writes 8 B/trace
+    gbytes = 8 * n + 64 * P * n + 64 * n + 8 * n + 8 * n_traces
+    g_ms, e_ms = float(np.mean(g)), float(np.mean(e))
+    return {"what": "SN spans of every 4096 consecutive traces interleaved (ES start_time "
+                    "order); step = device grouping + edge aggregation",
+            "spans": n, "traces": n_traces, "radix_passes": P,
+            "spans_per_s": allsum(n / float(np.mean(wall))), "step_ms": float(np.mean(wall)) * 1e3,
+            "group_ms": g_ms, "edge_ms": e_ms,
+            "group_bytes": gbytes, "group_GBps": gbytes / (g_ms * 1e-3) / 1e9,
+            "group_frac": gbytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
 def load_traffic(n_spans: int) -> float | None:
     """HBM bytes per launch from the committed PMC profile of this workload."""
     p = ROOT / "profiles" / "edge_agg_pmc.json"
@@ -169,13 +219,19 @@ def main() -> int:
     ap.add_argument("--cpu-traces", type=int, default=1 << 21)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip PageRank / EWMA legs")
+    ap.add_argument("--no-extras", action="store_true", help="headline line only")
+    ap.add_argument("--legs", default=",".join(LEGS),
+                    help="extra legs to run (comma list of " + ", ".join(LEGS) + ")")
     ap.add_argument("--ppr-nodes", type=int, default=100_000)
     ap.add_argument("--ppr-iters", type=int, default=100)
     ap.add_argument("--ewma-series", type=int, default=100_000)
     ap.add_argument("--ewma-steps", type=int, default=131040, help="steps per chunk")
     ap.add_argument("--ewma-chunks", type=int, default=8)
     args = ap.parse_args()
+    legs = set() if args.no_extras else {x for x in args.legs.split(",") if x}
+    unknown = legs - set(LEGS)
+    if unknown:
+        ap.error(f"unknown legs {sorted(unknown)}")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,7 +324,7 @@ def main() -> int:
             "bytes_per_launch": bytes_launch,
         },
     }
-    if not args.no_extras:
+    if "trace_structure" in legs:
         # --- trace structure on the same resident spans:
         # reads 20 B/span + 8 B/trace, writes 13 B/span + 12 B/trace
         ctx.trace_structure(spans, download=False)
@@ -282,9 +338,32 @@ def main() -> int:
             "spans_per_s": allsum(spans.n_spans / (t_ms * 1e-3)), "kernel_ms": t_ms,
             "bytes_per_launch": ts_bytes, "achieved_GBps": ts_bytes / (t_ms * 1e-3) / 1e9,
             "frac": ts_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    if "in_trace_shuffled" in legs:
+        # --- the same spans with every trace's spans in a random order (the
+        # parent scan can no longer rely on parents sitting early)
+        intra = ctx.shuffle(spans, seed=args.seed + 1, window_traces=0)
+        result["sn_in_trace_shuffled"] = edge_leg(ctx, intra, 3, "edge kernel on SN spans "
+                                                  "shuffled inside every trace")
+        intra.free()
+    if "ungrouped" in legs:
+        # --- ungrouped input (north_star (2)): the spans of every 4096
+        # consecutive traces interleaved in a random order, as the ES path
+        # pulls hits sorted by start_time across concurrent traces
+        # (enhanced_trace_collector.py:80-90); a step = device grouping
+        # (segmented radix sort) + edge aggregation
+        inter = ctx.shuffle(spans, seed=args.seed + 2, window_traces=4096)
+        result["ungrouped"] = ungrouped_leg(ctx, inter, spans.n_traces, allsum)
+        inter.free()
     spans.free()
+    if "tt_width" in legs:
+        # --- TrainTicket width (BASELINE config 2 topology, 46 services:
+        # E = 2208 edges) at 2^27 traces (~3.1e9 spans, two launches)
+        tt = ctx.generate(anomod.SynthSpec("TT", seed=args.seed, p_orphan_ppm=100),
+                          args.traces_per_gpu, shard=rank)
+        result["tt_width"] = edge_leg(ctx, tt, 3, "edge kernel on synthetic TrainTicket spans")
+        tt.free()
 
-    if not args.no_extras:
+    if "pagerank" in legs:
         # --- PageRank RCA: replicas (one graph + personalization per GPU)
         g = anomod.DeviceGraph(ctx, synthetic=(args.ppr_nodes, 10, 11 + rank))
         p = np.random.default_rng(rank).random(g.N)
@@ -338,6 +417,7 @@ def main() -> int:
             "vectors": kb, "vector_iters_per_s_per_gpu": kb * args.ppr_iters / (b_ms * 1e-3),
             "iters_per_s_per_gpu": args.ppr_iters / (b_ms * 1e-3)}
         g.free()
+    if "ewma" in legs:
         # --- EWMA/z, BASELINE config 4 at its size: S = 10^5 series x ~10^6
         # steps (8 chunks of 131 040 steps = 52 GB each: X is 400 GB, more
         # than HBM).  Each chunk is generated in HBM (fill_synthetic(t0),
@@ -368,7 +448,7 @@ def main() -> int:
         }
         ser.free()
 
-    if not args.no_extras and world == 1:
+    if "tt_config2" in legs and world == 1:
         result["tt_config2"] = tt_config2(ctx)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

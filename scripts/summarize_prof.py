@@ -4,6 +4,8 @@ profile summaries under profiles/:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
   profiles/<tag>_bench.json         the bench line of the same round
+  profiles/<tag>_pmc.json           HBM bytes per launch of the edge, trace-structure
+                                    and EWMA kernels
   profiles/edge_agg_pmc.json        HBM bytes per edge-aggregation launch
                                     (FETCH_SIZE x 2 per the gfx950 correction
                                     in MI355X_MICROARCH.md "HBM", + WRITE_SIZE;
@@ -44,23 +46,41 @@ def main() -> int:
             bench = json.loads(line)
     if bench:
         (out / f"{tag}_bench.json").write_text(json.dumps(bench, indent=1) + "\n")
-    fetch = counter(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", "edge_agg_kernel")
-    write = counter(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE", "edge_agg_kernel")
-    if fetch and bench:
+    # HBM bytes per launch of each profiled kernel (PMC passes of
+    # scripts/profile.sh), against the algorithmic bytes of the same launch
+    # from the bench line of the same box
+    alg = {}
+    if bench:
+        alg["edge_agg_kernel"] = bench["roofline"]["bytes_per_launch"]
+        if "trace_structure" in bench:
+            alg["trace_struct_kernel"] = bench["trace_structure"]["bytes_per_launch"]
+        if "ewma" in bench:
+            e = bench["ewma"]
+            samples = e["steps_per_chunk"] * e["S"]
+            alg["ewma_zt_kernel"] = 4 * samples + 4 * samples // e["W"] + 40 * e["S"]
+    kernels = {}
+    for k, a in alg.items():
+        fetch = counter(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)
+        write = counter(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE", k)
+        if not fetch:
+            continue
         f_b = sum(fetch) / len(fetch) * 1024 * 2
         w_b = sum(write) / len(write) * 1024 if write else 0.0
-        alg = bench["roofline"]["bytes_per_launch"]
-        d = {"kernel": "edge_agg_kernel", "round": tag,
-             "n_spans": bench["config"]["spans_per_gpu"],
-             "fetch_size_kib": sum(fetch) / len(fetch), "write_size_kib": sum(write) / len(write)
-             if write else None,
-             "read_bytes_per_launch": f_b, "write_bytes_per_launch": w_b,
-             "hbm_bytes_per_launch": f_b + w_b, "algorithmic_bytes_per_launch": alg,
-             "traffic_over_algorithmic": (f_b + w_b) / alg,
-             "correction": "FETCH_SIZE (KiB) x 1024 x 2 (gfx950: FETCH_SIZE counts half of a "
-                           "wide coalesced read); WRITE_SIZE x 1024"}
+        kernels[k] = {"launches": len(fetch), "fetch_size_kib": sum(fetch) / len(fetch),
+                      "write_size_kib": sum(write) / len(write) if write else None,
+                      "read_bytes_per_launch": f_b, "write_bytes_per_launch": w_b,
+                      "hbm_bytes_per_launch": f_b + w_b, "algorithmic_bytes_per_launch": a,
+                      "traffic_over_algorithmic": (f_b + w_b) / a}
+    corr = ("FETCH_SIZE (KiB) x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide coalesced "
+            "read, MI355X_MICROARCH.md HBM); WRITE_SIZE x 1024")
+    if kernels:
+        (out / f"{tag}_pmc.json").write_text(json.dumps(
+            {"round": tag, "correction": corr, "kernels": kernels}, indent=1) + "\n")
+        print(json.dumps(kernels, indent=1))
+    if "edge_agg_kernel" in kernels:
+        d = dict(kernel="edge_agg_kernel", round=tag, n_spans=bench["config"]["spans_per_gpu"],
+                 correction=corr, **kernels["edge_agg_kernel"])
         (out / "edge_agg_pmc.json").write_text(json.dumps(d, indent=1) + "\n")
-        print(json.dumps(d, indent=1))
     return 0
 
 
