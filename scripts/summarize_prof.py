@@ -71,8 +71,53 @@ def main() -> int:
                       "read_bytes_per_launch": f_b, "write_bytes_per_launch": w_b,
                       "hbm_bytes_per_launch": f_b + w_b, "algorithmic_bytes_per_launch": a,
                       "traffic_over_algorithmic": (f_b + w_b) / a}
+    # SQ counters of the same kernels (two passes), per launch
+    for k in list(kernels):
+        sq = {}
+        for sub in ("pmc_sq", "pmc_sq2"):
+            path = prof / sub / "run_counter_collection.csv"
+            if not path.exists():
+                continue
+            with open(path) as f:
+                acc: dict = {}
+                for r in csv.DictReader(f):
+                    if k in r["Kernel_Name"]:
+                        acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            for name, v in acc.items():
+                sq[name] = sum(v) / len(v)
+        if sq:
+            if sq.get("SQ_WAVE_CYCLES"):
+                sq["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0.0) / sq["SQ_WAVE_CYCLES"]
+            if sq.get("SQ_ACTIVE_INST_LDS"):
+                sq["lds_bank_conflict_frac"] = (sq.get("SQ_LDS_BANK_CONFLICT", 0.0)
+                                                / sq["SQ_ACTIVE_INST_LDS"])
+            kernels[k]["sq"] = sq
     corr = ("FETCH_SIZE (KiB) x 1024 x 2 (gfx950: FETCH_SIZE counts half of a wide coalesced "
             "read, MI355X_MICROARCH.md HBM); WRITE_SIZE x 1024")
+    # The headline kernel's own dispatches in the kernel trace (the first
+    # warmup + steps launches of the SN-width edge kernel; later launches of
+    # the same kernel belong to other legs), against the bench's hipEvent time
+    trace = prof / "trace" / "run_kernel_trace.csv"
+    if bench and trace.exists():
+        rows = []
+        with open(trace) as f:
+            for r in csv.DictReader(f):
+                if "edge_agg_kernel<1, 1>" in r["Kernel_Name"]:
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        rows.sort()
+        k = bench["warmup"] + bench["steps"]
+        head = [(e - b) * 1e-6 for b, e in rows[:k]]
+        timed = head[bench["warmup"]:]
+        if timed:
+            hk = {"round": tag, "kernel": "edge_agg_kernel<1, 1> (SN width: lds_hist, lds_stats)",
+                  "dispatches": len(timed), "rocprof_avg_ms": sum(timed) / len(timed),
+                  "rocprof_min_ms": min(timed), "rocprof_max_ms": max(timed),
+                  "bench_hipevent_kernel_ms": bench["roofline"]["kernel_ms"],
+                  "bench_ms_per_step": bench["ms_per_step"],
+                  "note": "the profiled run repeats the bench command on the same box right "
+                          "after the unprofiled bench run"}
+            (out / f"{tag}_headline_kernel.json").write_text(json.dumps(hk, indent=1) + "\n")
+            print(json.dumps(hk, indent=1))
     if kernels:
         (out / f"{tag}_pmc.json").write_text(json.dumps(
             {"round": tag, "correction": corr, "kernels": kernels}, indent=1) + "\n")
