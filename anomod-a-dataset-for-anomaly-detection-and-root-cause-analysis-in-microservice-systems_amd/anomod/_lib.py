@@ -156,6 +156,7 @@ _SIGS = {
     "anomod_spans_group": (_i32, [_vp, _vp, _P(_vp)]),
     "anomod_spans_shuffle": (_i32, [_vp, _vp, _u64, _u64, _P(_vp)]),
     "anomod_edge_aggregate_ungrouped": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
+    "anomod_edge_quantiles_exact": (_i32, [_vp, _vp, _u32, _P(_u32), _u32, _P(_f64), _P(_u64)]),
     "anomod_synth_n_services": (_i32, [_u32, _P(_u32)]),
     "anomod_synth_service_name": (C.c_char_p, [_u32, _u32]),
     "anomod_synth_count_host": (_i32, [_P(SynthSpec), _u64, _u64, _P(_u64)]),

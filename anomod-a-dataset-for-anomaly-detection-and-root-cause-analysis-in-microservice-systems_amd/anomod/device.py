@@ -227,6 +227,27 @@ class Context:
             if tmp is not None:
                 tmp.free()
 
+    def edge_quantiles_exact(self, spans: DeviceSpans | SpanSet, q_pct=(50, 99)):
+        """Exact per-edge order statistics x[(c*q)//100] of the sorted edge
+        latencies ([E, len(q_pct)], NaN for empty edges) and the per-edge
+        counts: the cross-check of the histogram quantiles (§8a a11)."""
+        tmp = None
+        if isinstance(spans, SpanSet):
+            tmp = spans = self.upload(spans)
+        try:
+            q = np.ascontiguousarray(q_pct, np.uint32)
+            S = len(spans.services)
+            E = edge_rows(S)
+            out = np.empty((E, q.shape[0]), np.float64)
+            cnt = np.empty(E, np.uint64)
+            self._check(self._lib.anomod_edge_quantiles_exact(
+                self.handle, spans.handle, S, L.ptr(q, C.c_uint32), q.shape[0],
+                L.ptr(out, C.c_double), L.ptr(cnt, C.c_uint64)))
+            return out, cnt
+        finally:
+            if tmp is not None:
+                tmp.free()
+
     def trace_structure(self, spans: DeviceSpans | SpanSet,
                         download: bool = True) -> TraceStructure | None:
         """Per-span parent/depth/children and per-trace roots/services

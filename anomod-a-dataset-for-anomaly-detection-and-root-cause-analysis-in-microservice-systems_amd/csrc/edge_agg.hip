@@ -38,6 +38,8 @@
 #include <cstring>
 #include <limits>
 
+#include <hipcub/hipcub.hpp>
+
 #include "chunk.h"
 #include "common.h"
 
@@ -51,7 +53,8 @@ using namespace chunk;
 constexpr int kWavesPerWG = ANOMOD_WAVES;
 constexpr int kThreads = kWave * kWavesPerWG;
 // LDS histogram table, two forms in the same 64 KiB (see ht_* below).
-enum HistForm { kHtHbm = 0, kHtPair = 1, kHtCompact = 2 };
+enum HistForm { kHtHbm = 0, kHtPair = 1, kHtCompact = 2,
+                kHtKeys = 3 };  // exact-quantile mode: write (edge << 32 | dur) per span
 constexpr int kPairBucketLog2 = 11;  // pair: 2048 buckets of 4 slots, keys | counts
 constexpr uint32_t kPairSlots = 4u << kPairBucketLog2;
 constexpr int kPairMaxProbe = 48;
@@ -108,6 +111,7 @@ struct Table {
   unsigned int* mx;          // [E]
   unsigned long long* ctr;   // trace-segment counter of the dynamic tail (zeroed per launch)
   uint32_t kb;               // key bits of a histogram slot (count in the 32 - kb above)
+  unsigned long long* keys;  // kHtKeys: [n_spans] edge << 32 | dur, by span position
 };
 
 struct Cols {
@@ -372,7 +376,11 @@ __device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uin
       }
       wave_sync();
     }
-    if (active) record<HT, ST>(smem, p * S + c, d, fl, tab);
+    if constexpr (HT == kHtKeys) {
+      if (active) tab.keys[i] = ((unsigned long long)(p * S + c) << 32) | d;
+    } else {
+      if (active) record<HT, ST>(smem, p * S + c, d, fl, tab);
+    }
   }
 }
 
@@ -464,8 +472,12 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
         p = ((R.sf[r] & 0xFFFFu) + 1u + (uint32_t)(R.pid[r] & 1u)) % S;
       }
     }
-    if (i < c.n) record<HT, ST>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r],
-                                             R.sf[r] >> 16, tab);
+    if constexpr (HT == kHtKeys) {
+      if (i < c.n)
+        tab.keys[c.base + i] = ((unsigned long long)(p * S + (R.sf[r] & 0xFFFFu)) << 32) | R.dur[r];
+    } else {
+      if (i < c.n) record<HT, ST>(smem, p * S + (R.sf[r] & 0xFFFFu), R.dur[r], R.sf[r] >> 16, tab);
+    }
   }
   wave_sync();
 }
@@ -673,6 +685,34 @@ __global__ __launch_bounds__(kWave) void edge_finalize_kernel(Table tab,
   if (r99 >= excl && r99 < incl) p99[e] = quantile_from(r99, excl, incl, v, lane);
 }
 
+// Exact nearest-rank picks from the per-span keys sorted by (edge, dur): one
+// thread per edge finds its segment by binary search and reads
+// x[(c * q) // 100] (the reference's sorted(x)[int(c*q)],
+// monitor_http_responses.py:180-190).
+__global__ __launch_bounds__(256) void exact_pick_kernel(const unsigned long long* __restrict__ sk,
+                                                         uint64_t n, uint32_t E,
+                                                         const uint32_t* __restrict__ q_pct,
+                                                         uint32_t nq, double* __restrict__ out,
+                                                         unsigned long long* __restrict__ count) {
+  const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+  if (e >= E) return;
+  auto lower = [&](unsigned long long key) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (sk[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  const uint64_t a = lower((unsigned long long)e << 32);
+  const uint64_t b = lower((unsigned long long)(e + 1u) << 32);
+  const uint64_t c = b - a;
+  if (count) count[e] = c;
+  for (uint32_t k = 0; k < nq; ++k)
+    out[(uint64_t)e * nq + k] =
+        c ? (double)(uint32_t)sk[a + c * q_pct[k] / 100u] : (double)NAN;
+}
+
 using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                           const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
 
@@ -824,6 +864,92 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   fan(out->max_us, L.off_mx, E * 4ull);
   fan(out->p50_us, L.off_p50, E * 8ull);
   fan(out->p99_us, L.off_p99, E * 8ull);
+  return ANOMOD_OK;
+}
+
+int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S,
+                                const uint32_t* q_pct, uint32_t nq, double* out,
+                                uint64_t* count) {
+  ANOMOD_REQUIRE(nullptr, ctx && spans && q_pct && out,
+                 "anomod_edge_quantiles_exact: NULL argument");
+  ANOMOD_REQUIRE(ctx, S >= 1 && S <= 4096, "n_services=%u out of range [1, 4096]", S);
+  ANOMOD_REQUIRE(ctx, nq >= 1 && nq <= 16, "nq=%u outside [1, 16]", nq);
+  for (uint32_t k = 0; k < nq; ++k)
+    ANOMOD_REQUIRE(ctx, q_pct[k] <= 99, "q_pct[%u]=%u outside [0, 99]", k, q_pct[k]);
+  ANOMOD_REQUIRE(ctx, spans->device == ctx->device, "span set lives on another device");
+  ANOMOD_REQUIRE(ctx, spans->grouped, "span set is not grouped by trace: anomod_spans_group first");
+  ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < S,
+                 "span service index %u >= n_services %u", spans->max_svc, S);
+  if (int rc = bind(ctx)) return rc;
+  const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
+  const uint64_t n = spans->n_spans;
+  int kbits = 1;
+  while ((uint64_t)E >> kbits) ++kbits;
+  // One workspace: keys | sorted keys | sort temp | q | out | count | ctr
+  size_t sort_tmp = 0;
+  if (n)
+    ANOMOD_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(
+                        nullptr, sort_tmp, (const unsigned long long*)nullptr,
+                        (unsigned long long*)nullptr, n, 0, 32 + kbits, ctx->stream));
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t b_keys = al(n * 8), b_tmp = al(sort_tmp), b_q = al(nq * 4), b_out = al(E * nq * 8ull),
+               b_cnt = al(E * 8ull);
+  char* w = nullptr;
+  if (hipMalloc(&w, 2 * b_keys + b_tmp + b_q + b_out + b_cnt + 256) != hipSuccess) {
+    set_error(ctx, "hipMalloc for the exact-quantile workspace (%llu spans) failed",
+              (unsigned long long)n);
+    return ANOMOD_ENOMEM;
+  }
+  auto* keys = reinterpret_cast<unsigned long long*>(w);
+  auto* sorted = reinterpret_cast<unsigned long long*>(w + b_keys);
+  void* tmp = w + 2 * b_keys;
+  auto* d_q = reinterpret_cast<uint32_t*>(w + 2 * b_keys + b_tmp);
+  auto* d_out = reinterpret_cast<double*>(w + 2 * b_keys + b_tmp + b_q);
+  auto* d_cnt = reinterpret_cast<unsigned long long*>(w + 2 * b_keys + b_tmp + b_q + b_out);
+  auto* d_ctr = reinterpret_cast<unsigned long long*>(w + 2 * b_keys + b_tmp + b_q + b_out + b_cnt);
+  int rc = ANOMOD_OK;
+  hipError_t e = hipMemcpyAsync(d_q, q_pct, nq * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess && n && spans->n_traces) {
+    // per-span (edge, latency) keys from the aggregation kernel's own walk and
+    // parent rule, then one radix sort over edge|dur
+    Table tab{};
+    tab.keys = keys;
+    tab.ctr = d_ctr;
+    KernelFn fn = edge_agg_kernel<kHtKeys, kStHbm>;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn),
+                                                     kThreads, 0);
+    const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
+    std::vector<uint64_t> cuts;
+    if (e == hipSuccess) rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts);
+    for (size_t k = 0; e == hipSuccess && rc == ANOMOD_OK && k + 1 < cuts.size(); ++k) {
+      e = hipMemsetAsync(d_ctr, 0, 8, ctx->stream);
+      if (e != hipSuccess) break;
+      hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
+                         spans->parent_span_id, spans->svc_flags, spans->dur_us,
+                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tab);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess && rc == ANOMOD_OK)
+      e = hipcub::DeviceRadixSort::SortKeys(tmp, sort_tmp, keys, sorted, n, 0, 32 + kbits,
+                                             ctx->stream);
+  }
+  if (e == hipSuccess && rc == ANOMOD_OK) {
+    hipLaunchKernelGGL(exact_pick_kernel, dim3((E + 255) / 256), dim3(256), 0, ctx->stream,
+                       sorted, spans->n_traces ? n : 0, E, d_q, nq, d_out, d_cnt);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && rc == ANOMOD_OK)
+    e = hipMemcpyAsync(out, d_out, E * nq * 8ull, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && rc == ANOMOD_OK && count)
+    e = hipMemcpyAsync(count, d_cnt, E * 8ull, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(w);
+  if (rc != ANOMOD_OK) return rc;
+  if (e != hipSuccess) {
+    set_error(ctx, "exact edge quantiles failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
   return ANOMOD_OK;
 }
 

@@ -33,7 +33,7 @@ import numpy as np  # noqa: E402
 import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
-LEGS = ("trace_structure", "in_trace_shuffled", "ungrouped", "tt_width", "pagerank", "ewma",
+LEGS = ("trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped", "tt_width", "pagerank", "ewma",
         "tt_config2")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
@@ -338,6 +338,23 @@ def main() -> int:
             "spans_per_s": allsum(spans.n_spans / (t_ms * 1e-3)), "kernel_ms": t_ms,
             "bytes_per_launch": ts_bytes, "achieved_GBps": ts_bytes / (t_ms * 1e-3) / 1e9,
             "frac": ts_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    if "exact_quantiles" in legs:
+        # --- §8a a11 cross-check: exact per-edge order statistics (edge keys
+        # + one radix sort) against the histogram quantiles of the headline
+        # table: the bin-midpoint error the histogram costs
+        t0 = time.perf_counter()
+        ex, cnt = ctx.edge_quantiles_exact(spans, (50, 99))
+        q_s = time.perf_counter() - t0
+        ok = cnt > 0
+        rel = {}
+        for k, name in ((0, "p50_us"), (1, "p99_us")):
+            h = getattr(table, name)[ok]
+            x = ex[ok, k]
+            r = np.abs(h - x) / np.maximum(x, 1.0)
+            rel[name] = {"max_rel_err": float(r.max()), "mean_rel_err": float(r.mean())}
+        result["exact_quantiles"] = {
+            "what": "exact x[(c*q)//100] per edge vs the 896-bin histogram midpoints",
+            "edges": int(ok.sum()), "seconds": q_s, **rel}
     if "in_trace_shuffled" in legs:
         # --- the same spans with every trace's spans in a random order (the
         # parent scan can no longer rely on parents sitting early)

@@ -228,6 +228,14 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
  * workspace the ctx keeps) then aggregate; a grouped set is aggregated as is. */
 int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
                                     uint32_t n_services, anomod_edge_table* out);
+/* Exact per-edge order statistics (SURVEY.md §8a a11 cross-check mode): the
+ * same per-span edges as the aggregation, one radix sort of (edge, latency)
+ * keys, then per edge x[(c * q_pct[k]) // 100] of its sorted latencies (the
+ * reference's sorted(x)[int(c*q)], monitor_http_responses.py:180-190).
+ * out: [E][nq] doubles (NaN for an empty edge); count: [E] (may be NULL).
+ * Needs a grouped set; q_pct[k] in [0, 99], nq <= 16.                       */
+int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
+                                const uint32_t* q_pct, uint32_t nq, double* out, uint64_t* count);
 /* One-shot host convenience: upload + aggregate + download.               */
 int anomod_edge_aggregate(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
                           const uint64_t* trace_ptr, uint64_t n_traces, anomod_edge_table* out);

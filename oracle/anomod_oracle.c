@@ -85,6 +85,31 @@ void oracle_edge_aggregate(uint32_t S, const uint64_t* span_id, const uint64_t* 
   }
 }
 
+/* The edge row of every span of traces [t0, t1) (the same first-match
+ * parent rule as oracle_edge_aggregate), for exact per-edge order
+ * statistics. */
+void oracle_span_edges(uint32_t S, const uint64_t* span_id, const uint64_t* parent,
+                       const uint16_t* svc, const uint64_t* trace_ptr, uint64_t t0, uint64_t t1,
+                       uint32_t* edge) {
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t a = trace_ptr[t], b = trace_ptr[t + 1];
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t pid = parent[i];
+      uint32_t p = S;
+      if (pid != 0) {
+        p = S + 1;
+        for (uint64_t q = a; q < b; ++q) {
+          if (span_id[q] == pid) {
+            p = svc[q];
+            break;
+          }
+        }
+      }
+      edge[i] = p * S + svc[i];
+    }
+  }
+}
+
 /* Nearest-rank quantile from a histogram row: rank r = (n*q_pct)//100
  * (monitor_http_responses.py:187-189), value = midpoint of the bin that
  * holds the r-th (0-based) sample; NaN when the row is empty. */

@@ -31,6 +31,8 @@ def lib():
         _lib.oracle_edge_aggregate.argtypes = [C.c_uint32] + [C.c_void_p] * 6 + [
             C.c_uint64, C.c_uint64] + [C.c_void_p] * 6
         _lib.oracle_quantiles.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
+        _lib.oracle_span_edges.argtypes = [C.c_uint32] + [C.c_void_p] * 4 + [
+            C.c_uint64, C.c_uint64, C.c_void_p]
         _lib.oracle_ewma_z.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_double,
                                        C.c_uint32, C.c_double, C.c_void_p]
         _lib.oracle_trace_structure.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_uint64,
@@ -84,6 +86,33 @@ def trace_structure(spans, S: int | None = None) -> dict:
     lib().oracle_trace_structure(*[_p(a) for a in arrs], 0, nt, words,
                                  *[_p(out[k]) for k in ("parent_pos", "depth", "n_children",
                                                         "span_flags", "n_roots", "svc_mask")])
+    return out
+
+
+def span_edges(spans, S: int | None = None) -> np.ndarray:
+    """Edge row of every span (first-match parent rule of the aggregation)."""
+    S = len(spans.services) if S is None else S
+    arrs = [np.ascontiguousarray(getattr(spans, k)) for k in
+            ("span_id", "parent_span_id", "svc", "trace_ptr")]
+    out = np.zeros(spans.n_spans, np.uint32)
+    lib().oracle_span_edges(S, *[_p(a) for a in arrs], 0, spans.n_traces, _p(out))
+    return out
+
+
+def exact_quantiles(spans, q_pct=(50, 99), S: int | None = None) -> np.ndarray:
+    """Per edge: sorted(latencies)[(c*q)//100] (monitor_http_responses.py:
+    180-190 nearest rank, floor index), NaN for an empty edge; [E, len(q)]."""
+    S = len(spans.services) if S is None else S
+    E = (S + 2) * S
+    e = span_edges(spans, S)
+    order = np.lexsort((spans.dur_us, e))
+    es, ds = e[order], spans.dur_us[order]
+    cnt = np.bincount(es, minlength=E)
+    start = np.r_[0, np.cumsum(cnt)[:-1]]
+    out = np.full((E, len(q_pct)), np.nan)
+    for k, q in enumerate(q_pct):
+        nz = cnt > 0
+        out[nz, k] = ds[start[nz] + cnt[nz] * q // 100]
     return out
 
 

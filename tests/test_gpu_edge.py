@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import anomod
-from oracle import native
+from oracle import native, spec
 
 pytestmark = pytest.mark.gpu
 
@@ -208,3 +208,23 @@ def test_multi_launch_split_bit_exact(ctx, monkeypatch, cap):
     assert_table_equal(ctx.edge_aggregate(sp), ref)
     monkeypatch.delenv("ANOMOD_MAX_LAUNCH_SPANS")
     assert_table_equal(ctx.edge_aggregate(sp), ref)
+
+
+@pytest.mark.parametrize("S,n_traces,max_len", [(12, 20000, 24), (46, 4000, 60), (3, 1, 3000)])
+def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
+    """§8a a11 cross-check mode: exact per-edge order statistics on the GPU
+    (edge keys from the aggregation walk + one radix sort) == numpy sort of
+    each edge's latencies; the histogram quantile sits within its bin."""
+    rng = np.random.default_rng(S + n_traces)
+    sp = _random_spanset(rng, S, n_traces, max_len, dup=0.02)
+    q = (0, 50, 95, 99)
+    got, cnt = ctx.edge_quantiles_exact(sp, q)
+    want = native.exact_quantiles(sp, q)
+    np.testing.assert_array_equal(got, want)
+    tab = native.finalize(native.edge_aggregate(sp))
+    np.testing.assert_array_equal(cnt, tab["count"])
+    ok = cnt > 0
+    for k, qq in ((1, "p50_us"), (3, "p99_us")):  # histogram midpoint vs exact: same bin
+        ex = got[ok, k].astype(np.uint32)
+        b = [spec.hist_bounds(spec.hist_bin(int(v))) for v in ex]
+        np.testing.assert_array_equal(tab[qq][ok], [0.5 * (lo + hi) for lo, hi in b])

@@ -184,3 +184,26 @@ def test_group_by_trace_is_a_stable_grouping():
     assert spec.group_by_trace(np.zeros(0, np.uint64))[1].tolist() == [0]
     # mix64 is the SplitMix64 finaliser
     assert int(spec.mix64([1])[0]) == 0x5692161D100B05E5
+
+
+def test_exact_edge_quantiles_follow_reference_percentiles(golden):
+    """oracle exact per-edge order statistics == the reference's own
+    generate_summary picks (sorted(x)[len//2], [int(n*0.99)]) on the
+    latency lists of tests/golden/percentiles.json, placed on one edge."""
+    import anomod
+    cases = json.loads((golden / "percentiles.json").read_text())
+    checked = 0
+    for case in cases:
+        lat = [v for v in case["latencies"] if v > 0]
+        if not lat or not all(float(v).is_integer() for v in lat):
+            continue
+        checked += 1
+        n = len(lat)
+        sp = anomod.SpanSet(["a"], np.array([0, n], np.uint64), np.zeros(n, np.uint64),
+                            np.arange(1, n + 1, dtype=np.uint64), np.zeros(n, np.uint64),
+                            np.zeros(n, np.uint16), np.zeros(n, np.uint16),
+                            np.asarray(lat, np.uint32))
+        q = native.exact_quantiles(sp, (50, 95, 99))
+        ref = case["latency_statistics"]  # written by the reference's generate_summary
+        assert (q[1, 0], q[1, 1], q[1, 2]) == (ref["median"], ref["p95"], ref["p99"])
+    assert checked >= 5
