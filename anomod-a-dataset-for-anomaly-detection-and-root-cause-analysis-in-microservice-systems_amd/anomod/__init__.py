@@ -12,7 +12,8 @@ ctypes C ABI (include/anomod.h); there is no CPU fallback.
 from ._lib import (FLAG_ERROR, HIST_BINS, HIST_SUB_BITS, AnomodError, EXPORTED_SYMBOLS,
                    LIB_PATH, lib)
 from .decode import (MetricMatrix, decode_jaeger, decode_native, load_trace_file, decode_metric_long_csv,
-                     decode_prometheus_csv_dir, decode_skywalking_payload, decode_skywalking_raw,
+                     decode_metric_long_csv_native, decode_prometheus_csv_dir,
+                     decode_prometheus_csv_dir_native, decode_skywalking_payload, decode_skywalking_raw,
                      jaeger_span_rows, merge_jaeger_dumps, skywalking_parents)
 from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec, device_count,
                      device_count_safe,
@@ -28,7 +29,8 @@ __all__ = [
     "AnomodError", "Context", "DeviceGraph", "DeviceSeries", "DeviceSpans", "EdgeTable",
     "EXPORTED_SYMBOLS", "Experiment", "FLAG_ERROR", "Features", "HIST_BINS", "HIST_SUB_BITS",
     "LIB_PATH", "MetricMatrix", "SpanSet", "SynthSpec", "decode_jaeger",
-    "decode_metric_long_csv", "decode_prometheus_csv_dir", "decode_skywalking_payload",
+    "decode_metric_long_csv", "decode_metric_long_csv_native", "decode_prometheus_csv_dir",
+    "decode_prometheus_csv_dir_native", "decode_skywalking_payload",
     "decode_skywalking_raw", "default_context", "device_count", "device_count_safe", "edge_rows", "fault_target",
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
     "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",

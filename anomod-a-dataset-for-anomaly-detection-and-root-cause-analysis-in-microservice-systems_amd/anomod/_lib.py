@@ -178,6 +178,15 @@ _SIGS = {
     "anomod_decoded_columns": (_i32, [_vp, _P(SpanSoA), _P(_u64)]),
     "anomod_decoded_free": (_i32, [_vp]),
     "anomod_hash64": (_u64, [C.c_char_p, _u64]),
+    "anomod_decode_metric_long_csv": (_i32, [C.c_char_p, _u64, _P(_vp)]),
+    "anomod_decode_prometheus_csvs": (_i32, [_P(C.c_char_p), _P(_u64), _P(C.c_char_p), _u32,
+                                             _P(_vp)]),
+    "anomod_metrics_info": (_i32, [_vp, _P(_u64), _P(_u64)]),
+    "anomod_metrics_matrix": (_i32, [_vp, _P(_f32), _P(_f64)]),
+    "anomod_metrics_series_name": (C.c_char_p, [_vp, _u64]),
+    "anomod_metrics_series_nlabels": (_u32, [_vp, _u64]),
+    "anomod_metrics_series_label": (C.c_char_p, [_vp, _u64, _u32, _P(C.c_char_p)]),
+    "anomod_metrics_free": (_i32, [_vp]),
     "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),
     "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),

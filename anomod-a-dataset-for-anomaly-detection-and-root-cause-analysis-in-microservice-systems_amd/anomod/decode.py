@@ -363,6 +363,52 @@ def decode_prometheus_csv_dir(directory) -> MetricMatrix:
     return _to_matrix(samples, ts_set)
 
 
+def _metrics_from_handle(h) -> MetricMatrix:
+    lib = L.lib()
+    try:
+        T, S = C.c_uint64(), C.c_uint64()
+        L.check(lib.anomod_metrics_info(h, C.byref(T), C.byref(S)))
+        X = np.empty((T.value, S.value), np.float32)
+        ts = np.empty(T.value, np.float64)
+        L.check(lib.anomod_metrics_matrix(h, L.ptr(X, C.c_float), L.ptr(ts, C.c_double)))
+        series = []
+        val = C.c_char_p()
+        for s in range(S.value):
+            name = lib.anomod_metrics_series_name(h, s).decode()
+            labels = []
+            for j in range(lib.anomod_metrics_series_nlabels(h, s)):
+                k = lib.anomod_metrics_series_label(h, s, j, C.byref(val))
+                labels.append((k.decode(), val.value.decode()))
+            series.append((name, tuple(labels)))
+    finally:
+        lib.anomod_metrics_free(h)
+    return MetricMatrix(X, ts, series)
+
+
+def decode_metric_long_csv_native(path_or_bytes) -> MetricMatrix:
+    """decode_metric_long_csv in libanomod (csrc/metrics_decode.cpp): the
+    same matrix, without a Python dict per row."""
+    data = (path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray))
+            else Path(path_or_bytes).read_bytes())
+    h = C.c_void_p()
+    L.check(L.lib().anomod_decode_metric_long_csv(bytes(data), len(data), C.byref(h)))
+    return _metrics_from_handle(h)
+
+
+def decode_prometheus_csv_dir_native(directory) -> MetricMatrix:
+    """decode_prometheus_csv_dir in libanomod: one CSV per query, files in
+    sorted path order, series = (file stem, 'metric' column)."""
+    paths = sorted(Path(directory).glob("*.csv"))
+    blobs = [p.read_bytes() for p in paths]
+    n = len(paths)
+    data = (C.c_char_p * max(1, n))(*blobs)
+    lens = (C.c_uint64 * max(1, n))(*[len(b) for b in blobs])
+    stems = (C.c_char_p * max(1, n))(*[p.stem.encode() for p in paths])
+    h = C.c_void_p()
+    L.check(L.lib().anomod_decode_prometheus_csvs(data, lens, stems, n, C.byref(h)))
+    return _metrics_from_handle(h)
+
+
 # --------------------------------------------------------------------------
 # Native decoders (libanomod, csrc/decode.cpp): same columns as the Python
 # decoders above, without a Python object per span

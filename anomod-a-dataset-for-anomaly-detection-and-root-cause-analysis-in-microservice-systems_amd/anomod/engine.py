@@ -124,8 +124,8 @@ def load_experiment(source, *, metrics=None, name: str | None = None,
     mm = None
     if metrics is not None:
         mp = Path(metrics)
-        mm = (decode.decode_prometheus_csv_dir(mp) if mp.is_dir()
-              else decode.decode_metric_long_csv(mp))
+        mm = (decode.decode_prometheus_csv_dir_native(mp) if mp.is_dir()
+              else decode.decode_metric_long_csv_native(mp))
     return Experiment(exp_name, spans, mm, fault_target(exp_name), {"trace_file": str(doc_path)})
 
 

@@ -1,0 +1,463 @@
+// Native metric-file decoders (host C++): the
+// Prometheus CSVs the reference's collectors write -> the time-major series
+// matrix X[T][S] the EWMA/z kernels read, without a Python dict per row.
+//
+//  TT long CSV (metric_collector.py:400-478; rows :427-443, column order
+//  :453-467): metric_name,timestamp,datetime,value,<sorted label columns>.
+//    series key = (metric_name, the row's non-empty label (name, value) pairs
+//    sorted); value '' = missing ('NaN' -> None -> '' at :435); the collector
+//    queries three metrics twice (key_metrics :37-109, loop :420-423), so rows
+//    are de-duplicated on (series, timestamp), first occurrence kept.
+//  SN metric directory (fetch_prometheus_metrics.py:47-67 + main :92-102, one
+//    CSV per query as collect_metric.sh names them): timestamp = naive local
+//    datetime string, value, metric = the label string (:51), one column per
+//    label.  series key = (file stem, the 'metric' column).
+//
+// Rules shared with anomod/decode.py (decode_metric_long_csv /
+// decode_prometheus_csv_dir), whose outputs the tests pin to the reference's
+// files: CSV per Python's csv module (excel dialect: "" escapes inside quoted
+// fields, \r\n or \n records; a header name repeated keeps the last column),
+// values and TT timestamps by strtod (Python float(): correctly rounded),
+// datetime strings as datetime.fromisoformat(..).timestamp() (naive = local
+// time: seconds + microseconds / 1e6; with an offset: exact microseconds /
+// 1e6), timestamps = the sorted distinct values over all rows, series sorted
+// as Python sorts the key tuples, X f32 with NaN where a series has no row.
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <deque>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/anomod.h"
+
+namespace anomod {
+void set_error(anomod_ctx* ctx, const char* fmt, ...);
+}
+
+struct anomod_metrics {
+  struct Series {
+    std::string name;                                        // metric_name / file stem
+    std::vector<std::pair<std::string, std::string>> labels;  // sorted by (name, value)
+  };
+  std::vector<Series> series;  // sorted
+  std::vector<double> ts;      // sorted distinct timestamps
+  std::vector<float> X;        // [T][S]
+};
+
+namespace {
+
+using Labels = std::vector<std::pair<std::string, std::string>>;
+
+// One CSV record: field views (quoted fields with "" escapes are unescaped
+// into `scratch`, which stays alive until the next record).
+struct CsvReader {
+  const char* p;
+  const char* end;
+  std::deque<std::string> scratch;  // stable addresses: fields view into them
+  std::vector<std::string_view> fields;
+
+  CsvReader(const char* b, size_t n) : p(b), end(b + n) {}
+
+  bool next() {  // false at end of input
+    fields.clear();
+    size_t used = 0;
+    if (p >= end) return false;
+    while (true) {
+      if (p < end && *p == '"') {  // quoted field
+        ++p;
+        if (used == scratch.size()) scratch.emplace_back();
+        std::string& s = scratch[used++];
+        s.clear();
+        while (p < end) {
+          const char* q = static_cast<const char*>(memchr(p, '"', (size_t)(end - p)));
+          if (!q) {  // unterminated: the rest of the input
+            s.append(p, (size_t)(end - p));
+            p = end;
+            break;
+          }
+          s.append(p, (size_t)(q - p));
+          p = q + 1;
+          if (p < end && *p == '"') {
+            s.push_back('"');
+            ++p;
+            continue;
+          }
+          break;
+        }
+        // text after the closing quote up to the delimiter joins the field
+        // (the csv module keeps it)
+        const char* f = p;
+        while (p < end && *p != ',' && *p != '\n' && *p != '\r') ++p;
+        s.append(f, (size_t)(p - f));
+        fields.emplace_back(s);
+      } else {
+        const char* f = p;
+        while (p < end && *p != ',' && *p != '\n' && *p != '\r') ++p;
+        fields.emplace_back(f, (size_t)(p - f));
+      }
+      if (p < end && *p == ',') {
+        ++p;
+        continue;
+      }
+      // end of record
+      if (p < end && *p == '\r') ++p;
+      if (p < end && *p == '\n') ++p;
+      return true;
+    }
+  }
+};
+
+bool parse_float(std::string_view v, double& out) {  // Python float() of a CSV field
+  std::string s(v);
+  const char* b = s.c_str();
+  while (*b == ' ' || *b == '\t') ++b;
+  if (!*b) return false;
+  char* e = nullptr;
+  errno = 0;
+  out = strtod(b, &e);
+  if (e == b) return false;
+  while (*e == ' ' || *e == '\t' || *e == '\n' || *e == '\r') ++e;
+  return *e == '\0';
+}
+
+int digits(std::string_view s, size_t at, size_t n, int& v) {
+  if (at + n > s.size()) return 0;
+  v = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const char c = s[at + i];
+    if (c < '0' || c > '9') return 0;
+    v = v * 10 + (c - '0');
+  }
+  return 1;
+}
+
+// datetime.fromisoformat(s).timestamp() for the forms pandas writes:
+// YYYY-MM-DD[?HH[:MM[:SS[.fff|.ffffff]]]][+HH:MM[:SS[.ffffff]]|-HH:MM...]
+bool iso_timestamp(std::string_view s, double& out) {
+  int Y, M, D, h = 0, m = 0, sec = 0, us = 0;
+  if (!digits(s, 0, 4, Y) || s.size() < 10 || s[4] != '-' || !digits(s, 5, 2, M) || s[7] != '-' ||
+      !digits(s, 8, 2, D))
+    return false;
+  size_t i = 10;
+  bool aware = false;
+  long long off_us = 0;
+  if (i < s.size()) {
+    ++i;  // any one separator character
+    if (!digits(s, i, 2, h)) return false;
+    i += 2;
+    if (i < s.size() && s[i] == ':') {
+      if (!digits(s, i + 1, 2, m)) return false;
+      i += 3;
+      if (i < s.size() && s[i] == ':') {
+        if (!digits(s, i + 1, 2, sec)) return false;
+        i += 3;
+        if (i < s.size() && s[i] == '.') {
+          size_t j = i + 1;
+          while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j;
+          const size_t nd = j - i - 1;
+          if (nd != 3 && nd != 6) return false;
+          int f = 0;
+          digits(s, i + 1, nd, f);
+          us = nd == 3 ? f * 1000 : f;
+          i = j;
+        }
+      }
+    }
+    if (i < s.size()) {  // UTC offset
+      if (s[i] != '+' && s[i] != '-') return false;
+      const int sign = s[i] == '-' ? -1 : 1;
+      int oh, om, os = 0, ous = 0;
+      if (!digits(s, i + 1, 2, oh) || i + 3 >= s.size() || s[i + 3] != ':' ||
+          !digits(s, i + 4, 2, om))
+        return false;
+      size_t j = i + 6;
+      if (j < s.size() && s[j] == ':') {
+        if (!digits(s, j + 1, 2, os)) return false;
+        j += 3;
+        if (j < s.size() && s[j] == '.') {
+          if (!digits(s, j + 1, 6, ous)) return false;
+          j += 7;
+        }
+      }
+      if (j != s.size()) return false;
+      aware = true;
+      off_us = sign * (((long long)oh * 3600 + om * 60 + os) * 1000000LL + ous);
+    }
+  }
+  if (M < 1 || M > 12 || D < 1 || D > 31 || h > 23 || m > 59 || sec > 59) return false;
+  struct tm t;
+  memset(&t, 0, sizeof t);
+  t.tm_year = Y - 1900;
+  t.tm_mon = M - 1;
+  t.tm_mday = D;
+  t.tm_hour = h;
+  t.tm_min = m;
+  t.tm_sec = sec;
+  if (aware) {  // (self - epoch).total_seconds(): exact microseconds / 1e6
+    const long long u = (long long)timegm(&t) * 1000000LL + us - off_us;
+    out = (double)u / 1e6;
+  } else {  // local time: seconds + microseconds / 1e6
+    t.tm_isdst = -1;
+    const time_t u = mktime(&t);
+    out = (double)u + us / 1e6;
+  }
+  return true;
+}
+
+struct Sample {
+  double t;
+  float v;
+  uint32_t series;
+  uint64_t order;  // row order: first occurrence wins
+};
+
+struct Builder {
+  std::unordered_map<std::string, uint32_t> index;  // serialised key -> provisional series
+  std::vector<anomod_metrics::Series> series;
+  std::vector<Sample> samples;
+  std::string key;
+
+  uint32_t series_of(const std::string& name, const Labels& labels) {
+    key.assign(name);
+    for (const auto& kv : labels) {
+      key.push_back('\0');
+      key.append(kv.first);
+      key.push_back('\0');
+      key.append(kv.second);
+    }
+    auto it = index.find(key);
+    if (it != index.end()) return it->second;
+    const uint32_t id = (uint32_t)series.size();
+    index.emplace(key, id);
+    series.push_back({name, labels});
+    return id;
+  }
+
+  anomod_metrics* finish() {
+    auto* out = new anomod_metrics();
+    // series in Python tuple order
+    std::vector<uint32_t> order(series.size());
+    for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      if (series[a].name != series[b].name) return series[a].name < series[b].name;
+      return series[a].labels < series[b].labels;
+    });
+    std::vector<uint32_t> rank(series.size());
+    for (uint32_t i = 0; i < order.size(); ++i) rank[order[i]] = i;
+    out->series.reserve(series.size());
+    for (uint32_t i : order) out->series.push_back(std::move(series[i]));
+    // distinct timestamps
+    out->ts.reserve(samples.size());
+    for (const Sample& s : samples) out->ts.push_back(s.t);
+    std::sort(out->ts.begin(), out->ts.end());
+    out->ts.erase(std::unique(out->ts.begin(), out->ts.end()), out->ts.end());
+    const size_t T = out->ts.size(), S = out->series.size();
+    out->X.assign(T * S, std::nanf(""));
+    // first occurrence per (series, t): later rows of the same cell skipped
+    std::vector<uint8_t> seen(T * S, 0);
+    for (const Sample& s : samples) {  // samples are in row order
+      const size_t c = (size_t)(std::lower_bound(out->ts.begin(), out->ts.end(), s.t) -
+                                out->ts.begin());
+      const size_t cell = c * S + rank[s.series];
+      if (seen[cell]) continue;
+      seen[cell] = 1;
+      out->X[cell] = s.v;
+    }
+    return out;
+  }
+};
+
+// Columns of a header: name -> the LAST index with that name (a dict built
+// from the row keeps the last value of a repeated name).
+std::vector<int> header_last(const std::vector<std::string>& hdr) {
+  std::vector<int> keep(hdr.size(), 1);
+  for (size_t i = 0; i < hdr.size(); ++i)
+    for (size_t j = i + 1; j < hdr.size(); ++j)
+      if (hdr[i] == hdr[j]) keep[i] = 0;
+  return keep;
+}
+
+int find_col(const std::vector<std::string>& hdr, const char* name) {
+  int at = -1;
+  for (size_t i = 0; i < hdr.size(); ++i)
+    if (hdr[i] == name) at = (int)i;
+  return at;
+}
+
+int decode_long(const char* data, uint64_t len, Builder& b) {
+  CsvReader rd(data, len);
+  if (!rd.next()) return ANOMOD_OK;  // empty file: no rows
+  std::vector<std::string> hdr(rd.fields.begin(), rd.fields.end());
+  const std::vector<int> keep = header_last(hdr);
+  const int c_name = find_col(hdr, "metric_name"), c_ts = find_col(hdr, "timestamp"),
+            c_val = find_col(hdr, "value");
+  std::vector<int> label_cols;
+  for (size_t i = 0; i < hdr.size(); ++i)
+    if (keep[i] && hdr[i] != "metric_name" && hdr[i] != "timestamp" && hdr[i] != "datetime" &&
+        hdr[i] != "value")
+      label_cols.push_back((int)i);
+  if (c_name < 0 || c_ts < 0) {
+    anomod::set_error(nullptr, "metric CSV: no metric_name / timestamp column");
+    return ANOMOD_EINVAL;
+  }
+  Labels labels;
+  uint64_t row = 0;
+  while (rd.next()) {
+    if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;  // blank line (skipped)
+    ++row;
+    const auto field = [&](int c) -> std::string_view {
+      return c >= 0 && (size_t)c < rd.fields.size() ? rd.fields[c] : std::string_view();
+    };
+    labels.clear();
+    for (int c : label_cols) {
+      const std::string_view v = field(c);
+      if (!v.empty()) labels.emplace_back(hdr[c], std::string(v));
+    }
+    std::sort(labels.begin(), labels.end());
+    double t;
+    if (!parse_float(field(c_ts), t) || std::isnan(t)) {
+      anomod::set_error(nullptr, "metric CSV row %llu: bad timestamp '%.*s'",
+                        (unsigned long long)row, (int)field(c_ts).size(), field(c_ts).data());
+      return ANOMOD_EINVAL;
+    }
+    const std::string_view vs = field(c_val);
+    double v = NAN;
+    if (!vs.empty() && !parse_float(vs, v)) {
+      anomod::set_error(nullptr, "metric CSV row %llu: bad value '%.*s'", (unsigned long long)row,
+                        (int)vs.size(), vs.data());
+      return ANOMOD_EINVAL;
+    }
+    const uint32_t s = b.series_of(std::string(field(c_name)), labels);
+    b.samples.push_back({t, (float)v, s, b.samples.size()});
+  }
+  return ANOMOD_OK;
+}
+
+int decode_prom(const char* data, uint64_t len, const std::string& stem, Builder& b) {
+  CsvReader rd(data, len);
+  if (!rd.next()) return ANOMOD_OK;
+  std::vector<std::string> hdr(rd.fields.begin(), rd.fields.end());
+  const int c_ts = find_col(hdr, "timestamp"), c_val = find_col(hdr, "value"),
+            c_met = find_col(hdr, "metric");
+  if (c_ts < 0) {
+    anomod::set_error(nullptr, "%s: no timestamp column", stem.c_str());
+    return ANOMOD_EINVAL;
+  }
+  Labels labels(1);
+  labels[0].first = "metric";
+  uint64_t row = 0;
+  while (rd.next()) {
+    if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;
+    ++row;
+    const auto field = [&](int c) -> std::string_view {
+      return c >= 0 && (size_t)c < rd.fields.size() ? rd.fields[c] : std::string_view();
+    };
+    double t;
+    if (!iso_timestamp(field(c_ts), t)) {
+      anomod::set_error(nullptr, "%s row %llu: bad timestamp '%.*s'", stem.c_str(),
+                        (unsigned long long)row, (int)field(c_ts).size(), field(c_ts).data());
+      return ANOMOD_EINVAL;
+    }
+    const std::string_view vs = field(c_val);
+    double v = NAN;
+    if (!vs.empty() && !parse_float(vs, v)) {
+      anomod::set_error(nullptr, "%s row %llu: bad value '%.*s'", stem.c_str(),
+                        (unsigned long long)row, (int)vs.size(), vs.data());
+      return ANOMOD_EINVAL;
+    }
+    labels[0].second.assign(field(c_met));
+    const uint32_t s = b.series_of(stem, labels);
+    b.samples.push_back({t, (float)v, s, b.samples.size()});
+  }
+  return ANOMOD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int anomod_decode_metric_long_csv(const char* data, uint64_t len, anomod_metrics** out) {
+  if (!out || (!data && len)) {
+    anomod::set_error(nullptr, "anomod_decode_metric_long_csv: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  *out = nullptr;
+  try {
+    Builder b;
+    if (int rc = decode_long(data, len, b)) return rc;
+    *out = b.finish();
+  } catch (const std::bad_alloc&) {
+    anomod::set_error(nullptr, "out of host memory decoding a metric CSV");
+    return ANOMOD_ENOMEM;
+  }
+  return ANOMOD_OK;
+}
+
+int anomod_decode_prometheus_csvs(const char* const* data, const uint64_t* lens,
+                                  const char* const* stems, uint32_t n_files,
+                                  anomod_metrics** out) {
+  if (!out || (n_files && (!data || !lens || !stems))) {
+    anomod::set_error(nullptr, "anomod_decode_prometheus_csvs: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  *out = nullptr;
+  try {
+    Builder b;
+    for (uint32_t f = 0; f < n_files; ++f)
+      if (int rc = decode_prom(data[f], lens[f], stems[f] ? stems[f] : "", b)) return rc;
+    *out = b.finish();
+  } catch (const std::bad_alloc&) {
+    anomod::set_error(nullptr, "out of host memory decoding metric CSVs");
+    return ANOMOD_ENOMEM;
+  }
+  return ANOMOD_OK;
+}
+
+int anomod_metrics_info(const anomod_metrics* m, uint64_t* T, uint64_t* S) {
+  if (!m) {
+    anomod::set_error(nullptr, "anomod_metrics_info: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  if (T) *T = m->ts.size();
+  if (S) *S = m->series.size();
+  return ANOMOD_OK;
+}
+
+int anomod_metrics_matrix(const anomod_metrics* m, float* X, double* timestamps) {
+  if (!m) {
+    anomod::set_error(nullptr, "anomod_metrics_matrix: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  if (X && !m->X.empty()) memcpy(X, m->X.data(), m->X.size() * sizeof(float));
+  if (timestamps && !m->ts.empty()) memcpy(timestamps, m->ts.data(), m->ts.size() * sizeof(double));
+  return ANOMOD_OK;
+}
+
+const char* anomod_metrics_series_name(const anomod_metrics* m, uint64_t s) {
+  return m && s < m->series.size() ? m->series[s].name.c_str() : nullptr;
+}
+
+uint32_t anomod_metrics_series_nlabels(const anomod_metrics* m, uint64_t s) {
+  return m && s < m->series.size() ? (uint32_t)m->series[s].labels.size() : 0u;
+}
+
+const char* anomod_metrics_series_label(const anomod_metrics* m, uint64_t s, uint32_t j,
+                                        const char** value) {
+  if (!m || s >= m->series.size() || j >= m->series[s].labels.size()) return nullptr;
+  if (value) *value = m->series[s].labels[j].second.c_str();
+  return m->series[s].labels[j].first.c_str();
+}
+
+int anomod_metrics_free(anomod_metrics* m) {
+  delete m;
+  return ANOMOD_OK;
+}
+
+}  // extern "C"

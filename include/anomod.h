@@ -212,6 +212,33 @@ int anomod_decoded_free(anomod_decoded* d);
 /* The 64-bit id hash of the decoders (xxh64, seed 0; 0 maps to 1).       */
 uint64_t anomod_hash64(const char* s, uint64_t len);
 
+/* ---- native metric-file decoders --------------
+ * Prometheus CSVs -> the time-major series matrix X[T][S] (f32, NaN = no
+ * sample) the EWMA/z kernels read:
+ *   anomod_decode_metric_long_csv   TT long CSV of metric_collector.py:400-478
+ *                                   (series = (metric_name, sorted non-empty
+ *                                   labels); rows de-duplicated on (series,
+ *                                   timestamp), first kept, :420-423)
+ *   anomod_decode_prometheus_csvs   SN metric directory, one CSV per query as
+ *                                   fetch_prometheus_metrics.py:47-67,99 writes
+ *                                   it (series = (file stem, 'metric' label
+ *                                   string); naive datetimes read as local time)
+ * Timestamps are the sorted distinct values of all rows; series are sorted
+ * by (name, labels).  The same rules as anomod/decode.py's Python decoders. */
+typedef struct anomod_metrics anomod_metrics;
+int anomod_decode_metric_long_csv(const char* data, uint64_t len, anomod_metrics** out);
+int anomod_decode_prometheus_csvs(const char* const* data, const uint64_t* lens,
+                                  const char* const* stems, uint32_t n_files,
+                                  anomod_metrics** out);
+int anomod_metrics_info(const anomod_metrics* m, uint64_t* T, uint64_t* S);
+int anomod_metrics_matrix(const anomod_metrics* m, float* X /* [T][S] */,
+                          double* timestamps /* [T] */);
+const char* anomod_metrics_series_name(const anomod_metrics* m, uint64_t s);
+uint32_t anomod_metrics_series_nlabels(const anomod_metrics* m, uint64_t s);
+const char* anomod_metrics_series_label(const anomod_metrics* m, uint64_t s, uint32_t j,
+                                        const char** value);
+int anomod_metrics_free(anomod_metrics* m);
+
 /* ---- edge aggregation (the hot path) -------------------------------------
  * Call-graph edge table with per-edge latency histogram, count, errors,
  * sum/min/max and p50/p99.  Replaces and extends the per-span loops of

@@ -1,0 +1,103 @@
+"""Native metric-file decoders (csrc/metrics_decode.cpp) against the Python
+decoders (anomod/decode.py) — which tests/test_decode.py pins to the files
+the reference wrote — on the reference goldens and on fuzzed CSVs.  No GPU."""
+import csv
+import io
+import random
+import time
+
+import numpy as np
+import pytest
+
+import anomod
+
+
+def _same(a: anomod.MetricMatrix, b: anomod.MetricMatrix):
+    assert a.series == b.series
+    np.testing.assert_array_equal(a.timestamps, b.timestamps)
+    np.testing.assert_array_equal(a.X, b.X)  # NaN == NaN here
+
+
+@pytest.fixture
+def utc(monkeypatch):
+    monkeypatch.setenv("TZ", "UTC")
+    time.tzset()
+    yield
+    monkeypatch.undo()
+    time.tzset()
+
+
+def test_long_csv_golden(golden):
+    p = golden / "metric_long.csv"
+    _same(anomod.decode_metric_long_csv_native(p), anomod.decode_metric_long_csv(p))
+
+
+def test_prometheus_dir_golden(golden, utc):
+    d = golden / "prom_dir"
+    _same(anomod.decode_prometheus_csv_dir_native(d), anomod.decode_prometheus_csv_dir(d))
+
+
+def _fuzz_long(rng: random.Random, rows: int) -> bytes:
+    labels = ["instance", "pod", "namespace", "job", "container", "le", "name"]
+    vals = ['ts-order-service-7d9c', 'a,b', 'say "hi"', 'x\ny', '', 'ünï', '10.0.0.1:9100']
+    buf = io.StringIO()
+    w = csv.writer(buf, lineterminator=rng.choice(["\n", "\r\n"]))
+    cols = ["metric_name", "timestamp", "datetime", "value"] + sorted(rng.sample(labels, 5))
+    if rng.random() < 0.3:
+        cols.append(cols[-1])  # a repeated header name: the last column wins
+    w.writerow(cols)
+    names = ["up", "process_open_fds", "container_memory_usage_bytes", "node_load1"]
+    for _ in range(rows):
+        t = 1762178400 + 15 * rng.randrange(40) + rng.choice([0, 0, 0.5, 0.25])
+        v = rng.choice(["", "NaN", "inf", "-inf", "1e-7", repr(rng.uniform(-1e9, 1e9)),
+                        str(rng.randrange(1000)), " 2.5 "])
+        if v == "NaN":
+            v = ""
+        row = [rng.choice(names), repr(t), "2025-11-03T14:00:00", v]
+        row += [rng.choice(vals) for _ in cols[4:]]
+        if rng.random() < 0.05:
+            row = row[: rng.randrange(2, len(row))]  # short rows
+        w.writerow(row)
+        if rng.random() < 0.02:
+            buf.write("\n")  # blank line
+    return buf.getvalue().encode()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_long_csv_fuzz(seed, tmp_path):
+    data = _fuzz_long(random.Random(seed), 400)
+    p = tmp_path / "m.csv"
+    p.write_bytes(data)
+    _same(anomod.decode_metric_long_csv_native(data), anomod.decode_metric_long_csv(p))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_prometheus_dir_fuzz(seed, tmp_path, utc):
+    rng = random.Random(seed)
+    for f in range(rng.randrange(1, 5)):
+        buf = io.StringIO()
+        w = csv.writer(buf)
+        w.writerow(["timestamp", "value", "metric", "service"])
+        for _ in range(rng.randrange(0, 80)):
+            sec = rng.randrange(60)
+            frac = rng.choice(["", ".500", ".250000", ".123456"])
+            ts = f"2025-11-03 22:{rng.randrange(60):02d}:{sec:02d}{frac}"
+            v = rng.choice(["", "inf", repr(rng.uniform(0, 1e6)), "3"])
+            svc = rng.choice(["media-service", "text-service", ""])
+            w.writerow([ts, v, f'service="{svc}"' if svc else "", svc])
+        (tmp_path / f"q{f}_{rng.randrange(100)}.csv").write_text(buf.getvalue())
+    _same(anomod.decode_prometheus_csv_dir_native(tmp_path),
+          anomod.decode_prometheus_csv_dir(tmp_path))
+
+
+def test_empty_and_header_only(tmp_path):
+    for data in (b"", b"metric_name,timestamp,datetime,value\n"):
+        m = anomod.decode_metric_long_csv_native(data)
+        assert m.T == 0 and m.S == 0
+
+
+def test_bad_rows_raise():
+    with pytest.raises(anomod.AnomodError):
+        anomod.decode_metric_long_csv_native(b"metric_name,timestamp,datetime,value\nup,x,y,1\n")
+    with pytest.raises(anomod.AnomodError):
+        anomod.decode_metric_long_csv_native(b"metric_name,timestamp,datetime,value\nup,1,y,zz\n")
