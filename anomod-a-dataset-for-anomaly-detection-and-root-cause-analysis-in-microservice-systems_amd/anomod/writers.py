@@ -151,3 +151,114 @@ def to_text(writer, *args) -> str:
     buf = io.StringIO(newline="")
     writer(*args, buf)
     return buf.getvalue()
+
+
+# --------------------------------------------------------------------------
+# TT files of one experiment from a span set / metric matrix (the layouts
+# load_experiment reads: trace_collector.py:564-581 payload, json.dump
+# indent=2; metric_collector.py:453-467 long CSV).  Used to stage the
+# dataset's file formats at their LFS sizes for end-to-end timing.
+# --------------------------------------------------------------------------
+def _utc_iso_ms(ms: int) -> str:  # utc_iso (trace_collector.py:126-131)
+    return datetime.utcfromtimestamp(ms / 1000).isoformat(timespec="milliseconds") + "Z"
+
+
+def skywalking_payload(spans, experiment_name: str, t0_ms: int = 1762178400000) -> dict:
+    """A collector payload ({metadata, traces}) holding `spans`: one segment
+    per trace, node ids "{segment}:{k}", SpanRecord.to_dict fields
+    (trace_collector.py:86-123), durations in whole ms."""
+    import numpy as np  # noqa: F401  (spans columns are numpy arrays)
+
+    traces = []
+    services_seen = set()
+    ptr = spans.trace_ptr.tolist()
+    sid = spans.span_id.tolist()
+    pid = spans.parent_span_id.tolist()
+    svc = spans.svc.tolist()
+    fl = spans.flags.tolist()
+    dur = spans.dur_us.tolist()
+    names = spans.services
+    for t in range(spans.n_traces):
+        a, b = ptr[t], ptr[t + 1]
+        if a == b:
+            continue
+        tid = f"{t:08x}.{spans.trace_hash[a]:016x}"
+        seg = f"seg{t:08x}"
+        pos = {}
+        for i in range(a, b):
+            pos.setdefault(sid[i], i - a)
+        start = t0_ms + t
+        recs, roots, svcs = [], [], set()
+        for i in range(a, b):
+            k = i - a
+            p = pos.get(pid[i]) if pid[i] else None
+            node, pnode = f"{seg}:{k}", (f"{seg}:{p}" if p is not None else None)
+            if pnode is None:
+                roots.append(node)
+            s_ms = start + k
+            e_ms = s_ms + dur[i] // 1000
+            sc = names[svc[i]]
+            svcs.add(sc)
+            tags = [{"key": "http.method", "value": "GET"},
+                    {"key": "url", "value": f"http://{sc}:8080/api/v1/op{k}"}]
+            recs.append({
+                "node_id": node, "trace_id": tid, "segment_id": seg, "span_id": k,
+                "parent_span_id": p if p is not None else -1, "parent_node_id": pnode,
+                "depth": 0, "children_node_ids": [], "service_code": sc,
+                "service_instance": f"{sc}-7d9c4b6f5-x2x9k", "start_time_utc": _utc_iso_ms(s_ms),
+                "end_time_utc": _utc_iso_ms(e_ms), "start_timestamp_ms": s_ms,
+                "end_timestamp_ms": e_ms, "duration_ms": e_ms - s_ms,
+                "endpoint_name": f"/api/v1/op{k}", "type": "Entry" if p is None else "Exit",
+                "peer": None if p is None else f"{sc}:8080", "component": "SpringMVC",
+                "layer": "Http", "is_error": bool(fl[i] & 1), "tags": tags,
+                "tags_map": {d["key"]: d["value"] for d in tags}, "logs": [], "refs": []})
+        services_seen |= svcs
+        traces.append({"summary": {"trace_id": tid, "segment_id": seg, "duration": 0,
+                                   "start": str(start), "endpoint_names": ["/api"],
+                                   "is_error": False},
+                       "span_count": len(recs), "services_involved": sorted(svcs),
+                       "root_span_node_ids": roots, "spans": recs})
+    return {"metadata": {"generated_at": "2025-11-03T14:02:00Z", "lookback_hours": 1,
+                         "requested_trace_limit": len(traces), "min_trace_duration_ms": 0,
+                         "collected_traces": len(traces), "available_total": len(traces),
+                         "services_discovered": sorted(services_seen),
+                         "experiment_name": experiment_name,
+                         "skywalking_base_url": "http://skywalking-oap:12800",
+                         "skywalking_graphql": "http://skywalking-oap:12800/graphql"},
+            "traces": traces}
+
+
+def write_metric_long_csv_matrix(X, timestamps, series, out) -> int:
+    """A metric matrix as the TT long CSV (metric_collector.py:453-467:
+    metric_name, timestamp, datetime, value, then the sorted label columns;
+    NaN -> empty), one row per (series, timestamp), series-major as the
+    collector emits them.  Vectorised over a series' samples."""
+    import numpy as np
+
+    label_names = sorted({k for _, labels in series for k, _ in labels})
+    ts = np.asarray(timestamps)
+    ts_txt = np.array([repr(float(t)) if not float(t).is_integer() else str(int(t)) for t in ts],
+                      dtype=object)
+    dt_txt = np.array([datetime.utcfromtimestamp(float(t)).strftime("%Y-%m-%d %H:%M:%S")
+                       for t in ts], dtype=object)
+    head = ",".join(["metric_name", "timestamp", "datetime", "value"] + label_names) + "\n"
+    rows = 0
+    with open(out, "w", encoding="utf-8", newline="") as fh:
+        fh.write(head)
+        for j, (name, labels) in enumerate(series):
+            d = dict(labels)
+            tail = "," + ",".join(_csv_field(d.get(k, "")) for k in label_names) + "\n"
+            col = X[:, j].astype(np.float64)
+            vals = np.char.mod("%.9g", col).astype(object)
+            vals[np.isnan(col)] = ""
+            pre = _csv_field(name) + ","
+            fh.write("".join((pre + ts_txt + "," + dt_txt + "," + vals + tail).tolist()))
+            rows += col.shape[0]
+    return rows
+
+
+def _csv_field(v: str) -> str:
+    v = str(v)
+    if any(c in v for c in ',"\r\n'):
+        return '"' + v.replace('"', '""') + '"'
+    return v

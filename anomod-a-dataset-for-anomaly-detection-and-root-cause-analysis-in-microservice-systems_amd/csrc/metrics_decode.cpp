@@ -32,6 +32,7 @@
 #include <deque>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -114,9 +115,55 @@ struct CsvReader {
   }
 };
 
+// Clinger's fast path: [-]digits[.digits] with <= 15 significant digits and
+// <= 22 fraction digits is m / 10^k with both exact doubles, so the one IEEE
+// division is the correctly rounded value strtod returns.
+bool fast_decimal(std::string_view v, double& out) {
+  static const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                  1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                  1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  size_t i = 0;
+  const bool neg = !v.empty() && v[0] == '-';
+  if (neg) ++i;
+  uint64_t m = 0;
+  int nd = 0, frac = -1;
+  for (; i < v.size(); ++i) {
+    const char c = v[i];
+    if (c >= '0' && c <= '9') {
+      if (m == 0 && c == '0') {  // leading zeros do not count
+        if (frac >= 0) ++frac;
+        continue;
+      }
+      if (++nd > 15) return false;
+      m = m * 10 + (uint64_t)(c - '0');
+      if (frac >= 0) ++frac;
+    } else if (c == '.' && frac < 0) {
+      frac = 0;
+    } else {
+      return false;
+    }
+  }
+  if (i == (neg ? 1u : 0u) || (frac == 0 && nd == 0 && v.size() - (neg ? 1 : 0) == 1)) return false;
+  const int k = frac < 0 ? 0 : frac;
+  if (k > 22) return false;
+  const double d = (double)m / kPow10[k];
+  out = neg ? -d : d;
+  return true;
+}
+
 bool parse_float(std::string_view v, double& out) {  // Python float() of a CSV field
-  std::string s(v);
-  const char* b = s.c_str();
+  if (fast_decimal(v, out)) return true;
+  char buf[64];
+  std::string big;
+  const char* b;
+  if (v.size() < sizeof buf) {
+    if (!v.empty()) memcpy(buf, v.data(), v.size());
+    buf[v.size()] = '\0';
+    b = buf;
+  } else {
+    big.assign(v);
+    b = big.c_str();
+  }
   while (*b == ' ' || *b == '\t') ++b;
   if (!*b) return false;
   char* e = nullptr;
@@ -220,9 +267,23 @@ struct Sample {
 
 struct Builder {
   std::unordered_map<std::string, uint32_t> index;  // serialised key -> provisional series
+  std::vector<std::string> keys;                      // by series id (the fast path's keys)
   std::vector<anomod_metrics::Series> series;
   std::vector<Sample> samples;
   std::string key;
+
+  // Series id of a key already serialised as name \0 k1 \0 v1 ...; `make`
+  // builds the (name, labels) only when the series is new.
+  template <class Make>
+  uint32_t series_of_key(const std::string& k, Make&& make) {
+    auto it = index.find(k);
+    if (it != index.end()) return it->second;
+    const uint32_t id = (uint32_t)series.size();
+    index.emplace(k, id);
+    keys.push_back(k);
+    series.push_back(make());
+    return id;
+  }
 
   uint32_t series_of(const std::string& name, const Labels& labels) {
     key.assign(name);
@@ -253,22 +314,45 @@ struct Builder {
     for (uint32_t i = 0; i < order.size(); ++i) rank[order[i]] = i;
     out->series.reserve(series.size());
     for (uint32_t i : order) out->series.push_back(std::move(series[i]));
-    // distinct timestamps
-    out->ts.reserve(samples.size());
-    for (const Sample& s : samples) out->ts.push_back(s.t);
-    std::sort(out->ts.begin(), out->ts.end());
-    out->ts.erase(std::unique(out->ts.begin(), out->ts.end()), out->ts.end());
+    // distinct timestamps: a hash map to a provisional column, then sorted
+    std::unordered_map<double, uint32_t> col_of;
+    col_of.reserve(1024);
+    std::vector<uint32_t> col(samples.size());
+    double last = std::nan("");
+    uint32_t last_c = 0;
+    for (size_t i = 0; i < samples.size(); ++i) {
+      const double t = samples[i].t;
+      if (t == last) {  // (NaN never matches: timestamps are never NaN)
+        col[i] = last_c;
+        continue;
+      }
+      auto it = col_of.find(t);
+      if (it == col_of.end()) {
+        it = col_of.emplace(t, (uint32_t)out->ts.size()).first;
+        out->ts.push_back(t);
+      }
+      last = t;
+      last_c = col[i] = it->second;
+    }
+    std::vector<uint32_t> ord(out->ts.size());
+    for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return out->ts[a] < out->ts[b]; });
+    std::vector<uint32_t> crank(ord.size());
+    std::vector<double> sorted_ts(ord.size());
+    for (uint32_t i = 0; i < ord.size(); ++i) {
+      crank[ord[i]] = i;
+      sorted_ts[i] = out->ts[ord[i]];
+    }
+    out->ts.swap(sorted_ts);
     const size_t T = out->ts.size(), S = out->series.size();
     out->X.assign(T * S, std::nanf(""));
     // first occurrence per (series, t): later rows of the same cell skipped
     std::vector<uint8_t> seen(T * S, 0);
-    for (const Sample& s : samples) {  // samples are in row order
-      const size_t c = (size_t)(std::lower_bound(out->ts.begin(), out->ts.end(), s.t) -
-                                out->ts.begin());
-      const size_t cell = c * S + rank[s.series];
+    for (size_t i = 0; i < samples.size(); ++i) {  // samples are in row order
+      const size_t cell = (size_t)crank[col[i]] * S + rank[samples[i].series];
       if (seen[cell]) continue;
       seen[cell] = 1;
-      out->X[cell] = s.v;
+      out->X[cell] = samples[i].v;
     }
     return out;
   }
@@ -291,53 +375,129 @@ int find_col(const std::vector<std::string>& hdr, const char* name) {
   return at;
 }
 
-int decode_long(const char* data, uint64_t len, Builder& b) {
-  CsvReader rd(data, len);
-  if (!rd.next()) return ANOMOD_OK;  // empty file: no rows
-  std::vector<std::string> hdr(rd.fields.begin(), rd.fields.end());
-  const std::vector<int> keep = header_last(hdr);
-  const int c_name = find_col(hdr, "metric_name"), c_ts = find_col(hdr, "timestamp"),
-            c_val = find_col(hdr, "value");
-  std::vector<int> label_cols;
-  for (size_t i = 0; i < hdr.size(); ++i)
-    if (keep[i] && hdr[i] != "metric_name" && hdr[i] != "timestamp" && hdr[i] != "datetime" &&
-        hdr[i] != "value")
-      label_cols.push_back((int)i);
-  if (c_name < 0 || c_ts < 0) {
-    anomod::set_error(nullptr, "metric CSV: no metric_name / timestamp column");
-    return ANOMOD_EINVAL;
-  }
+struct LongHeader {
+  std::vector<std::string> hdr;
+  std::vector<int> label_cols;  // in label-name order
+  int c_name = -1, c_ts = -1, c_val = -1;
+};
+
+// The data rows of [p, end) (whole records) into b.
+int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builder& b,
+                     uint64_t row0) {
+  CsvReader rd(p, (size_t)(end - p));
   Labels labels;
-  uint64_t row = 0;
+  std::string key;
+  uint64_t row = row0;
   while (rd.next()) {
     if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;  // blank line (skipped)
     ++row;
     const auto field = [&](int c) -> std::string_view {
       return c >= 0 && (size_t)c < rd.fields.size() ? rd.fields[c] : std::string_view();
     };
-    labels.clear();
-    for (int c : label_cols) {
+    const std::string_view nm = field(H.c_name);
+    key.assign(nm.data(), nm.size());
+    for (int c : H.label_cols) {
       const std::string_view v = field(c);
-      if (!v.empty()) labels.emplace_back(hdr[c], std::string(v));
+      if (v.empty()) continue;
+      key.push_back('\0');
+      key.append(H.hdr[c]);
+      key.push_back('\0');
+      key.append(v.data(), v.size());
     }
-    std::sort(labels.begin(), labels.end());
     double t;
-    if (!parse_float(field(c_ts), t) || std::isnan(t)) {
+    if (!parse_float(field(H.c_ts), t) || std::isnan(t)) {
       anomod::set_error(nullptr, "metric CSV row %llu: bad timestamp '%.*s'",
-                        (unsigned long long)row, (int)field(c_ts).size(), field(c_ts).data());
+                        (unsigned long long)row, (int)field(H.c_ts).size(), field(H.c_ts).data());
       return ANOMOD_EINVAL;
     }
-    const std::string_view vs = field(c_val);
+    const std::string_view vs = field(H.c_val);
     double v = NAN;
     if (!vs.empty() && !parse_float(vs, v)) {
       anomod::set_error(nullptr, "metric CSV row %llu: bad value '%.*s'", (unsigned long long)row,
                         (int)vs.size(), vs.data());
       return ANOMOD_EINVAL;
     }
-    const uint32_t s = b.series_of(std::string(field(c_name)), labels);
+    const uint32_t s = b.series_of_key(key, [&] {
+      labels.clear();
+      for (int c : H.label_cols) {
+        const std::string_view lv = field(c);
+        if (!lv.empty()) labels.emplace_back(H.hdr[c], std::string(lv));
+      }
+      return anomod_metrics::Series{std::string(nm), labels};
+    });
     b.samples.push_back({t, (float)v, s, b.samples.size()});
   }
   return ANOMOD_OK;
+}
+
+int metric_threads() {
+  const char* e = getenv("ANOMOD_DECODE_THREADS");
+  if (e && atoi(e) > 0) return std::min(atoi(e), 64);
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::min<unsigned>(hc ? hc : 1u, 16u);
+}
+
+int decode_long(const char* data, uint64_t len, Builder& b) {
+  CsvReader rd(data, len);
+  if (!rd.next()) return ANOMOD_OK;  // empty file: no rows
+  LongHeader H;
+  H.hdr.assign(rd.fields.begin(), rd.fields.end());
+  const std::vector<int> keep = header_last(H.hdr);
+  H.c_name = find_col(H.hdr, "metric_name");
+  H.c_ts = find_col(H.hdr, "timestamp");
+  H.c_val = find_col(H.hdr, "value");
+  for (size_t i = 0; i < H.hdr.size(); ++i)
+    if (keep[i] && H.hdr[i] != "metric_name" && H.hdr[i] != "timestamp" &&
+        H.hdr[i] != "datetime" && H.hdr[i] != "value")
+      H.label_cols.push_back((int)i);
+  // label names are distinct: visiting the columns in name order yields each
+  // row's non-empty (name, value) pairs already sorted
+  std::sort(H.label_cols.begin(), H.label_cols.end(),
+            [&](int a, int c) { return H.hdr[a] < H.hdr[c]; });
+  if (H.c_name < 0 || H.c_ts < 0) {
+    anomod::set_error(nullptr, "metric CSV: no metric_name / timestamp column");
+    return ANOMOD_EINVAL;
+  }
+  const char* body = rd.p;
+  const char* end = data + len;
+  const int threads = metric_threads();
+  // Large files without any quote character (every record ends at a newline)
+  // parse in newline-aligned pieces on several threads; the pieces' series
+  // and samples are merged in file order, so the result is the one-thread one.
+  if (threads > 1 && end - body > (8 << 20) && !memchr(body, '"', (size_t)(end - body))) {
+    std::vector<const char*> cut{body};
+    for (int t = 1; t < threads; ++t) {
+      const char* c = body + (size_t)(end - body) * (size_t)t / (size_t)threads;
+      if (c <= cut.back()) continue;
+      const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(end - c)));
+      if (!nl) break;
+      if (nl + 1 > cut.back() && nl + 1 < end) cut.push_back(nl + 1);
+    }
+    cut.push_back(end);
+    const size_t np = cut.size() - 1;
+    std::vector<Builder> part(np);
+    std::vector<int> rc(np, ANOMOD_OK);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < np; ++k)
+      th.emplace_back([&, k] { rc[k] = decode_long_rows(H, cut[k], cut[k + 1], part[k], 0); });
+    for (auto& x : th) x.join();
+    for (size_t k = 0; k < np; ++k)
+      if (rc[k] != ANOMOD_OK) return rc[k];  // (row numbers in the message are per piece)
+    size_t total = 0;
+    for (const Builder& pb : part) total += pb.samples.size();
+    b.samples.reserve(total);
+    for (Builder& pb : part) {
+      std::vector<uint32_t> map(pb.series.size());
+      for (size_t s = 0; s < pb.series.size(); ++s) {
+        Builder* src = &pb;
+        map[s] = b.series_of_key(pb.keys[s], [&] { return std::move(src->series[s]); });
+      }
+      for (const Sample& sm : pb.samples)
+        b.samples.push_back({sm.t, sm.v, map[sm.series], b.samples.size()});
+    }
+    return ANOMOD_OK;
+  }
+  return decode_long_rows(H, body, end, b, 0);
 }
 
 int decode_prom(const char* data, uint64_t len, const std::string& stem, Builder& b) {
