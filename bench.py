@@ -33,8 +33,8 @@ import numpy as np  # noqa: E402
 import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
-LEGS = ("trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped", "tt_width", "pagerank", "ewma",
-        "tt_config2")
+LEGS = ("trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped", "tt_width",
+        "pagerank", "ewma", "tt_config2", "tt_config2_files")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
 
@@ -147,6 +147,74 @@ def tt_config2(ctx) -> dict:
             "spans_per_s": spans / el, "samples_per_s": samples / el,
             "top3_hit_rate": float(np.mean(hits)),
             "note": "end to end through features()/rank(): host-latency-bound at this size"}
+
+
+def _stage_tt_experiment(args) -> tuple[str, str, str | None]:
+    """Write one synthetic TrainTicket experiment in the dataset's layout:
+    <dir>/<exp>/<exp>_skywalking_traces_<ts>.json (the collector payload,
+    json.dump indent=2: trace_collector.py:564-581) and <exp>_metrics_<ts>.csv
+    (the long CSV of metric_collector.py:453-467)."""
+    root, i, fault = args
+    from anomod import writers
+
+    name = f"tt_{i:02d}_{fault or 'normal'}"
+    exp = anomod.load_experiment(anomod.SynthSpec("TT", seed=20251103 + i, fault_service=fault),
+                                 n_traces=650, series_per_service=130, name=name)
+    d = Path(root) / name
+    d.mkdir(parents=True, exist_ok=True)
+    tj = d / f"{name}_skywalking_traces_20251103_140200.json"
+    tj.write_text(json.dumps(writers.skywalking_payload(exp.spans, name), indent=2,
+                             ensure_ascii=False), encoding="utf-8")
+    mc = d / f"{name}_metrics_20251103_140200.csv"
+    writers.write_metric_long_csv_matrix(exp.metrics.X, exp.metrics.timestamps,
+                                         exp.metrics.series, mc)
+    return str(d), str(mc), fault
+
+
+def stage_tt_files(root: str) -> list:
+    """The 13 TT experiments of tt_config2 as files, written by a process
+    pool (forked before this process touches the GPU)."""
+    import multiprocessing as mp
+
+    work = [(root, i, f) for i, f in enumerate(TT_FAULTS)]
+    with mp.get_context("fork").Pool(min(len(work), max(1, host_cores()["usable"]))) as pool:
+        return pool.map(_stage_tt_experiment, work)
+
+
+def tt_config2_files(ctx, staged: list) -> dict:
+    """BASELINE config 2 from files: each experiment's trace payload and long
+    metric CSV go through load_experiment (native decoders) -> features() ->
+    rank(), decode included in the timing."""
+    def one(d, mc):
+        return anomod.load_experiment(d, metrics=mc)
+
+    one(*staged[0][:2])  # warm the page cache and the decoders
+    t0 = time.perf_counter()
+    t_dec = 0.0
+    base = None
+    hits = []
+    spans = samples = 0
+    for d, mc, fault in staged:
+        a = time.perf_counter()
+        e = one(d, mc)
+        t_dec += time.perf_counter() - a
+        f = anomod.features(e, ctx, baseline=base)
+        if base is None:
+            base = f
+        else:
+            hits.append(anomod.hit_at(anomod.rank(f, ctx=ctx), fault, 3))
+        spans += e.spans.n_spans
+        samples += e.metrics.S * e.metrics.T
+    el = time.perf_counter() - t0
+    sizes = [next(Path(d).glob("*.json")).stat().st_size for d, _, _ in staged]
+    csv_sizes = [Path(mc).stat().st_size for _, mc, _ in staged]
+    return {"experiments": len(staged), "spans": spans, "samples": samples, "seconds": el,
+            "ms_per_experiment": el / len(staged) * 1e3, "decode_seconds": t_dec,
+            "trace_json_mb_mean": float(np.mean(sizes)) / 1e6,
+            "metric_csv_mb_mean": float(np.mean(csv_sizes)) / 1e6,
+            "top3_hit_rate": float(np.mean(hits)),
+            "note": "files in the dataset layout (collector payload JSON indent=2 + long metric "
+                    "CSV) -> load_experiment (native decoders) -> features -> rank"}
 
 
 def edge_leg(ctx, spans, reps: int, what: str) -> dict:
@@ -265,6 +333,16 @@ def main() -> int:
         t = torch.tensor([v], dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
         return float(t.item())
+
+    staged = None
+    if "tt_config2_files" in legs and world == 1:
+        # staged before the GPU is touched (the pool forks)
+        import tempfile
+
+        stage_root = tempfile.mkdtemp(prefix="anomod_tt_files_")
+        t_stage = time.perf_counter()
+        staged = stage_tt_files(stage_root)
+        t_stage = time.perf_counter() - t_stage
 
     ctx = anomod.Context(local)
     if world > 1:
@@ -467,6 +545,12 @@ def main() -> int:
 
     if "tt_config2" in legs and world == 1:
         result["tt_config2"] = tt_config2(ctx)
+    if staged is not None:
+        result["tt_config2_files"] = tt_config2_files(ctx, staged)
+        result["tt_config2_files"]["staging_seconds"] = t_stage
+        import shutil
+
+        shutil.rmtree(stage_root, ignore_errors=True)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(spec, args.cpu_traces, args.cpu_seconds)
