@@ -88,7 +88,9 @@ constexpr int kOffSum = kOffHt + kHtBytes;               // u64 [kLdsEdges][kSum
 // probing, ds_cmpst inserts), the sum replicas indexed by slot — a trace set
 // touches far fewer edges than E.
 constexpr uint32_t kSlotEdges = 512;
-static_assert(kSlotEdges <= kLdsEdges, "slot sums reuse the direct sum replicas");
+// the slot form's sums reuse the direct form's replica area
+constexpr uint32_t kSlotSumReps = (kLdsEdges * kSumReps) / kSlotEdges;
+static_assert(kSlotSumReps >= 1 && (kSlotSumReps & (kSlotSumReps - 1)) == 0, "slot sum replicas");
 constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs | slots
 constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts (direct form)
 constexpr int kStatsBytes = (int)(kLdsEdges * 12 > kSlotEdges * 16 ? kLdsEdges * 12
@@ -270,7 +272,8 @@ __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uin
       mm = u32x2{0xFFFFFFFFu, 0u};  // unknown: the atomics below decide
     }
     if (s != 0xFFFFFFFFu) {
-      atomicAdd(&lsum[s * kSumReps + (__lane_id() & (kSumReps - 1u))], (unsigned long long)d);
+      atomicAdd(&lsum[s * kSlotSumReps + (__lane_id() & (kSlotSumReps - 1u))],
+                (unsigned long long)d);
       if (d < mm.x) atomicMin(&st4[4u * s + 1u], d);
       if (d > mm.y) atomicMax(&st4[4u * s + 2u], d);
       if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&st4[4u * s + 3u], 1u);
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     if constexpr (ST == kStSlot) {
       auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
       auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
-      for (uint32_t e = tid; e < kSlotEdges * kSumReps; e += kThreads) lsum[e] = 0ull;
+      for (uint32_t e = tid; e < kSlotEdges * kSlotSumReps; e += kThreads) lsum[e] = 0ull;
       for (uint32_t e = tid; e < kSlotEdges; e += kThreads) {
         st4[4u * e] = 0u;
         st4[4u * e + 1u] = 0xFFFFFFFFu;
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       if (key) {
         const uint32_t e = key - 1u;
         unsigned long long sum = 0;
-        for (uint32_t k = 0; k < kSumReps; ++k) sum += lsum[s * kSumReps + k];
+        for (uint32_t k = 0; k < kSlotSumReps; ++k) sum += lsum[s * kSlotSumReps + k];
         atomicAdd(&tab.sum[e], sum);
         if (st4[4u * s + 3u]) atomicAdd(&tab.err[e], (unsigned long long)st4[4u * s + 3u]);
         atomicMin(&tab.mn[e], st4[4u * s + 1u]);

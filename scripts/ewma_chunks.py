@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""Per-chunk EWMA kernel times at config-4 size: each chunk filled once and
+scored three times (state reset to the carried state is not needed for
+timing), to tell data-dependent chunk costs from run-to-run noise."""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "anomod-a-dataset-for-anomaly-detection-and-root-cause-analysis-in-microservice-systems_amd"), str(ROOT)]
+import anomod  # noqa: E402
+from anomod import _lib as L  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 131040
+chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+with anomod.Context(0) as ctx:
+    ser = anomod.DeviceSeries(ctx, steps, 100000)
+    out = []
+    for c in range(chunks):
+        ser.fill_synthetic(7, c * steps)
+        ms = []
+        for _ in range(3):
+            ser.ewma_z(2 / 61, 60, download=False)
+            ms.append(round(ctx.stage_ms(L.STAGE_EWMA), 3))
+        out.append(ms)
+        print(json.dumps({"chunk": c, "ms": ms}), flush=True)
+    ser.free()
