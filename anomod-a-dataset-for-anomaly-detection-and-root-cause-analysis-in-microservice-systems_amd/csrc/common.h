@@ -56,6 +56,10 @@ struct anomod_spans {
   uint64_t n_spans = 0;
   uint64_t n_traces = 0;
   uint32_t max_svc = 0;      // largest service index present (host-validated)
+  // longest trace in spans when known (upload, synthetic generation);
+  // UINT64_MAX = unknown.  Lets a call skip the long-trace pass when no
+  // trace outgrows a wave chunk.
+  uint64_t max_trace_len = ~0ull;
   bool grouped = true;       // false: spans in arrival order, trace_ptr = NULL
                              // (anomod_spans_upload_ungrouped; group first)
   uint64_t* trace_hash = nullptr;

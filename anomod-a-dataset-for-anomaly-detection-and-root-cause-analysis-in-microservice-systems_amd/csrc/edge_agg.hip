@@ -114,6 +114,9 @@ struct Table {
   unsigned long long* ctr;   // trace-segment counter of the dynamic tail (zeroed per launch)
   uint32_t kb;               // key bits of a histogram slot (count in the 32 - kb above)
   unsigned long long* keys;  // kHtKeys: [n_spans] edge << 32 | dur, by span position
+  unsigned long long* big;       // long traces: [0] listed, [1] ticket of edge_big_kernel
+  unsigned long long* big_list;  // long traces: trace indices
+  uint64_t t_base;           // trace index of this launch's first trace
 };
 
 struct Cols {
@@ -338,55 +341,6 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
   }
 }
 
-// A trace longer than kStage: wave-cooperative scan of the trace's span ids,
-// staged kStage at a time through the wave's LDS area (O(L^2 / 64) per trace;
-// rare — real traces are tens of spans).
-template <int HT, int ST>
-__device__ void big_trace(unsigned char* smem, unsigned char* wsm, int lane, uint64_t lo,
-                          uint64_t hi, const Cols& col, uint32_t S, const Table& tab) {
-  auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
-  auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
-  for (uint64_t i0 = lo; i0 < hi; i0 += kWave) {
-    const uint64_t i = i0 + lane;
-    const bool active = i < hi;
-    uint64_t pid = 0;
-    uint32_t d = 0, fl = 0, c = 0;
-    if (active) {
-      pid = col.parent[i];
-      d = col.dur[i];
-      const uint32_t sf = col.svcfl[i];
-      c = sf & 0xFFFFu;
-      fl = sf >> 16;
-    }
-    uint32_t p = (pid == 0) ? S : S + 1u;
-    bool done = !active || pid == 0;
-    for (uint64_t q0 = lo; q0 < hi; q0 += kStage) {
-      if (__all(done)) break;
-      const uint32_t m = (uint32_t)((hi - q0) < (uint64_t)kStage ? (hi - q0) : (uint64_t)kStage);
-      for (uint32_t q = lane; q < m; q += kWave) {
-        lsid[q] = col.span_id[q0 + q];
-        lsvc[q] = (uint16_t)col.svcfl[q0 + q];
-      }
-      wave_sync();
-      if (!done) {
-        for (uint32_t q = 0; q < m; ++q) {
-          if (lsid[q] == pid) {
-            p = lsvc[q];
-            done = true;
-            break;
-          }
-        }
-      }
-      wave_sync();
-    }
-    if constexpr (HT == kHtKeys) {
-      if (active) tab.keys[i] = ((unsigned long long)(p * S + c) << 32) | d;
-    } else {
-      if (active) record<HT, ST>(smem, p * S + c, d, fl, tab);
-    }
-  }
-}
-
 // Span columns of a chunk held in registers while the previous chunk is
 // processed (software pipeline, one chunk ahead).
 struct Regs {
@@ -395,7 +349,7 @@ struct Regs {
 };
 
 __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int lane, Regs& R) {
-  const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by big_trace()
+  const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by edge_big_kernel
   const auto rsid = rsrc(col.span_id + c.base, n * 8u);
   const auto rpid = rsrc(col.parent + c.base, n * 8u);
   const auto rsf = rsrc(col.svcfl + c.base, n * 4u);
@@ -485,6 +439,108 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   wave_sync();
 }
 
+// Traces longer than kStage do not fit a wave's staging area: the chunk walk
+// only lists them (big_list[j] = trace index, big[0] = count), and
+// edge_big_kernel resolves them afterwards, one workgroup per trace.  The
+// workgroup's LDS holds a hash table of kBigWin span ids at a time (id ->
+// first position in the window, atomicMin); the trace's spans are looked up
+// kBigPer per thread against the windows in trace order, so the first window
+// holding a span's parent reference gives the first match (the reference
+// rule).  O(L * ceil(L / kBigWin)) work, O(L) for L <= kBigWin; the records go
+// to HBM with global atomics (kHtHbm / kStHbm), or as keys in the exact mode.
+constexpr int kBigThreads = 1024;
+constexpr uint32_t kBigWin = 4096;    // ids per table window
+constexpr uint32_t kBigSlots = 8192;  // table slots (load <= 0.5)
+constexpr int kBigPer = 8;            // spans per thread per lookup block
+
+__device__ __forceinline__ uint32_t big_slot(uint64_t id) {
+  return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> (64 - 13)) & (kBigSlots - 1u);
+}
+
+template <int HT>
+__global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
+    const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+    const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+    const uint64_t* __restrict__ trace_ptr, uint32_t S, Table tab) {
+  __shared__ unsigned long long bkey[kBigSlots];  // 0 = empty (id 0 is never a parent ref)
+  __shared__ uint32_t bpos[kBigSlots];
+  __shared__ unsigned long long s_j;
+  const int tid = threadIdx.x;
+  const uint64_t nbig = tab.big[0];
+  if (nbig == 0) return;
+  for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
+    bkey[k] = 0ull;
+    bpos[k] = 0xFFFFFFFFu;
+  }
+  while (true) {
+    __syncthreads();  // table clear / s_j reuse
+    if (tid == 0) s_j = atomicAdd(&tab.big[1], 1ull);
+    __syncthreads();
+    const uint64_t j = s_j;
+    if (j >= nbig) break;
+    const uint64_t t = tab.big_list[j];
+    const uint64_t lo = trace_ptr[t], L = trace_ptr[t + 1] - lo;
+    for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kBigThreads * kBigPer) {
+      uint64_t pid[kBigPer], q[kBigPer];  // q: first position of the parent ref (~0: none yet)
+      bool need = false;
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
+        pid[r] = i < L ? parent[lo + i] : 0ull;
+        q[r] = ~0ull;
+        need |= pid[r] != 0ull;
+      }
+      for (uint64_t w0 = 0; w0 < L; w0 += kBigWin) {
+        if (!__syncthreads_or(need)) break;  // also orders the previous clear
+        for (uint32_t k = tid; k < kBigWin && w0 + k < L; k += kBigThreads) {
+          const uint64_t id = span_id[lo + w0 + k];
+          if (id == 0ull) continue;
+          for (uint32_t sl = big_slot(id);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+            const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id);
+            if (prev == 0ull || prev == id) {
+              atomicMin(&bpos[sl], k);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        need = false;
+#pragma unroll
+        for (int r = 0; r < kBigPer; ++r) {
+          if (pid[r] == 0ull || q[r] != ~0ull) continue;
+          for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+            const unsigned long long key = bkey[sl];
+            if (key == pid[r]) {
+              q[r] = w0 + bpos[sl];
+              break;
+            }
+            if (key == 0ull) break;
+          }
+          need |= q[r] == ~0ull;
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
+          bkey[k] = 0ull;
+          bpos[k] = 0xFFFFFFFFu;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
+        if (i >= L) continue;
+        const uint32_t sf = svcfl[lo + i];
+        const uint32_t p = pid[r] == 0ull ? S : q[r] == ~0ull ? S + 1u : (svcfl[lo + q[r]] & 0xFFFFu);
+        const uint32_t edge = p * S + (sf & 0xFFFFu);
+        if constexpr (HT == kHtKeys) {
+          tab.keys[lo + i] = ((unsigned long long)edge << 32) | dur[lo + i];
+        } else {
+          record<kHtHbm, kStHbm>(nullptr, edge, dur[lo + i], sf >> 16, tab);
+        }
+      }
+    }
+  }
+}
+
 template <int HT, int ST>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
@@ -551,10 +607,12 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi);
     Regs R;
     load_regs(col, cur, lane, R);
+    uint64_t t_cur = t_begin;
     uint64_t t_next = t_begin + (cur.k ? cur.k : 1u);
     load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
     while (true) {
       const bool has_next = t_next < t_end;
+      const uint64_t t_nxt = t_next;
       Chunk nxt{};
       Regs Rn;
       if (has_next) {
@@ -563,13 +621,14 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         t_next += nxt.k ? nxt.k : 1u;
         load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
       }
-      if (cur.k == 0) {
-        big_trace<HT, ST>(smem, wsm, lane, cur.base, cur.base + cur.n, col, S, tab);
+      if (cur.k == 0) {  // a trace longer than kStage: listed for edge_big_kernel
+        if (lane == 0) tab.big_list[atomicAdd(&tab.big[0], 1ull)] = tab.t_base + t_cur;
       } else {
         process_chunk<HT, ST>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
+      t_cur = t_nxt;
       R = Rn;
     }
   }
@@ -736,23 +795,46 @@ KernelFn pick_kernel(uint32_t E, const char** name) {
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
 // all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
-// ctr (u64, zeroed with them) | count | p50 | p99 | mn.  [off_err, bytes) is copied to the host in one D2H.
+// ctr (u64) | big counters (u64 x 2; both zeroed with them) | count | p50 |
+// p99 | mn | long-trace list.  [off_err, end_small) is copied to the host in
+// one D2H.
 struct Layout {
   uint64_t E;
-  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_count, off_p50, off_p99, off_mn, bytes;
-  explicit Layout(uint64_t e) : E(e) {
+  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_count, off_p50, off_p99,
+      off_mn, end_small, bytes;
+  Layout(uint64_t e, uint64_t big_cap) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
     off_sum = off_err + E * 8;
     off_mx = off_sum + E * 8;
     off_ctr = (off_mx + E * 4 + 7) & ~size_t(7);
-    off_count = off_ctr + 8;
+    off_big = off_ctr + 8;
+    off_count = off_big + 16;
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
-    bytes = off_mn + E * 4;
+    end_small = off_mn + E * 4;
+    bytes = ((end_small + 7) & ~size_t(7)) + big_cap * 8;
   }
+  size_t off_list() const { return (end_small + 7) & ~size_t(7); }
 };
+
+// Long traces (> kStage spans) a span set can hold: 0 when its longest trace
+// is known to fit a chunk.
+uint64_t big_capacity(const anomod_spans* s) {
+  if (s->max_trace_len <= (uint64_t)kStage) return 0;
+  const uint64_t by_spans = s->n_spans / (uint64_t)(kStage + 1);
+  return by_spans < s->n_traces ? by_spans : s->n_traces;
+}
+
+// The long-trace pass after the chunk walk (no-op when nothing was listed).
+template <int HT>
+hipError_t launch_big(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S, const Table& tab) {
+  hipLaunchKernelGGL(edge_big_kernel<HT>, dim3((unsigned)ctx->num_cus), dim3(kBigThreads), 0,
+                     ctx->stream, spans->span_id, spans->parent_span_id, spans->svc_flags,
+                     spans->dur_us, spans->trace_ptr, S, tab);
+  return hipGetLastError();
+}
 
 }  // namespace
 }  // namespace anomod
@@ -780,10 +862,11 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   ANOMOD_CHECK_LOCAL(ctx, local, spans->n_spans == 0 || spans->max_svc < S,
                      "span service index %u >= n_services %u", spans->max_svc, S);
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
-  const Layout L(E);
+  const uint64_t big_cap = big_capacity(spans);
+  const Layout L(E, big_cap);
   if (local == ANOMOD_OK) local = bind(ctx);
   if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
-  if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.bytes - L.off_err);
+  if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.end_small - L.off_err);
   if (int rc = comm_agree(ctx, local)) return rc;
   char* base = static_cast<char*>(ctx->d_table);
   Table tab;
@@ -793,13 +876,15 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
   tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
   tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
+  tab.big = reinterpret_cast<unsigned long long*>(base + L.off_big);
+  tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
   tab.kb = 1;
   while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
   auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
   auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
   auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
 
-  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx|ctr
+  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx|ctr|big
   ANOMOD_HIP(ctx, hipMemsetAsync(tab.mn, 0xFF, E * 4ull, ctx->stream));
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
@@ -819,11 +904,14 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     if (int rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts)) return rc;
     for (size_t k = 0; k + 1 < cuts.size(); ++k) {
       if (k > 0) ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
+      Table tk = tab;
+      tk.t_base = cuts[k];
       hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
                          spans->parent_span_id, spans->svc_flags, spans->dur_us,
-                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tab);
+                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
       ANOMOD_HIP(ctx, hipGetLastError());
     }
+    if (big_cap) ANOMOD_HIP(ctx, (launch_big<kHtHbm>(ctx, spans, S, tab)));
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
 
@@ -849,7 +937,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
 
   // The per-edge vectors come back in one D2H into pinned staging, then
   // fan out on the host; the histogram (when asked for) goes straight.
-  const size_t small = L.bytes - L.off_err;
+  const size_t small = L.end_small - L.off_err;
   ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, base + L.off_err, small, hipMemcpyDeviceToHost,
                                  ctx->stream));
   if (out->hist)
@@ -888,7 +976,9 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
   const uint64_t n = spans->n_spans;
   int kbits = 1;
   while ((uint64_t)E >> kbits) ++kbits;
-  // One workspace: keys | sorted keys | sort temp | q | out | count | ctr
+  // One workspace: keys | sorted keys | sort temp | q | out | count | ctr +
+  // long-trace counters | long-trace list
+  const uint64_t big_cap = big_capacity(spans);
   size_t sort_tmp = 0;
   if (n)
     ANOMOD_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(
@@ -898,7 +988,7 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
   const size_t b_keys = al(n * 8), b_tmp = al(sort_tmp), b_q = al(nq * 4), b_out = al(E * nq * 8ull),
                b_cnt = al(E * 8ull);
   char* w = nullptr;
-  if (hipMalloc(&w, 2 * b_keys + b_tmp + b_q + b_out + b_cnt + 256) != hipSuccess) {
+  if (hipMalloc(&w, 2 * b_keys + b_tmp + b_q + b_out + b_cnt + 256 + big_cap * 8) != hipSuccess) {
     set_error(ctx, "hipMalloc for the exact-quantile workspace (%llu spans) failed",
               (unsigned long long)n);
     return ANOMOD_ENOMEM;
@@ -918,6 +1008,8 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
     Table tab{};
     tab.keys = keys;
     tab.ctr = d_ctr;
+    tab.big = d_ctr + 1;
+    tab.big_list = d_ctr + 32;
     KernelFn fn = edge_agg_kernel<kHtKeys, kStHbm>;
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn),
@@ -925,14 +1017,18 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
     const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
     std::vector<uint64_t> cuts;
     if (e == hipSuccess) rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts);
+    if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 24, ctx->stream);  // ctr + big counters
     for (size_t k = 0; e == hipSuccess && rc == ANOMOD_OK && k + 1 < cuts.size(); ++k) {
-      e = hipMemsetAsync(d_ctr, 0, 8, ctx->stream);
+      if (k > 0) e = hipMemsetAsync(d_ctr, 0, 8, ctx->stream);
       if (e != hipSuccess) break;
+      Table tk = tab;
+      tk.t_base = cuts[k];
       hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
                          spans->parent_span_id, spans->svc_flags, spans->dur_us,
-                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tab);
+                         spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
       e = hipGetLastError();
     }
+    if (e == hipSuccess && rc == ANOMOD_OK && big_cap) e = launch_big<kHtKeys>(ctx, spans, S, tab);
     if (e == hipSuccess && rc == ANOMOD_OK)
       e = hipcub::DeviceRadixSort::SortKeys(tmp, sort_tmp, keys, sorted, n, 0, 32 + kbits,
                                              ctx->stream);

@@ -796,6 +796,7 @@ int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* in, uint64_t seed,
                            &s))
     return rc;
   s->max_svc = in->max_svc;
+  s->max_trace_len = in->max_trace_len;  // traces keep their spans either way
   s->grouped = keep;
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
   const SoaOut sout{s->trace_hash, s->span_id, s->parent_span_id, s->svc_flags, s->dur_us};

@@ -567,6 +567,9 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
     return rc;
   }
   s->max_svc = (uint32_t)h->services.size() - 1u;
+  s->max_trace_len = 0;
+  for (size_t k = 0; k + 1 < h->tmpl_off.size(); ++k)
+    s->max_trace_len = std::max<uint64_t>(s->max_trace_len, h->tmpl_off[k + 1] - h->tmpl_off[k]);
   *out = s;
   return ANOMOD_OK;
 }
@@ -581,9 +584,12 @@ int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_
                  "span arrays must be non-NULL");
   ANOMOD_REQUIRE(ctx, n_traces < (1ull << 36), "n_traces too large");
   // Host-side validation: kernels index by these values.
-  for (uint64_t t = 0; t < n_traces; ++t)
+  uint64_t max_len = 0;
+  for (uint64_t t = 0; t < n_traces; ++t) {
     ANOMOD_REQUIRE(ctx, trace_ptr[t] <= trace_ptr[t + 1],
                    "trace_ptr is not non-decreasing at trace %llu", (unsigned long long)t);
+    max_len = std::max<uint64_t>(max_len, trace_ptr[t + 1] - trace_ptr[t]);
+  }
   if (n_traces) {
     ANOMOD_REQUIRE(ctx, trace_ptr[n_traces] <= n_spans,
                    "trace_ptr[n_traces]=%llu exceeds n_spans=%llu",
@@ -595,6 +601,7 @@ int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_
   anomod_spans* s = nullptr;
   if (int rc = alloc_spans(ctx, n_spans, n_traces, soa->trace_hash != nullptr, &s)) return rc;
   s->max_svc = max_svc;
+  s->max_trace_len = max_len;
   hipError_t e = hipSuccess;
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (e == hipSuccess && bytes)

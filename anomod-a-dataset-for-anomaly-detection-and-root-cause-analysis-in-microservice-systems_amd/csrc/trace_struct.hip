@@ -76,9 +76,14 @@ struct TsOut {
   uint32_t* n_roots;
   unsigned long long* svc_mask;  // [n_traces * words]
   uint32_t words;                // ceil(S / 64)
-  int* scr_f;                    // big traces only: node (first span) of each span
-  int* scr_pf;                   // big traces only: first span of its own parent ref
   unsigned long long* ctr;       // trace-segment counter of the dynamic tail (zeroed per launch)
+  // Traces longer than kStage, listed by the chunk walk for ts_big_kernel:
+  // big[0] listed, big[1] their spans, big[2] ticket, big[3] error flag;
+  // big_list[2j] = trace index, big_list[2j + 1] = its offset in the scratch.
+  unsigned long long* big;
+  unsigned long long* big_list;
+  uint32_t* scr;                 // ts_big_kernel: 4 u32 per listed span (4 arrays of big[1])
+  uint64_t scr_n;                // big[1]
 };
 
 // One ordered pass over [a, b), kTsScan ids per step (ds_read2_b64 from the
@@ -298,106 +303,239 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
   wave_sync();
 }
 
-// A trace longer than kStage, resolved against HBM by the whole wave.
-__device__ void ts_big(int lane, uint64_t lo, uint64_t hi, uint64_t t,
-                       const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
-                       const uint32_t* __restrict__ svcfl, const TsOut& o) {
-  const uint32_t L = (uint32_t)(hi - lo);
-  auto first_last_g = [&](uint64_t x, int& f, int& l) {
-    f = l = -1;
-    for (uint32_t q = 0; q < L; ++q)
-      if (span_id[lo + q] == x) {
-        if (f < 0) f = (int)q;
-        l = (int)q;
+// Traces longer than kStage: one workgroup per trace (ts_big_kernel), after
+// the chunk walk.  The span-id questions are answered through an LDS hash
+// table of kBigWin ids at a time (id -> first / last position in the window):
+// every span probes each window in trace order, so the first window holding
+// an id gives its first occurrence and the last one its last occurrence —
+// O(L * ceil(L / kBigWin)) work.  Depth: parent pointer jumping over the
+// trace in global scratch (log L rounds) without duplicated ids, else the
+// longest-path relaxation of ts_chunk over the whole workgroup.
+constexpr int kBigThreads = 1024;
+constexpr uint32_t kBigWin = 4096;    // ids per table window
+constexpr uint32_t kBigSlots = 8192;  // table slots (load <= 0.5)
+constexpr int kBigPer = 4;            // spans per thread per lookup block
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t big_slot(uint64_t id) {
+  return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> (64 - 13)) & (kBigSlots - 1u);
+}
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kBigThreads) void ts_big_kernel(
+    const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+    const uint32_t* __restrict__ svcfl, const uint64_t* __restrict__ trace_ptr, TsOut o) {
+  __shared__ unsigned long long bkey[kBigSlots];  // 0 = empty; id 0 goes to zmin / zmax
+  __shared__ uint32_t bmin[kBigSlots], bmax[kBigSlots];
+  __shared__ uint32_t zmin, zmax, s_roots;
+  __shared__ unsigned long long s_j, s_mask;
+  const int tid = threadIdx.x;
+  const uint64_t nbig = o.big[0];
+  uint32_t* const s0 = o.scr;  // f, then jump target (even rounds)
+  uint32_t* const s1 = o.scr + o.scr_n;      // pf, then distance (even rounds)
+  uint32_t* const s2 = o.scr + 2 * o.scr_n;  // l, then jump target (odd rounds)
+  uint32_t* const s3 = o.scr + 3 * o.scr_n;  // node parent, then distance (odd rounds)
+  for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
+    bkey[k] = 0ull;
+    bmin[k] = kNone;
+    bmax[k] = 0u;
+  }
+  while (true) {
+    __syncthreads();
+    if (tid == 0) {
+      s_j = atomicAdd(&o.big[2], 1ull);
+      zmin = kNone;
+      zmax = 0u;
+      s_roots = 0u;
+      s_mask = 0ull;
+    }
+    __syncthreads();
+    const uint64_t j = s_j;
+    if (j >= nbig) break;
+    const uint64_t t = o.big_list[2 * j], off = o.big_list[2 * j + 1];
+    const uint64_t lo = trace_ptr[t];
+    const uint64_t L64 = trace_ptr[t + 1] - lo;
+    if (L64 >= (uint64_t)kDone) {  // positions are u32 with a flag bit
+      if (tid == 0) atomicOr(&o.big[3], 1ull);
+      continue;
+    }
+    const uint32_t L = (uint32_t)L64;
+    // ---- phase 1: f / l (own id), pf (own parent reference) per span
+    for (uint32_t b0 = 0; b0 < L; b0 += kBigThreads * kBigPer) {
+      uint64_t sid[kBigPer], pid[kBigPer];
+      uint32_t f[kBigPer], l[kBigPer], pf[kBigPer];
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        const uint32_t i = b0 + (uint32_t)r * kBigThreads + tid;
+        sid[r] = i < L ? span_id[lo + i] : 0ull;
+        pid[r] = i < L ? parent[lo + i] : 0ull;
+        f[r] = l[r] = pf[r] = kNone;
       }
-  };
-  auto first_g = [&](uint64_t x) -> int {
-    if (x == 0ull) return -1;
-    for (uint32_t q = 0; q < L; ++q)
-      if (span_id[lo + q] == x) return (int)q;
-    return -1;
-  };
-  uint32_t roots = 0;
-  unsigned long long mask = 0;
-  int* D = reinterpret_cast<int*>(o.depth + lo);  // node depths during relaxation
-  // pass 1: node parents, flags, child counts (atomics on n_children), the
-  // edge list (own node, own parent's node) and the root depths
-  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
-    const uint32_t i = i0 + lane;
-    if (i < L) {
-      int f, l;
-      first_last_g(span_id[lo + i], f, l);
-      const int pf = first_g(parent[lo + i]);
-      const int np = (l == (int)i) ? pf : first_g(parent[lo + l]);
-      if (pf >= 0) atomicAdd(&o.n_children[lo + pf], 1u);
-      o.parent_pos[lo + i] = np >= 0 ? (uint32_t)np : ANOMOD_NO_PARENT;
-      o.flags[lo + i] = (uint8_t)((np < 0 ? ANOMOD_SPAN_ROOT : 0u) |
-                                    (f == (int)i ? ANOMOD_SPAN_FIRST : 0u));
-      if (np < 0 && f == (int)i) ++roots;
-      D[i] = (np < 0 && f == (int)i) ? 0 : -1;
-      o.scr_f[lo + i] = f;
-      o.scr_pf[lo + i] = pf;
+      for (uint32_t w0 = 0; w0 < L; w0 += kBigWin) {
+        for (uint32_t k = tid; k < kBigWin && w0 + k < L; k += kBigThreads) {
+          const uint64_t id = span_id[lo + w0 + k];
+          if (id == 0ull) {
+            atomicMin(&zmin, k);
+            atomicMax(&zmax, k);
+            continue;
+          }
+          for (uint32_t sl = big_slot(id);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+            const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id);
+            if (prev == 0ull || prev == id) {
+              atomicMin(&bmin[sl], k);
+              atomicMax(&bmax[sl], k);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        auto probe = [&](uint64_t x, uint32_t& mn, uint32_t& mx) {
+          if (x == 0ull) {
+            mn = zmin;
+            mx = zmax;
+            return mn != kNone;
+          }
+          for (uint32_t sl = big_slot(x);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+            const unsigned long long key = bkey[sl];
+            if (key == x) {
+              mn = bmin[sl];
+              mx = bmax[sl];
+              return true;
+            }
+            if (key == 0ull) return false;
+          }
+        };
+#pragma unroll
+        for (int r = 0; r < kBigPer; ++r) {
+          const uint32_t i = b0 + (uint32_t)r * kBigThreads + tid;
+          if (i >= L) continue;
+          uint32_t mn, mx;
+          if (probe(sid[r], mn, mx)) {
+            if (f[r] == kNone) f[r] = w0 + mn;
+            l[r] = w0 + mx;
+          }
+          if (pid[r] != 0ull && pf[r] == kNone && probe(pid[r], mn, mx)) pf[r] = w0 + mn;
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
+          bkey[k] = 0ull;
+          bmin[k] = kNone;
+          bmax[k] = 0u;
+        }
+        if (tid == 0) {
+          zmin = kNone;
+          zmax = 0u;
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        const uint32_t i = b0 + (uint32_t)r * kBigThreads + tid;
+        if (i >= L) continue;
+        s0[off + i] = f[r];
+        s1[off + i] = pf[r];
+        s2[off + i] = l[r];
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: node parent (the LAST span's reference, resolved = that
+    // span's pf), child counts, flags, roots, services
+    bool dup = false;
+    uint32_t roots = 0;
+    unsigned long long mask = 0;
+    for (uint32_t i = tid; i < L; i += kBigThreads) {
+      const uint32_t f = s0[off + i], pf = s1[off + i], l = s2[off + i];
+      const uint32_t np = (l == i) ? pf : s1[off + l];
+      if (pf != kNone) atomicAdd(&o.n_children[lo + pf], 1u);
+      o.parent_pos[lo + i] = np != kNone ? np : ANOMOD_NO_PARENT;
+      o.flags[lo + i] = (uint8_t)((np == kNone ? ANOMOD_SPAN_ROOT : 0u) |
+                                  (f == i ? ANOMOD_SPAN_FIRST : 0u));
+      if (np == kNone && f == i) ++roots;
+      dup |= f != i;
+      s3[off + i] = np;
       const uint32_t sv = svcfl[lo + i] & 0xFFFFu;
       if (o.words == 1u) mask |= 1ull << sv;
-      else
-        atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
+      else atomicOr(&o.svc_mask[t * o.words + (sv >> 6)], 1ull << (sv & 63u));
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __builtin_amdgcn_wave_barrier();
-  // pass 2: longest-path relaxation of the edges pf -> f (the BFS keeps a
-  // node's deepest visit); a reached cycle keeps growing past L
-  for (uint32_t round = 0; round < 2u * L + 2u; ++round) {
-    bool changed = false;
-    for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
-      const uint32_t i = i0 + lane;
-      if (i < L) {
-        const int pf = o.scr_pf[lo + i];
-        if (pf >= 0) {
-          const int f = o.scr_f[lo + i];
-          const int dp = __hip_atomic_load(&D[pf], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (dp >= 0 &&
-              dp + 1 > __hip_atomic_load(&D[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    if (roots) atomicAdd(&s_roots, roots);
+    if (mask) atomicOr(&s_mask, mask);
+    if (!__syncthreads_or(dup)) {
+      // ---- phase 3: pointer jumping (every node is its own first span)
+      for (uint32_t i = tid; i < L; i += kBigThreads) {
+        const uint32_t np = s3[off + i];
+        s0[off + i] = np != kNone ? np : (i | kDone);
+        s1[off + i] = np != kNone ? 1u : 0u;
+      }
+      uint32_t rounds = 1;
+      while ((1ull << rounds) < (uint64_t)L) ++rounds;
+      uint32_t *na = s0, *da = s1, *nb = s2, *db = s3;
+      for (uint32_t round = 0; round <= rounds; ++round) {
+        bool live = false;
+        __syncthreads();
+        for (uint32_t i = tid; i < L; i += kBigThreads) {
+          const uint32_t nx = na[off + i], d = da[off + i];
+          if (nx & kDone) {
+            nb[off + i] = nx;
+            db[off + i] = d;
+          } else {
+            nb[off + i] = na[off + nx];
+            db[off + i] = d + da[off + nx];
+            live = true;
+          }
+        }
+        uint32_t* tn = na; na = nb; nb = tn;
+        uint32_t* td = da; da = db; db = td;
+        if (!__syncthreads_or(live)) break;
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < L; i += kBigThreads) {
+        const uint32_t nx = na[off + i];
+        o.depth[lo + i] = (nx & kDone) ? da[off + i] : 0u;
+      }
+    } else {
+      // ---- phase 3 (duplicated ids): longest path from the roots along the
+      // edges pf -> f over node depths (in the depth output, -1 = not
+      // reached); a depth outgrowing L marks a reached cycle -> 0
+      int* D = reinterpret_cast<int*>(o.depth + lo);
+      for (uint32_t i = tid; i < L; i += kBigThreads) {
+        const uint32_t f = s0[off + i];
+        D[i] = (f == i && s3[off + i] == kNone) ? 0 : -1;
+      }
+      for (uint64_t round = 0; round < 2ull * L + 2ull; ++round) {
+        __syncthreads();
+        bool changed = false;
+        for (uint32_t i = tid; i < L; i += kBigThreads) {
+          const uint32_t pf = s1[off + i];
+          if (pf == kNone) continue;
+          const uint32_t f = s0[off + i];
+          const int dp = (int)ld_agent(reinterpret_cast<uint32_t*>(D) + pf);
+          if (dp >= 0 && dp + 1 > (int)ld_agent(reinterpret_cast<uint32_t*>(D) + f)) {
             atomicMax(&D[f], dp + 1);
             changed = true;
           }
         }
+        if (!__syncthreads_or(changed)) break;
       }
+      __syncthreads();
+      for (uint32_t i = tid; i < L; i += kBigThreads) {
+        const int d = (int)ld_agent(reinterpret_cast<uint32_t*>(D) + s0[off + i]);
+        s2[off + i] = (d >= 0 && d < (int)L) ? (uint32_t)d : 0u;
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < L; i += kBigThreads) o.depth[lo + i] = s2[off + i];
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    __builtin_amdgcn_wave_barrier();
-    if (__ballot(changed) == 0ull) break;
-  }
-  // pass 3: each span's depth (its node's, staged in scr_pf: D is read
-  // until every lane is done) and a duplicate id's child count (its first
-  // span's)
-  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
-    const uint32_t i = i0 + lane;
-    if (i < L) {
-      const int f = o.scr_f[lo + i];
-      const int d = __hip_atomic_load(&D[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      o.scr_pf[lo + i] = (d >= 0 && d < (int)L) ? d : 0;
-      if (f != (int)i)
-        o.n_children[lo + i] = __hip_atomic_load(&o.n_children[lo + f], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+    // a duplicated id's child count is its node's (first span's)
+    for (uint32_t i = tid; i < L; i += kBigThreads) {
+      const uint32_t f = s0[off + i];
+      if (dup && f != i) o.n_children[lo + i] = ld_agent(&o.n_children[lo + f]);
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t i0 = 0; i0 < L; i0 += kWave) {
-    const uint32_t i = i0 + lane;
-    if (i < L) o.depth[lo + i] = (uint32_t)o.scr_pf[lo + i];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __builtin_amdgcn_wave_barrier();
-  // per-trace outputs
-  for (int off = 32; off > 0; off >>= 1) {
-    roots += (uint32_t)__shfl_xor((int)roots, off);
-    mask |= (unsigned long long)__shfl_xor((long long)mask, off);
-  }
-  if (lane == 0) {
-    o.n_roots[t] = roots;
-    if (o.words == 1u) o.svc_mask[t] = mask;
+    if (tid == 0) {
+      o.n_roots[t] = s_roots;
+      if (o.words == 1u) o.svc_mask[t] = s_mask;
+    }
   }
 }
 
@@ -416,7 +554,7 @@ __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4)))
   // span columns of chunk c+1 are in flight while chunk c is resolved.
   auto load_cols = [&](const Chunk& c, uint64_t (&sid)[kPer], uint64_t (&pid)[kPer],
                        uint32_t (&svc)[kPer]) {
-    const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by ts_big()
+    const uint32_t n = c.k ? c.n : 0u;  // a big trace is read by ts_big_kernel
     const auto rsid = rsrc(span_id + c.base, n * 8u);
     const auto rpid = rsrc(parent + c.base, n * 8u);
     const auto rsf = rsrc(svcfl + c.base, n * 4u);
@@ -449,8 +587,15 @@ __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4)))
       t_next += nxt.k ? nxt.k : 1u;
       load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
     }
-    if (cur.k == 0) ts_big(lane, cur.base, cur.base + cur.n, t_cur, span_id, parent, svcfl, o);
-    else ts_chunk(wsm, lane, cur, t_cur, sid, pid, svc, o);
+    if (cur.k == 0) {  // longer than kStage: listed for ts_big_kernel
+      if (lane == 0) {
+        const unsigned long long j = atomicAdd(&o.big[0], 1ull);
+        o.big_list[2 * j] = t_cur;
+        o.big_list[2 * j + 1] = atomicAdd(&o.big[1], (unsigned long long)cur.n);
+      }
+    } else {
+      ts_chunk(wsm, lane, cur, t_cur, sid, pid, svc, o);
+    }
     if (!has_next) break;
     cur = nxt;
     t_cur = t_nxt;
@@ -511,23 +656,30 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   const size_t off_depth = n * 4, off_cnt = 2 * n * 4, off_flags = 3 * n * 4;
   const size_t off_roots = (off_flags + n + 7) & ~(size_t)7;
   const size_t off_mask = (off_roots + nt * 4 + 7) & ~(size_t)7;
-  // + scratch for traces longer than a chunk: (own node, parent's node) per span
-  const size_t off_scr = (off_mask + nt * words * 8 + 15) & ~(size_t)15;
-  const size_t off_ctr = off_scr + n * 8 + 8;
-  const size_t bytes = off_ctr + 8;
+  // + the long-trace counters and list (traces > kStage spans: at most
+  // n / (kStage + 1) of them; none when the longest trace is known to fit)
+  const uint64_t big_cap = spans->max_trace_len <= (uint64_t)kStage
+                               ? 0
+                               : std::min<uint64_t>(nt, n / (uint64_t)(kStage + 1));
+  const size_t off_big = (off_mask + nt * words * 8 + 15) & ~(size_t)15;
+  const size_t off_ctr = off_big + 32;
+  const size_t off_list = off_ctr + 8;
+  const size_t bytes = off_list + big_cap * 16;
   char* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) {
     set_error(ctx, "hipMalloc(%zu) for trace-structure outputs failed", bytes);
     return ANOMOD_ENOMEM;
   }
+  uint32_t* scr = nullptr;
   auto fail = [&](hipError_t e, const char* what) {
     (void)hipFree(d);
+    if (scr) (void)hipFree(scr);
     set_error(ctx, "%s failed: %s", what, hipGetErrorString(e));
     return ANOMOD_EHIP;
   };
   hipError_t e = hipMemsetAsync(d + off_cnt, 0, n * 4, ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(d + off_mask, 0, nt * words * 8, ctx->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d + off_ctr, 0, 8, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d + off_big, 0, 40, ctx->stream);  // big counters + ctr
   if (e != hipSuccess) return fail(e, "hipMemsetAsync");
   TsOut o;
   o.parent_pos = reinterpret_cast<uint32_t*>(d);
@@ -537,9 +689,11 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   o.n_roots = reinterpret_cast<uint32_t*>(d + off_roots);
   o.svc_mask = reinterpret_cast<unsigned long long*>(d + off_mask);
   o.words = words;
-  o.scr_f = reinterpret_cast<int*>(d + off_scr);
-  o.scr_pf = reinterpret_cast<int*>(d + off_scr + n * 4);
   o.ctr = reinterpret_cast<unsigned long long*>(d + off_ctr);
+  o.big = reinterpret_cast<unsigned long long*>(d + off_big);
+  o.big_list = reinterpret_cast<unsigned long long*>(d + off_list);
+  o.scr = nullptr;
+  o.scr_n = 0;
   if (int rc = stage_begin(ctx, kStageTraceStruct)) {
     (void)hipFree(d);
     return rc;
@@ -556,8 +710,30 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
     e = hipGetLastError();
     if (e != hipSuccess) return fail(e, "trace_struct_kernel launch");
   }
+  if (big_cap) {
+    // the long traces listed by the walk -> scratch sized to their spans
+    unsigned long long cnt[2] = {0, 0};
+    e = hipMemcpyAsync(cnt, o.big, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return fail(e, "reading the long-trace count");
+    if (cnt[0]) {
+      if (hipMalloc(&scr, cnt[1] * 16) != hipSuccess) {
+        (void)hipFree(d);
+        set_error(ctx, "hipMalloc(%llu) for the long-trace scratch failed", cnt[1] * 16);
+        return ANOMOD_ENOMEM;
+      }
+      o.scr = scr;
+      o.scr_n = cnt[1];
+      hipLaunchKernelGGL(ts_big_kernel, dim3((unsigned)std::min<uint64_t>(cnt[0], ctx->num_cus)),
+                         dim3(kBigThreads), 0, ctx->stream, spans->span_id, spans->parent_span_id,
+                         spans->svc_flags, spans->trace_ptr, o);
+      e = hipGetLastError();
+      if (e != hipSuccess) return fail(e, "ts_big_kernel launch");
+    }
+  }
   if (int rc = stage_end(ctx, kStageTraceStruct)) {
     (void)hipFree(d);
+    if (scr) (void)hipFree(scr);
     return rc;
   }
   auto d2h = [&](void* dst, const void* src, size_t nbytes) -> hipError_t {
@@ -570,9 +746,13 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   if (e == hipSuccess) e = d2h(out->span_flags, o.flags, n);
   if (e == hipSuccess) e = d2h(out->n_roots, o.n_roots, nt * 4);
   if (e == hipSuccess) e = d2h(out->svc_mask, o.svc_mask, nt * words * 8);
+  unsigned long long too_long = 0;
+  if (e == hipSuccess && big_cap) e = d2h(&too_long, o.big + 3, 8);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return fail(e, "trace-structure download");
   (void)hipFree(d);
+  if (scr) (void)hipFree(scr);
+  ANOMOD_REQUIRE(ctx, !too_long, "a trace holds 2^31 spans or more");
   return ANOMOD_OK;
 }
 

@@ -293,3 +293,112 @@ def group_by_trace(trace_hash) -> tuple[np.ndarray, np.ndarray]:
     n = ks.shape[0]
     starts = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]]) if n else np.zeros(0, np.int64)
     return order, np.r_[starts, n].astype(np.uint64)
+
+
+# ---- long traces with unique span ids: vectorised restatement -------------
+# The C oracle resolves parents by an ordered scan, O(L^2) per trace — minutes
+# for a 10^5-span trace.  When every id is unique inside its trace, the first
+# match of a parent reference is its only match, so a sorted-id lookup gives
+# the same parents (jaeger_to_csv.py:34-38, trace_collector.py:424-443), and
+# the BFS depth of _build_span_records (:441-449) is the length of the parent
+# chain up to a root (0 when the chain never reaches one: a cycle).
+def hist_bins_np(d) -> np.ndarray:
+    """hist_bin over a u32 array."""
+    v = np.asarray(d, np.uint64)
+    bl = np.zeros(v.shape, np.uint64)
+    for k in range(32):
+        bl += (v >> np.uint64(k)) > 0
+    e = np.where(v < 64, np.uint64(0), bl - np.uint64(6))
+    return np.where(v < 64, v, (e << np.uint64(5)) + (v >> e)).astype(np.int64)
+
+
+def unique_id_parents(spans) -> np.ndarray:
+    """Trace-local parent position of every span (-1: parent reference 0 or
+    not in the trace), for span sets whose ids are unique inside each trace."""
+    ptr = np.asarray(spans.trace_ptr, np.int64)
+    n = int(ptr[-1]) if ptr.size else 0
+    lens = np.diff(ptr)
+    t_of = np.repeat(np.arange(lens.size), lens)
+    sid = np.asarray(spans.span_id, np.uint64)[:n]
+    pid = np.asarray(spans.parent_span_id, np.uint64)[:n]
+    order = np.lexsort((sid, t_of))  # by (trace, id)
+    key_t, key_id = t_of[order], sid[order]
+    assert not np.any((key_t[1:] == key_t[:-1]) & (key_id[1:] == key_id[:-1])), \
+        "ids repeat inside a trace: use the C oracle"
+    # per-span binary search of its parent reference inside its trace's id run
+    lo = np.searchsorted(key_t, t_of, "left")
+    hi = np.searchsorted(key_t, t_of, "right")
+    out = np.full(n, -1, np.int64)
+    idx = np.zeros(n, np.int64)
+    for t in range(lens.size):
+        a, b = int(ptr[t]), int(ptr[t + 1])
+        if a == b:
+            continue
+        r0, r1 = int(lo[a]), int(hi[a])
+        j = np.searchsorted(key_id[r0:r1], pid[a:b]) + r0
+        idx[a:b] = np.minimum(j, r1 - 1)
+    found = (pid != 0) & (key_id[idx] == pid) & (key_t[idx] == t_of)
+    out[found] = order[idx[found]] - ptr[t_of[found]]
+    return out
+
+
+def unique_id_edge_table(spans, S: int) -> dict:
+    """Edge table (as oracle_edge_aggregate) for unique-id span sets."""
+    ptr = np.asarray(spans.trace_ptr, np.int64)
+    n = int(ptr[-1]) if ptr.size else 0
+    par = unique_id_parents(spans)
+    svc = np.asarray(spans.svc, np.int64)[:n]
+    t_of = np.repeat(np.arange(ptr.size - 1), np.diff(ptr))
+    pid = np.asarray(spans.parent_span_id, np.uint64)[:n]
+    p = np.where(pid == 0, S, S + 1)
+    has = par >= 0
+    p[has] = svc[ptr[t_of[has]] + par[has]]
+    e = p * S + svc
+    E = (S + 2) * S
+    d = np.asarray(spans.dur_us, np.uint32)[:n]
+    err = (np.asarray(spans.flags, np.int64)[:n] & 1).astype(bool)
+    tab = {"count": np.bincount(e, minlength=E).astype(np.uint64),
+           "errors": np.bincount(e[err], minlength=E).astype(np.uint64),
+           "sum_us": np.zeros(E, np.uint64), "min_us": np.full(E, 0xFFFFFFFF, np.uint32),
+           "max_us": np.zeros(E, np.uint32)}
+    np.add.at(tab["sum_us"], e, d.astype(np.uint64))
+    np.minimum.at(tab["min_us"], e, d)
+    np.maximum.at(tab["max_us"], e, d)
+    tab["hist"] = np.bincount(e * 896 + hist_bins_np(d), minlength=E * 896).astype(
+        np.uint64).reshape(E, 896)
+    tab["edge"] = e
+    return tab
+
+
+def unique_id_trace_structure(spans, S: int) -> dict:
+    """oracle_trace_structure's outputs for unique-id span sets."""
+    ptr = np.asarray(spans.trace_ptr, np.int64)
+    nt = ptr.size - 1
+    n = int(ptr[-1]) if ptr.size else 0
+    par = unique_id_parents(spans)
+    t_of = np.repeat(np.arange(nt), np.diff(ptr))
+    gpar = np.where(par >= 0, par + ptr[t_of], -1)  # global parent index
+    svc = np.asarray(spans.svc, np.int64)[:n]
+    words = (S + 63) // 64
+    root = par < 0
+    # depth: pointer jumping up the parent chain (kDone = reached a root)
+    nxt = np.where(root, np.arange(n), gpar)
+    dst = np.where(root, 0, 1).astype(np.int64)
+    done = root.copy()
+    for _ in range(64):
+        if done.all():
+            break
+        live = ~done
+        dst[live] += dst[nxt[live]]
+        done_n = done.copy()
+        done_n[live] = done[nxt[live]]
+        nxt[live] = nxt[nxt[live]]
+        done = done_n
+    mask = np.zeros((nt, words), np.uint64)
+    np.bitwise_or.at(mask, (t_of, svc >> 6), np.left_shift(np.uint64(1), (svc & 63).astype(np.uint64)))
+    return {"parent_pos": np.where(root, 0xFFFFFFFF, par).astype(np.uint32),
+            "depth": np.where(done, dst, 0).astype(np.uint32),
+            "n_children": np.bincount(gpar[gpar >= 0], minlength=n).astype(np.uint32),
+            "span_flags": np.where(root, 3, 2).astype(np.uint8),
+            "n_roots": np.bincount(t_of[root], minlength=nt).astype(np.uint32),
+            "svc_mask": mask}
