@@ -34,6 +34,7 @@
 //  * per-edge error/sum/min/max live in LDS (E <= 512) and are flushed once;
 //  * all merges are integer adds / min / max: results are bit-exact and
 //    independent of geometry, scheduling and shard count.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -93,10 +94,19 @@ constexpr uint32_t kSlotSumReps = (kLdsEdges * kSumReps) / kSlotEdges;
 static_assert(kSlotSumReps >= 1 && (kSlotSumReps & (kSlotSumReps - 1)) == 0, "slot sum replicas");
 constexpr int kOffMm = kOffSum + (int)(kLdsEdges * kSumReps) * 8;  // u32 (min, max) pairs | slots
 constexpr int kOffErr = kOffMm + (int)kLdsEdges * 8;     // u32 error counts (direct form)
-constexpr int kStatsBytes = (int)(kLdsEdges * 12 > kSlotEdges * 16 ? kLdsEdges * 12
-                                                                  : kSlotEdges * 16);
-constexpr int kOffWave = kOffMm + kStatsBytes;
-enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2 };
+// Wide direct form (kLdsEdges < E <= kWideEdges, e.g. TrainTicket: E = 48 *
+// 46 = 2208): one 16-B entry {u64 sum, u32 min, u32 max} per edge + u32
+// error counts, indexed by edge (no slot hashing, no sum replicas).
+#ifndef ANOMOD_WIDE_EDGES
+#define ANOMOD_WIDE_EDGES 2304
+#endif
+constexpr uint32_t kWideEdges = ANOMOD_WIDE_EDGES;
+constexpr int kOffWideErr = kOffSum + (int)kWideEdges * 16;
+constexpr int kStatsEnd = std::max({kOffMm + (int)(kLdsEdges * 12),   // direct
+                                    kOffMm + (int)(kSlotEdges * 16),  // slot
+                                    kOffWideErr + (int)kWideEdges * 4});  // wide
+constexpr int kOffWave = (kStatsEnd + 15) & ~15;
+enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2, kStWide = 3 };
 constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
 constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2;  // u8 trace-start flags [kStage]
@@ -231,6 +241,8 @@ template <int ST>
 __device__ __forceinline__ StatPeek stat_peek(const unsigned char* smem, uint32_t edge) {
   if constexpr (ST == kStDirect && !(ANOMOD_ABL & 1)) {
     return {*reinterpret_cast<const u32x2*>(smem + kOffMm + 8u * edge), edge};
+  } else if constexpr (ST == kStWide && !(ANOMOD_ABL & 1)) {
+    return {*reinterpret_cast<const u32x2*>(smem + kOffSum + 16u * edge + 8u), edge};
   } else if constexpr (ST == kStSlot && !(ANOMOD_ABL & 1)) {
     // the home bucket of 4 entries (64 B, one round trip): simulated on the
     // TrainTicket mix, ~0 % of spans find their edge elsewhere (2.1 % with
@@ -264,6 +276,14 @@ __device__ __forceinline__ void stat_add(unsigned char* smem, uint32_t edge, uin
     if (d < pk.mm.x) atomicMin(&lmm[2u * edge], d);
     if (d > pk.mm.y) atomicMax(&lmm[2u * edge + 1u], d);
     if (fl & ANOMOD_FLAG_ERROR) atomicAdd(&lerr[edge], 1u);
+    return;
+  }
+  if constexpr (ST == kStWide) {
+    unsigned char* ent = smem + kOffSum + 16u * edge;
+    atomicAdd(reinterpret_cast<unsigned long long*>(ent), (unsigned long long)d);
+    if (d < pk.mm.x) atomicMin(reinterpret_cast<uint32_t*>(ent + 8), d);
+    if (d > pk.mm.y) atomicMax(reinterpret_cast<uint32_t*>(ent + 12), d);
+    if (fl & ANOMOD_FLAG_ERROR) atomicAdd(reinterpret_cast<uint32_t*>(smem + kOffWideErr) + edge, 1u);
     return;
   }
   if constexpr (ST == kStSlot) {
@@ -567,6 +587,17 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         lmm[2u * e + 1u] = 0u;
       }
     }
+    if constexpr (ST == kStWide) {
+      auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
+      auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
+      for (uint32_t e = tid; e < E; e += kThreads) {
+        ent[4u * e] = 0u;
+        ent[4u * e + 1u] = 0u;
+        ent[4u * e + 2u] = 0xFFFFFFFFu;
+        ent[4u * e + 3u] = 0u;
+        lerr[e] = 0u;
+      }
+    }
     if constexpr (ST == kStSlot) {
       auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
       auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
@@ -672,6 +703,19 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         if (st4[4u * s + 3u]) atomicAdd(&tab.err[e], (unsigned long long)st4[4u * s + 3u]);
         atomicMin(&tab.mn[e], st4[4u * s + 1u]);
         atomicMax(&tab.mx[e], st4[4u * s + 2u]);
+      }
+    }
+  }
+  if constexpr (ST == kStWide) {
+    auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      const uint32_t mn = ent[4u * e + 2u], mx = ent[4u * e + 3u];
+      if (mn != 0xFFFFFFFFu || mx != 0u) {
+        atomicAdd(&tab.sum[e], *reinterpret_cast<const unsigned long long*>(ent + 4u * e));
+        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
+        atomicMin(&tab.mn[e], mn);
+        atomicMax(&tab.mx[e], mx);
       }
     }
   }
@@ -784,6 +828,10 @@ KernelFn pick_kernel(uint32_t E, const char** name) {
   if (lds_hist && E <= kLdsEdges) {
     *name = "edge_agg_kernel<lds_hist,lds_stats>";
     return edge_agg_kernel<kHtPair, kStDirect>;
+  }
+  if (lds_hist && E <= kWideEdges) {
+    *name = "edge_agg_kernel<lds_compact_hist,wide_stats>";
+    return edge_agg_kernel<kHtCompact, kStWide>;
   }
   if (lds_hist) {
     *name = "edge_agg_kernel<lds_compact_hist,slot_stats>";

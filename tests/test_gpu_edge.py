@@ -67,8 +67,10 @@ def test_native_library_is_loaded(ctx):
 
 @pytest.mark.parametrize("S,n_traces,max_len", [
     (1, 100, 5), (3, 2000, 12), (12, 20000, 24), (20, 5000, 30),  # LDS-stat variants
-    (46, 5000, 60),   # TrainTicket width: 22-bit keys, HBM stats
-    (100, 2000, 40),  # beyond LDS keys: all-HBM path
+    (46, 5000, 60),   # TrainTicket width: compact 22-bit keys, wide per-edge stats
+    (47, 3000, 60),   # E = 2303: the widest table with wide stats
+    (48, 3000, 60),   # E = 2400: slot-hashed stats
+    (100, 2000, 40),  # compact keys, slot-hashed stats
 ])
 def test_random_sets_bit_exact(ctx, S, n_traces, max_len):
     rng = np.random.default_rng(S * 1000 + n_traces)
@@ -153,6 +155,17 @@ def test_device_generation_matches_host(ctx):
                   "dur_us"):
             np.testing.assert_array_equal(getattr(got, k), getattr(host, k), err_msg=k)
         assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(host))
+
+
+def test_tt_device_set_1e7_spans_bit_exact(ctx):
+    """TrainTicket width at ~1.0e7 spans (compact histogram + wide stats),
+    generated in HBM, against the C oracle on the host-generated twin."""
+    spec = anomod.SynthSpec("TT", seed=5, p_orphan_ppm=500, fault_service=7, fault_latency_mult=9)
+    n = 440_000
+    dev = ctx.generate(spec, n)
+    assert dev.n_spans >= 10_000_000
+    host = anomod.synth_generate_host(spec, n)
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(host))
 
 
 def test_jaeger_golden_edge_table(ctx, golden):
