@@ -49,7 +49,8 @@ struct anomod_graph {
   std::vector<unsigned long long> host_bacc;
   // persistent solve: [0] barrier arrivals, [1] timeout flag, [2] iterations done
   unsigned int* bar = nullptr;
-  int coop_blocks = -1;  // co-resident blocks of ppr_persistent_kernel (-1: not queried)
+  int coop_blocks = -1;  // co-resident workgroups of the persistent kernel (-1: not queried)
+  int coop_sub = 0;      // its 256-row blocks per workgroup
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
@@ -62,7 +63,10 @@ namespace {
 
 constexpr int kPprThreads = 256;
 constexpr int kRowsPerBlock = kPprThreads;  // one row per lane
-constexpr int kEdgeBatch = 8;              // in-edge loads issued together per lane
+#ifndef ANOMOD_PPR_EBATCH
+#define ANOMOD_PPR_EBATCH 8
+#endif
+constexpr int kEdgeBatch = ANOMOD_PPR_EBATCH;  // in-edge loads issued together per lane
 constexpr double kDScale = 4611686018427387904.0;  // 2^62: dangling mass <= 1
 constexpr double kEScale = 2305843009213693952.0;  // 2^61: L1 change <= 2
 constexpr int kAccSlots = 64;  // atomics spread over 64 words: no single-address queue
@@ -162,7 +166,9 @@ __device__ __forceinline__ void ppr_iter_body(
   if (r < N) {
     const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
     // In-degrees are short (uniform callees): one lane per row, kEdgeBatch
-    // (col, w) pairs loaded together, then the x gathers together.
+    // (col, w) pairs loaded together, then the x gathers together (lanes past
+    // the row's end gather x[0] with weight 0: adds +0.0, the same bits as
+    // skipping them).
     for (uint32_t k0 = b; k0 < e; k0 += kEdgeBatch) {
       uint32_t c[kEdgeBatch];
       float wv[kEdgeBatch];
@@ -172,9 +178,12 @@ __device__ __forceinline__ void ppr_iter_body(
         c[j] = ok ? in_col[k0 + j] : 0u;
         wv[j] = ok ? in_w[k0 + j] : 0.f;
       }
+      double xv[kEdgeBatch];
+#pragma unroll
+      for (int j = 0; j < kEdgeBatch; ++j) xv[j] = x_in[c[j]];
 #pragma unroll
       for (int j = 0; j < kEdgeBatch; ++j)
-        if (k0 + j < e) acc = ppr_edge(acc, x_in[c[j]], wv[j]);
+        if (k0 + j < e) acc = ppr_edge(acc, xv[j], wv[j]);
     }
   }
   // Dangling mass of x_in: wave 0 folds the fixed-point slots (exact).
@@ -280,26 +289,39 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
 // ppr_iter_kernel, so the vector is bit-identical to the per-launch path; in
 // tolerance mode every block reads the same L1 slots after the barrier and
 // stops at the same iteration.  bar[2] receives the iterations done.
-constexpr uint32_t kLdsEdges = 6144;  // 48 KB of (col, w) per block
+// A workgroup holds SUB consecutive 256-row blocks (SUB * 256 threads): the
+// rows, the edge order, the 256-row fixed-point partials and their slots are
+// the per-launch kernel's whatever SUB, only the number of workgroups meeting
+// at the grid barrier shrinks (391 -> 98 at N = 10^5 with SUB = 4).
+constexpr uint32_t kLdsEdgeBytes = 128 * 1024;  // (col, w) staging per workgroup
+#ifndef ANOMOD_PPR_GATHER
+#define ANOMOD_PPR_GATHER 4
+#endif
+constexpr int kPBatch = ANOMOD_PPR_GATHER;  // x gathers in flight per lane (persistent kernel)
 
-__global__ __launch_bounds__(kPprThreads) void ppr_persistent_kernel(
+template <int SUB>
+__global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
     const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
     const double* __restrict__ p, double alpha, double x0v, double* x0, double* x1,
     unsigned long long* acc, uint32_t iters, double ntol, unsigned int* bar) {
-  __shared__ uint32_t lcol[kLdsEdges];
-  __shared__ float lw[kLdsEdges];
-  __shared__ double red[kPprThreads / 64];
+  constexpr uint32_t kLdsE = SUB == 1 ? 6144u : kLdsEdgeBytes / 8u;  // SUB 1: 48 KB, 3 per CU
+  __shared__ uint32_t lcol[kLdsE];
+  __shared__ float lw[kLdsE];
+  __shared__ double red[2 * SUB * (kPprThreads / 64)];
   __shared__ double s_dsum;
   __shared__ int s_flag;
   __shared__ int s_stop;
   constexpr int S = kAccSlots;
-  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
-  const uint32_t r0 = blockIdx.x * kRowsPerBlock;
-  const uint32_t r1 = r0 + kRowsPerBlock < N ? r0 + kRowsPerBlock : N;
-  const uint32_t e0 = in_ptr[r0], e1 = in_ptr[r1];
-  const uint32_t nc = e1 - e0 < kLdsEdges ? e1 - e0 : kLdsEdges;
-  for (uint32_t i = threadIdx.x; i < nc; i += kPprThreads) {
+  const uint32_t sub = threadIdx.x / kPprThreads, lt = threadIdx.x % kPprThreads;
+  const uint32_t gb = blockIdx.x * SUB + sub;  // the 256-row block of this thread
+  const uint32_t r = gb * kRowsPerBlock + lt;
+  const uint32_t r0 = blockIdx.x * SUB * kRowsPerBlock;
+  const uint32_t r0e = r0 < N ? r0 : N;
+  const uint32_t r1 = r0 + SUB * kRowsPerBlock < N ? r0 + SUB * kRowsPerBlock : N;
+  const uint32_t e0 = in_ptr[r0e], e1 = in_ptr[r1];
+  const uint32_t nc = e1 - e0 < kLdsE ? e1 - e0 : kLdsE;
+  for (uint32_t i = threadIdx.x; i < nc; i += kPprThreads * SUB) {
     lcol[i] = in_col[e0 + i];
     lw[i] = in_w[e0 + i];
   }
@@ -314,6 +336,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_persistent_kernel(
   }
   __syncthreads();
   uint32_t done = iters;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t it = 0; it < iters; ++it) {
     const bool odd = it & 1u;
     const double* x_in = odd ? x1 : x0;
@@ -334,21 +357,26 @@ __global__ __launch_bounds__(kPprThreads) void ppr_persistent_kernel(
     }
     double sum = 0.0;
     if (r < N) {
-      for (uint32_t k0 = rb; k0 < re; k0 += kEdgeBatch) {
-        uint32_t c[kEdgeBatch];
-        float wv[kEdgeBatch];
+      // kPBatch gathers in flight per lane (in-degrees ~ Poisson(7) here: one
+      // round for nearly every row); lanes past the row's end gather x[0]
+      // with weight 0 (adds +0.0: the same bits as skipping them)
+      for (uint32_t k0 = rb; k0 < re; k0 += kPBatch) {
+        uint32_t c[kPBatch];
+        float wv[kPBatch];
 #pragma unroll
-        for (int j = 0; j < kEdgeBatch; ++j) {
+        for (int j = 0; j < kPBatch; ++j) {
           const uint32_t k = k0 + j, li = k - e0;
           const bool ok = k < re;
           c[j] = !ok ? 0u : li < nc ? lcol[li] : in_col[k];
           wv[j] = !ok ? 0.f : li < nc ? lw[li] : in_w[k];
         }
+        double xv[kPBatch];
 #pragma unroll
-        for (int j = 0; j < kEdgeBatch; ++j)
-          if (k0 + j < re)
-            sum = ppr_edge(sum, __hip_atomic_load(&x_in[c[j]], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT), wv[j]);
+        for (int j = 0; j < kPBatch; ++j)
+          xv[j] = __hip_atomic_load(&x_in[c[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < kPBatch; ++j)
+          if (k0 + j < re) sum = ppr_edge(sum, xv[j], wv[j]);
       }
     }
     if (threadIdx.x < 64) {
@@ -375,10 +403,25 @@ __global__ __launch_bounds__(kPprThreads) void ppr_persistent_kernel(
       eacc = fabs(y - xr);
       xr = y;
     }
-    const double ds = block_sum(dacc, red);
-    const double es = block_sum(eacc, red);
-    if (threadIdx.x == 0) {
-      const int slot = blockIdx.x & (kAccSlots - 1);
+    // per 256-row block: block_sum2's reduction tree (wave xor, then the
+    // block's 4 wave partials in order)
+    for (int off = 32; off > 0; off >>= 1) {
+      dacc += __shfl_xor(dacc, off);
+      eacc += __shfl_xor(eacc, off);
+    }
+    constexpr int nw = kPprThreads / 64;
+    if (lane == 0) {
+      red[2 * nw * sub + (wid % nw)] = dacc;
+      red[2 * nw * sub + nw + (wid % nw)] = eacc;
+    }
+    __syncthreads();
+    if (lt == 0) {
+      double ds = 0.0, es = 0.0;
+      for (int k = 0; k < nw; ++k) {
+        ds += red[2 * nw * sub + k];
+        es += red[2 * nw * sub + nw + k];
+      }
+      const int slot = gb & (kAccSlots - 1);
       atomicAdd(&acc[w * S + slot], __double2ull_rn(ds * kDScale));
       atomicAdd(&acc[(3 + w) * S + slot], __double2ull_rn(es * kEScale));
     }
@@ -470,6 +513,18 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
       d_zero[i] = 0ull;
       e_zero[i] = 0ull;
     }
+}
+
+#ifndef ANOMOD_PPR_SUB
+#define ANOMOD_PPR_SUB 1
+#endif
+constexpr int kPprSub = ANOMOD_PPR_SUB;  // 256-row blocks per persistent workgroup
+using PersistentFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*,
+                              const uint8_t*, const double*, double, double, double*, double*,
+                              unsigned long long*, uint32_t, double, unsigned int*);
+PersistentFn persistent_fn(int sub) {
+  return sub >= 4 ? ppr_persistent_kernel<4> : sub == 2 ? ppr_persistent_kernel<2>
+                                                        : ppr_persistent_kernel<1>;
 }
 
 void free_graph(anomod_graph* g) {
@@ -675,15 +730,18 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
                      dim3(kPprThreads), 0, ctx->stream, N, 1.0 / N, g->x[0], g->p, psum);
   ANOMOD_HIP(ctx, hipGetLastError());
   uint32_t done = 0;
-  // Tolerance mode: one cooperative launch for the whole solve when every
-  // block fits on the chip at once (N = 10^5: 391 blocks) — the stopping test
-  // runs on the device, 12.6 µs per iteration vs 34 µs with a host read-back
-  // per launch.  Fixed iterations: the replayed hipGraph of per-iteration
-  // launches (10.8 µs per iteration vs 11.1 µs persistent: at this size the
-  // grid barrier costs what a graph launch does).  ANOMOD_PPR_MODE=1 forces
-  // the per-launch path, 2 the persistent one (tests: same bits).
-  if (g->coop_blocks < 0) {
-    // Blocks resident at once.  The persistent solve is a PLAIN launch: the
+  // One persistent launch for the whole solve when every workgroup fits on
+  // the chip at once (N = 10^5: 391 blocks): the stopping test runs on the
+  // device; 8.7 us per iteration (fixed) / 9.4 (tolerance) against 9.8 for
+  // the replayed hipGraph of per-iteration launches and 30 us with a host
+  // read-back per launch (r02, scripts/time_pagerank.py).  Larger graphs take
+  // the graph (fixed iterations) or per-launch read-backs (tolerance).
+  // ANOMOD_PPR_MODE=1 forces the per-launch paths, 2 the persistent one
+  // (tests: same bits).
+  const char* sub_env = getenv("ANOMOD_PPR_SUB");
+  const int sub = sub_env ? atoi(sub_env) : kPprSub;
+  if (g->coop_blocks < 0 || g->coop_sub != sub) {
+    // Workgroups resident at once.  The persistent solve is a PLAIN launch: the
     // cooperative launch API only adds a launch-time check of this same
     // bound (MI355X_MICROARCH.md, coop-launch row), and a process that made
     // one segfaulted at exit under rocprofv3 --kernel-trace (r01,
@@ -693,21 +751,22 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     // bounded spin turns a block that never became resident into an error,
     // not a hang.
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ppr_persistent_kernel, kPprThreads,
-                                                     0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_fn(sub),
+                                                     kPprThreads * sub, 0) != hipSuccess)
       per_cu = 0;
     g->coop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
+    g->coop_sub = sub;
   }
   const char* mode_env = getenv("ANOMOD_PPR_MODE");
   const int mode = mode_env ? atoi(mode_env) : 0;
-  const bool persistent =
-      (int)g->grid <= g->coop_blocks && (mode == 2 || (mode == 0 && tol > 0.0));
+  const uint32_t pgrid = (g->grid + sub - 1) / sub;
+  const bool persistent = (int)pgrid <= g->coop_blocks && mode != 1;
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
   if (persistent) {
     ANOMOD_HIP(ctx, hipMemsetAsync(g->bar, 0, kBarWords * sizeof(unsigned int), ctx->stream));
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
-    hipLaunchKernelGGL(ppr_persistent_kernel, dim3(g->grid), dim3(kPprThreads), 0, ctx->stream,
+    hipLaunchKernelGGL(persistent_fn(sub), dim3(pgrid), dim3(kPprThreads * sub), 0, ctx->stream,
                        g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, x0v,
                        g->x[0], g->x[1], g->acc, iters, ntol, g->bar);
     ANOMOD_HIP(ctx, hipGetLastError());

@@ -164,12 +164,15 @@ def test_device_graph_replay(ctx):
     g.free()
 
 
-def test_pagerank_persistent_equals_per_launch(ctx, monkeypatch):
-    """The cooperative one-launch solve (grid barrier per iteration) and the
-    per-iteration launches give the same bits and stop at the same iteration."""
+@pytest.mark.parametrize("sub", ["1", "2", "4"])
+def test_pagerank_persistent_equals_per_launch(ctx, monkeypatch, sub):
+    """The one-launch solve (grid barrier per iteration; 1, 2 or 4 256-row
+    blocks per workgroup) and the per-iteration launches give the same bits
+    and stop at the same iteration."""
     g = anomod.DeviceGraph(ctx, synthetic=(100000, 7, 3))
     p = np.random.default_rng(2).random(g.N)
     out = {}
+    monkeypatch.setenv("ANOMOD_PPR_SUB", sub)
     for mode in ("2", "1"):  # persistent, per-launch
         monkeypatch.setenv("ANOMOD_PPR_MODE", mode)
         out[mode] = [g.pagerank(p, iters=it, tol=tol) for it, tol in
