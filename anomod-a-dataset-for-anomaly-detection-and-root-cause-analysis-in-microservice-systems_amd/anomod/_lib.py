@@ -208,7 +208,14 @@ _SIGS = {
     "anomod_comm_unique_id": (_i32, [_P(C.c_uint8)]),
     "anomod_ctx_attach_comm": (_i32, [_vp, _P(C.c_uint8), _i32, _i32]),
     "anomod_ctx_comm_info": (_i32, [_vp, _P(_i32), _P(_i32)]),
+    "anomod_ctx_attach_host_comm": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
 }
+
+# Host collective transport (include/anomod.h anomod_ctx_attach_host_comm).
+DTYPE_I32, DTYPE_U32, DTYPE_U64, DTYPE_F64 = 0, 1, 2, 3
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
+HostAllreduceFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_int)
+HostAllgatherFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64)
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

@@ -168,6 +168,44 @@ class Context:
         buf = (C.c_uint8 * L.UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
         self._check(self._lib.anomod_ctx_attach_comm(self.handle, buf, nranks, rank))
 
+    def comm_info(self) -> tuple[int, int]:
+        """(nranks, rank) of the attached transport ((1, 0) without one)."""
+        n, r = C.c_int(), C.c_int()
+        self._check(self._lib.anomod_ctx_comm_info(self.handle, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
+    def attach_host_comm(self, nranks: int, rank: int, allreduce, allgather):
+        """Host collective transport instead of RCCL: ``allreduce(buf, dtype,
+        op)`` reduces a numpy array in place over all ranks, ``allgather(buf,
+        block)`` fills every rank's ``block``-byte slice of a u8 array (this
+        rank's is set); libanomod stages every collective through pinned host
+        memory and calls them in the RCCL path's order."""
+        dtypes = {L.DTYPE_I32: np.int32, L.DTYPE_U32: np.uint32, L.DTYPE_U64: np.uint64,
+                  L.DTYPE_F64: np.float64}
+
+        def _ar(_user, buf, count, dtype, op):
+            try:
+                dt = np.dtype(dtypes[dtype])
+                raw = (C.c_uint8 * (count * dt.itemsize)).from_address(buf)
+                allreduce(np.frombuffer(raw, dtype=dt), dtype, op)
+                return 0
+            except Exception:  # noqa: BLE001 - reported to libanomod as a failed transport
+                return 1
+
+        def _ag(_user, buf, block):
+            try:
+                raw = (C.c_uint8 * (block * nranks)).from_address(buf)
+                allgather(np.frombuffer(raw, dtype=np.uint8), block)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        # the ctypes thunks must outlive every call libanomod makes through them
+        self._host_comm = (L.HostAllreduceFn(_ar), L.HostAllgatherFn(_ag))
+        self._check(self._lib.anomod_ctx_attach_host_comm(
+            self.handle, nranks, rank, C.cast(self._host_comm[0], C.c_void_p),
+            C.cast(self._host_comm[1], C.c_void_p), None))
+
     # -- spans
     def upload(self, spans: SpanSet) -> DeviceSpans:
         h = C.c_void_p()

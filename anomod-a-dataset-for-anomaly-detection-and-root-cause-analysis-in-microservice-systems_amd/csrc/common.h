@@ -33,8 +33,15 @@ struct anomod_ctx {
   hipEvent_t ev_end[anomod::kNumStages] = {};
   bool stage_recorded[anomod::kNumStages] = {};
   std::string err;
-  // RCCL communicator (one process per GPU)
+  // RCCL communicator (one process per GPU) ...
   ncclComm_t comm = nullptr;
+  // ... or a host transport (anomod_ctx_attach_host_comm: ranks sharing a
+  // device, or a host-side library such as gloo)
+  anomod_host_allreduce_fn host_allreduce = nullptr;
+  anomod_host_allgather_fn host_allgather = nullptr;
+  void* host_user = nullptr;
+  void* h_coll = nullptr;      // pinned staging of host-transport collectives
+  size_t coll_bytes = 0;
   int nranks = 1;
   int rank = 0;
   bool comm_aborted = false;   // set once the communicator was aborted
@@ -125,6 +132,19 @@ int stream_wait(anomod_ctx* ctx);
 // ANOMOD_OK only when every rank is OK — so either all ranks enter the data
 // collective or none does.  A no-op returning local_rc without a communicator.
 int comm_agree(anomod_ctx* ctx, int local_rc);
+// Collectives on the ctx stream over whichever transport is attached (RCCL,
+// or the host callbacks: staged through pinned memory, synchronous).
+// comm_attached: a live transport of any kind.  coll_begin / coll_end bracket
+// the calls RCCL should issue as one group.
+enum CollType { kCollI32 = ANOMOD_DTYPE_I32, kCollU32 = ANOMOD_DTYPE_U32,
+                kCollU64 = ANOMOD_DTYPE_U64, kCollF64 = ANOMOD_DTYPE_F64 };
+enum CollOp { kCollSum = ANOMOD_OP_SUM, kCollMin = ANOMOD_OP_MIN, kCollMax = ANOMOD_OP_MAX };
+bool comm_attached(const anomod_ctx* ctx);
+int coll_begin(anomod_ctx* ctx);
+int coll_end(anomod_ctx* ctx);
+int coll_allreduce(anomod_ctx* ctx, void* dbuf, size_t count, CollType t, CollOp op);
+// in place: this rank's block of count_per_rank elements sits at rank * count_per_rank
+int coll_allgather(anomod_ctx* ctx, void* dbuf, size_t count_per_rank, CollType t);
 // Trace cut points 0 = c_0 < ... < c_k = n_traces of a span set such that
 // every range [c_i, c_{i+1}) holds at most max_spans spans or is a single
 // trace (kernels with per-workgroup u32 counters launch once per range).

@@ -89,8 +89,95 @@ int stream_wait(anomod_ctx* ctx) {
   }
 }
 
+bool comm_attached(const anomod_ctx* ctx) {
+  return ctx->comm != nullptr || ctx->host_allreduce != nullptr;
+}
+
+int coll_begin(anomod_ctx* ctx) {
+  if (ctx->comm) ANOMOD_RCCL(ctx, ncclGroupStart());
+  return ANOMOD_OK;
+}
+
+int coll_end(anomod_ctx* ctx) {
+  if (ctx->comm) ANOMOD_RCCL(ctx, ncclGroupEnd());
+  return ANOMOD_OK;
+}
+
+namespace {
+size_t coll_size(CollType t) { return (t == kCollU64 || t == kCollF64) ? 8 : 4; }
+ncclDataType_t nccl_type(CollType t) {
+  switch (t) {
+    case kCollI32: return ncclInt32;
+    case kCollU32: return ncclUint32;
+    case kCollU64: return ncclUint64;
+    default: return ncclFloat64;
+  }
+}
+ncclRedOp_t nccl_op(CollOp op) { return op == kCollSum ? ncclSum : op == kCollMin ? ncclMin : ncclMax; }
+
+int ensure_coll_stage(anomod_ctx* ctx, size_t bytes) {
+  if (ctx->coll_bytes >= bytes) return ANOMOD_OK;
+  if (ctx->h_coll) ANOMOD_HIP(ctx, hipHostFree(ctx->h_coll));
+  ctx->h_coll = nullptr;
+  ctx->coll_bytes = 0;
+  ANOMOD_HIP(ctx, hipHostMalloc(&ctx->h_coll, bytes, hipHostMallocDefault));
+  ctx->coll_bytes = bytes;
+  return ANOMOD_OK;
+}
+
+// A host-transport call failed: the transport is dropped like an aborted
+// communicator (later calls fail fast instead of entering a collective
+// their peers may never join).
+int host_coll_failed(anomod_ctx* ctx, const char* what, int rc) {
+  set_error(ctx, "host collective %s failed on rank %d of %d (callback returned %d); "
+            "transport detached", what, ctx->rank, ctx->nranks, rc);
+  ctx->host_allreduce = nullptr;
+  ctx->host_allgather = nullptr;
+  ctx->comm_aborted = true;
+  return ANOMOD_ERCCL;
+}
+}  // namespace
+
+int coll_allreduce(anomod_ctx* ctx, void* dbuf, size_t count, CollType t, CollOp op) {
+  if (ctx->comm) {
+    ANOMOD_RCCL(ctx, ncclAllReduce(dbuf, dbuf, count, nccl_type(t), nccl_op(op), ctx->comm,
+                                   ctx->stream));
+    return ANOMOD_OK;
+  }
+  const size_t bytes = count * coll_size(t);
+  if (int rc = ensure_coll_stage(ctx, bytes)) return rc;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_coll, dbuf, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = ctx->host_allreduce(ctx->host_user, ctx->h_coll, count, (int)t, (int)op))
+    return host_coll_failed(ctx, "all-reduce", rc);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(dbuf, ctx->h_coll, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the staging is reused
+  return ANOMOD_OK;
+}
+
+int coll_allgather(anomod_ctx* ctx, void* dbuf, size_t count_per_rank, CollType t) {
+  const size_t blk = count_per_rank * coll_size(t);
+  char* d = static_cast<char*>(dbuf);
+  if (ctx->comm) {
+    ANOMOD_RCCL(ctx, ncclAllGather(d + (size_t)ctx->rank * blk, d, count_per_rank, nccl_type(t),
+                                   ctx->comm, ctx->stream));
+    return ANOMOD_OK;
+  }
+  const size_t bytes = blk * (size_t)ctx->nranks;
+  if (int rc = ensure_coll_stage(ctx, bytes)) return rc;
+  char* h = static_cast<char*>(ctx->h_coll);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(h + (size_t)ctx->rank * blk, d + (size_t)ctx->rank * blk, blk,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = ctx->host_allgather(ctx->host_user, h, blk))
+    return host_coll_failed(ctx, "all-gather", rc);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ANOMOD_OK;
+}
+
 int comm_agree(anomod_ctx* ctx, int local_rc) {
-  if (!ctx->comm) {
+  if (!comm_attached(ctx)) {
     if (ctx->comm_aborted && local_rc == ANOMOD_OK) {
       set_error(ctx, "the communicator of this context was aborted after an earlier failure");
       return ANOMOD_ERCCL;
@@ -102,8 +189,7 @@ int comm_agree(anomod_ctx* ctx, int local_rc) {
   ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->d_status, ctx->h_status, sizeof(int),
                                  hipMemcpyHostToDevice, ctx->stream));
   // statuses are <= 0: the minimum is an error whenever any rank has one
-  ANOMOD_RCCL(ctx, ncclAllReduce(ctx->d_status, ctx->d_status, 1, ncclInt32, ncclMin, ctx->comm,
-                                 ctx->stream));
+  if (int rc = coll_allreduce(ctx, ctx->d_status, 1, kCollI32, kCollMin)) return rc;
   ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_status, ctx->d_status, sizeof(int),
                                  hipMemcpyDeviceToHost, ctx->stream));
   if (int rc = stream_wait(ctx)) return rc;
@@ -261,6 +347,7 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->d_table) (void)hipFree(ctx->d_table);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_coll) (void)hipHostFree(ctx->h_coll);
   for (int s = 0; s < anomod::kNumStages; ++s) {
     if (ctx->ev_begin[s]) (void)hipEventDestroy(ctx->ev_begin[s]);
     if (ctx->ev_end[s]) (void)hipEventDestroy(ctx->ev_end[s]);
@@ -315,7 +402,7 @@ int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks
   ANOMOD_REQUIRE(nullptr, ctx && unique_id, "anomod_ctx_attach_comm: NULL argument");
   ANOMOD_REQUIRE(ctx, nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d of %d", rank,
                  nranks);
-  ANOMOD_REQUIRE(ctx, ctx->comm == nullptr && !ctx->comm_aborted,
+  ANOMOD_REQUIRE(ctx, !anomod::comm_attached(ctx) && !ctx->comm_aborted,
                  "ctx already has (or had) a communicator");
   if (int rc = anomod::bind(ctx)) return rc;
   if (!ctx->d_status) ANOMOD_HIP(ctx, hipMalloc(&ctx->d_status, sizeof(int)));
@@ -329,6 +416,28 @@ int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
   ANOMOD_RCCL(ctx, ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return ANOMOD_OK;
+}
+
+int anomod_ctx_attach_host_comm(anomod_ctx* ctx, int nranks, int rank,
+                                anomod_host_allreduce_fn allreduce,
+                                anomod_host_allgather_fn allgather, void* user) {
+  ANOMOD_REQUIRE(nullptr, ctx && allreduce && allgather,
+                 "anomod_ctx_attach_host_comm: NULL argument");
+  ANOMOD_REQUIRE(ctx, nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d of %d", rank,
+                 nranks);
+  ANOMOD_REQUIRE(ctx, !anomod::comm_attached(ctx) && !ctx->comm_aborted,
+                 "ctx already has (or had) a communicator");
+  if (int rc = anomod::bind(ctx)) return rc;
+  if (!ctx->d_status) ANOMOD_HIP(ctx, hipMalloc(&ctx->d_status, sizeof(int)));
+  if (!ctx->h_status)
+    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_status), sizeof(int),
+                                  hipHostMallocDefault));
+  ctx->host_allreduce = allreduce;
+  ctx->host_allgather = allgather;
+  ctx->host_user = user;
   ctx->nranks = nranks;
   ctx->rank = rank;
   return ANOMOD_OK;

@@ -965,15 +965,15 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
 
   // Any attached communicator merges, a 1-rank one included (an identity
   // reduce, so the RCCL call sequence is exercised on a single-GPU box too).
-  if (ctx->comm) {
+  if (comm_attached(ctx)) {
     if (int rc = stage_begin(ctx, kStageEdgeReduce)) return rc;
-    ANOMOD_RCCL(ctx, ncclGroupStart());
+    if (int rc = coll_begin(ctx)) return rc;
     // hist | err | sum are contiguous u64: one sum all-reduce.
-    ANOMOD_RCCL(ctx, ncclAllReduce(base, base, (size_t)E * kBins + 2ull * E, ncclUint64, ncclSum,
-                                   ctx->comm, ctx->stream));
-    ANOMOD_RCCL(ctx, ncclAllReduce(tab.mn, tab.mn, E, ncclUint32, ncclMin, ctx->comm, ctx->stream));
-    ANOMOD_RCCL(ctx, ncclAllReduce(tab.mx, tab.mx, E, ncclUint32, ncclMax, ctx->comm, ctx->stream));
-    ANOMOD_RCCL(ctx, ncclGroupEnd());
+    if (int rc = coll_allreduce(ctx, base, (size_t)E * kBins + 2ull * E, kCollU64, kCollSum))
+      return rc;
+    if (int rc = coll_allreduce(ctx, tab.mn, E, kCollU32, kCollMin)) return rc;
+    if (int rc = coll_allreduce(ctx, tab.mx, E, kCollU32, kCollMax)) return rc;
+    if (int rc = coll_end(ctx)) return rc;
     if (int rc = stage_end(ctx, kStageEdgeReduce)) return rc;
   }
 

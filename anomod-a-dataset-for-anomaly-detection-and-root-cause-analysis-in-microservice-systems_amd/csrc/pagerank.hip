@@ -931,7 +931,7 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
   ANOMOD_REQUIRE(ctx, alpha > 0.0 && alpha < 1.0, "alpha=%g outside (0, 1)", alpha);
   ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
   ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
-  const bool ranks = ctx->comm != nullptr || ctx->comm_aborted;
+  const bool ranks = comm_attached(ctx) || ctx->comm_aborted;
   ANOMOD_REQUIRE(ctx, !ranks || virtual_shards <= 1,
                  "virtual_shards=%u needs a context without a communicator", virtual_shards);
   const uint32_t G = ranks ? (uint32_t)ctx->nranks : (virtual_shards ? virtual_shards : 1u);
@@ -983,14 +983,11 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
       }
       ANOMOD_HIP(ctx, hipGetLastError());
       double* xb = g->x[b];
-      ANOMOD_RCCL(ctx, ncclGroupStart());
-      ANOMOD_RCCL(ctx, ncclAllReduce(A + w * S, A + w * S, S, ncclUint64, ncclSum, ctx->comm,
-                                     ctx->stream));
-      ANOMOD_RCCL(ctx, ncclAllReduce(A + (3 + w) * S, A + (3 + w) * S, S, ncclUint64, ncclSum,
-                                     ctx->comm, ctx->stream));
-      ANOMOD_RCCL(ctx, ncclAllGather(xb + (size_t)ctx->rank * sh.rows_per_shard, xb,
-                                     sh.rows_per_shard, ncclFloat64, ctx->comm, ctx->stream));
-      ANOMOD_RCCL(ctx, ncclGroupEnd());
+      if (int rc = coll_begin(ctx)) return rc;
+      if (int rc = coll_allreduce(ctx, A + w * S, S, kCollU64, kCollSum)) return rc;
+      if (int rc = coll_allreduce(ctx, A + (3 + w) * S, S, kCollU64, kCollSum)) return rc;
+      if (int rc = coll_allgather(ctx, xb, sh.rows_per_shard, kCollF64)) return rc;
+      if (int rc = coll_end(ctx)) return rc;
     } else {
       // Virtual shards on one device (the same row split, sequential
       // launches into shared accumulators): rehearses the sharding exactly.

@@ -438,6 +438,27 @@ int anomod_comm_unique_id(uint8_t* out /* ANOMOD_UNIQUE_ID_BYTES */);
 int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks, int rank);
 int anomod_ctx_comm_info(const anomod_ctx* ctx, int* nranks, int* rank);
 
+/* Host collective transport instead of RCCL (ranks that share one device —
+ * RCCL refuses two ranks on a GPU —, or any host-side library such as gloo):
+ * libanomod stages every collective through pinned host memory and calls
+ *   allreduce(user, buf, count, dtype, op): in place over all ranks
+ *   allgather(user, buf, bytes_per_rank): buf holds nranks blocks, this
+ *     rank's (at rank * bytes_per_rank) filled; afterwards all are
+ * returning 0 on success.  The same calls, in the same order, as the RCCL
+ * path (status agreement, edge-table merge, sharded PageRank exchange). */
+#define ANOMOD_DTYPE_I32 0
+#define ANOMOD_DTYPE_U32 1
+#define ANOMOD_DTYPE_U64 2
+#define ANOMOD_DTYPE_F64 3
+#define ANOMOD_OP_SUM 0
+#define ANOMOD_OP_MIN 1
+#define ANOMOD_OP_MAX 2
+typedef int (*anomod_host_allreduce_fn)(void* user, void* buf, uint64_t count, int dtype, int op);
+typedef int (*anomod_host_allgather_fn)(void* user, void* buf, uint64_t bytes_per_rank);
+int anomod_ctx_attach_host_comm(anomod_ctx* ctx, int nranks, int rank,
+                                anomod_host_allreduce_fn allreduce,
+                                anomod_host_allgather_fn allgather, void* user);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,121 @@
+"""GPU: libanomod's multi-rank path with two ranks on one device, through the
+host collective transport (anomod_ctx_attach_host_comm, driven by gloo via
+anomod.dist.attach_gloo) — RCCL refuses two ranks on a GPU, so this is how
+the 1-GPU box runs the collective sequence with nranks = 2:
+
+* edge table: traceId-hash shards, status agreement, u64 sum /
+  u32 min / u32 max merge -> every rank holds the oracle's unsharded table;
+* status agreement: one rank's invalid call fails BOTH ranks (no rank waits
+  in the merge), and the transport is dropped afterwards on neither;
+* row-sharded PageRank: per-iteration u64 all-reduces + x all-gather -> the
+  vector equals the unsharded solve bit for bit, in fixed and tolerance mode;
+* ungrouped spans: device grouping per shard, then the same merge.
+"""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+import anomod
+from oracle import native
+
+from conftest import PKG_DIR, ROOT
+from test_gpu_edge import assert_table_equal
+
+pytestmark = pytest.mark.gpu
+
+_WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path[:0] = [{pkg!r}, {root!r}]
+    import numpy as np
+    import torch.distributed as tdist
+    import anomod
+    from anomod import dist
+    tdist.init_process_group("gloo")
+    info = dist.rank_from_env()
+    out = {{}}
+    sp = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=9, p_orphan_ppm=3000), 30000)
+    part = dist.shard_spans(sp, info)
+    with anomod.Context(0) as c:
+        dist.attach_gloo(c, info)
+        assert c.comm_info() == (2, info.rank)
+        t = c.edge_aggregate(part)
+        for k in ("count", "errors", "sum_us", "min_us", "max_us", "hist", "p50_us", "p99_us"):
+            out[k] = getattr(t, k)
+        out["n_part"] = part.n_spans
+        # status agreement: rank 1 asks for too few services -> both ranks fail
+        bad = part if info.rank == 0 else anomod.SpanSet(part.services[:2], part.trace_ptr,
+            part.trace_hash, part.span_id, part.parent_span_id, part.svc, part.flags, part.dur_us)
+        try:
+            c.edge_aggregate(bad)
+            out["agree_err"] = ""
+        except anomod.AnomodError as e:
+            out["agree_err"] = str(e)
+        # the transport survives an agreed failure: a second merge works
+        t2 = c.edge_aggregate(part)
+        out["count2"] = t2.count
+        # ungrouped spans (arrival order interleaved) -> grouping on device, same merge
+        dev = c.upload(part)
+        ug = c.shuffle(dev, seed=3, window_traces=64)
+        t3 = c.edge_aggregate(ug)
+        out["count3"] = t3.count
+        out["hist3"] = t3.hist
+        ug.free()
+        dev.free()
+        # row-sharded PageRank over the two ranks vs this rank's unsharded solve
+        os.environ["ANOMOD_PPR_MODE"] = "1"
+        g = anomod.DeviceGraph(c, synthetic=(30000, 8, 6))
+        p = np.random.default_rng(1).random(g.N)
+        for iters, tol in ((37, 0.0), (1000, 1e-10)):
+            xs, ds = g.pagerank_sharded(p, iters=iters, tol=tol)
+            x, d = g.pagerank(p, iters=iters, tol=tol)
+            out[f"ppr_eq_{{iters}}"] = int(np.array_equal(xs, x) and ds == d)
+        g.free()
+    np.savez(os.path.join({out!r}, f"rank{{info.rank}}.npz"), **out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+""")
+
+
+def test_two_ranks_host_transport(tmp_path):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = tmp_path / "worker.py"
+    script.write_text(_WORKER.format(pkg=str(PKG_DIR), root=str(ROOT), out=str(tmp_path)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      start_new_session=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=100)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                if q.poll() is None:
+                    os.killpg(q.pid, 9)
+            pytest.fail("two-rank host-transport run timed out")
+    assert all(p.returncode == 0 for p in procs), "\n".join(outs)[-3000:]
+    sp = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=9, p_orphan_ppm=3000), 30000)
+    ref = native.edge_aggregate(sp, len(sp.services))
+    r0, r1 = (np.load(tmp_path / f"rank{r}.npz") for r in range(2))
+    assert int(r0["n_part"]) + int(r1["n_part"]) == sp.n_spans
+    assert 0 < int(r0["n_part"]) < sp.n_spans
+    for r in (r0, r1):
+        got = anomod.EdgeTable(services=sp.services, **{k: r[k] for k in (
+            "count", "errors", "sum_us", "min_us", "max_us", "hist", "p50_us", "p99_us")})
+        assert_table_equal(got, ref)
+        np.testing.assert_array_equal(r["count2"], ref["count"])
+        np.testing.assert_array_equal(r["count3"], ref["count"])
+        np.testing.assert_array_equal(r["hist3"], ref["hist"])
+        assert r["ppr_eq_37"] == 1 and r["ppr_eq_1000"] == 1
+    assert "n_services" in str(r1["agree_err"])     # the failing rank's own reason
+    assert str(r0["agree_err"]) != ""                 # its peer failed with it
