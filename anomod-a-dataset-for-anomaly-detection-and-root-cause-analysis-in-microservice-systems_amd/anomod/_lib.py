@@ -22,6 +22,7 @@ FLAG_ERROR = 0x1
 UNIQUE_ID_BYTES = 128
 TOPO_SN = 0
 TOPO_TT = 1
+TOPO_LONG = 2
 
 OK, EINVAL, EHIP, ERCCL, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
 _STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", ESTATE: "ESTATE"}

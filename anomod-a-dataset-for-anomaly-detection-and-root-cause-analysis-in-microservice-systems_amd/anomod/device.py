@@ -16,7 +16,8 @@ from .spans import EdgeTable, SpanSet, TraceStructure, edge_rows
 
 @dataclass
 class SynthSpec:
-    """Synthetic workload: topology 'SN' or 'TT'."""
+    """Synthetic workload: topology 'SN' or 'TT' (or 'LONG':
+    SN services in traces of 16..4000 spans, the length / depth stress case)."""
 
     topology: str = "SN"
     seed: int = 20251103
@@ -28,7 +29,7 @@ class SynthSpec:
 
     @property
     def topo_id(self) -> int:
-        return {"SN": L.TOPO_SN, "TT": L.TOPO_TT}[self.topology.upper()]
+        return {"SN": L.TOPO_SN, "TT": L.TOPO_TT, "LONG": L.TOPO_LONG}[self.topology.upper()]
 
     def services(self) -> list[str]:
         return synth_services(self.topology)
@@ -44,7 +45,7 @@ class SynthSpec:
 
 def synth_services(topology: str) -> list[str]:
     lib = L.lib()
-    tid = {"SN": L.TOPO_SN, "TT": L.TOPO_TT}[topology.upper()]
+    tid = {"SN": L.TOPO_SN, "TT": L.TOPO_TT, "LONG": L.TOPO_LONG}[topology.upper()]
     n = C.c_uint32()
     L.check(lib.anomod_synth_n_services(tid, C.byref(n)))
     return [lib.anomod_synth_service_name(tid, i).decode() for i in range(n.value)]

@@ -459,35 +459,151 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   wave_sync();
 }
 
-// Traces longer than kStage do not fit a wave's staging area: the chunk walk
-// only lists them (big_list[j] = trace index, big[0] = count), and
-// edge_big_kernel resolves them afterwards, one workgroup per trace.  The
-// workgroup's LDS holds a hash table of kBigWin span ids at a time (id ->
-// first position in the window, atomicMin); the trace's spans are looked up
-// kBigPer per thread against the windows in trace order, so the first window
-// holding a span's parent reference gives the first match (the reference
-// rule).  O(L * ceil(L / kBigWin)) work, O(L) for L <= kBigWin; the records go
-// to HBM with global atomics (kHtHbm / kStHbm), or as keys in the exact mode.
-constexpr int kBigThreads = 1024;
-constexpr uint32_t kBigWin = 4096;    // ids per table window
-constexpr uint32_t kBigSlots = 8192;  // table slots (load <= 0.5)
-constexpr int kBigPer = 8;            // spans per thread per lookup block
-
-__device__ __forceinline__ uint32_t big_slot(uint64_t id) {
-  return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> (64 - 13)) & (kBigSlots - 1u);
+// The workgroup's private LDS tables (histogram + per-edge stats), shared by
+// the chunk walk and the long-trace pass: zeroed at the start, merged into
+// the device table with integer atomics (order-free) at the end.
+template <int HT, int ST>
+__device__ __forceinline__ void tables_init(unsigned char* smem, uint32_t E, int tid) {
+  if constexpr (HT == kHtPair || HT == kHtCompact) {
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);  // both forms: 64 KiB of zeros
+    for (uint32_t s = tid; s < (uint32_t)kHtBytes / 4u; s += kThreads) hk[s] = 0u;
+  }
+  if constexpr (ST == kStDirect) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
+    for (uint32_t e = tid; e < E * kSumReps; e += kThreads) lsum[e] = 0ull;
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      lerr[e] = 0u;
+      lmm[2u * e] = 0xFFFFFFFFu;
+      lmm[2u * e + 1u] = 0u;
+    }
+  }
+  if constexpr (ST == kStWide) {
+    auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      ent[4u * e] = 0u;
+      ent[4u * e + 1u] = 0u;
+      ent[4u * e + 2u] = 0xFFFFFFFFu;
+      ent[4u * e + 3u] = 0u;
+      lerr[e] = 0u;
+    }
+  }
+  if constexpr (ST == kStSlot) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    for (uint32_t e = tid; e < kSlotEdges * kSlotSumReps; e += kThreads) lsum[e] = 0ull;
+    for (uint32_t e = tid; e < kSlotEdges; e += kThreads) {
+      st4[4u * e] = 0u;
+      st4[4u * e + 1u] = 0xFFFFFFFFu;
+      st4[4u * e + 2u] = 0u;
+      st4[4u * e + 3u] = 0u;
+    }
+  }
 }
 
-template <int HT>
+template <int HT, int ST>
+__device__ __forceinline__ void tables_flush(unsigned char* smem, uint32_t E, const Table& tab,
+                                             int tid) {
+  if constexpr (HT == kHtPair) {
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
+    for (uint32_t s = tid; s < kPairSlots; s += kThreads) {
+      const uint32_t cnt = hc[s];
+      if (cnt) atomicAdd(&tab.hist[hk[s] - 1u], (unsigned long long)cnt);
+    }
+  }
+  if constexpr (HT == kHtCompact) {
+    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
+    const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
+    for (uint32_t s = tid; s < kCmpSlots; s += kThreads) {
+      const uint32_t w = hk[s];
+      if (w >> tab.kb) atomicAdd(&tab.hist[(w & kmask) - 1u], (unsigned long long)(w >> tab.kb));
+    }
+  }
+  if constexpr (ST == kStSlot) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    for (uint32_t s = tid; s < kSlotEdges; s += kThreads) {
+      const uint32_t key = st4[4u * s];
+      if (key) {
+        const uint32_t e = key - 1u;
+        unsigned long long sum = 0;
+        for (uint32_t k = 0; k < kSlotSumReps; ++k) sum += lsum[s * kSlotSumReps + k];
+        atomicAdd(&tab.sum[e], sum);
+        if (st4[4u * s + 3u]) atomicAdd(&tab.err[e], (unsigned long long)st4[4u * s + 3u]);
+        atomicMin(&tab.mn[e], st4[4u * s + 1u]);
+        atomicMax(&tab.mx[e], st4[4u * s + 2u]);
+      }
+    }
+  }
+  if constexpr (ST == kStWide) {
+    auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      const uint32_t mn = ent[4u * e + 2u], mx = ent[4u * e + 3u];
+      if (mn != 0xFFFFFFFFu || mx != 0u) {
+        atomicAdd(&tab.sum[e], *reinterpret_cast<const unsigned long long*>(ent + 4u * e));
+        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
+        atomicMin(&tab.mn[e], mn);
+        atomicMax(&tab.mx[e], mx);
+      }
+    }
+  }
+  if constexpr (ST == kStDirect) {
+    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
+    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
+    auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
+    for (uint32_t e = tid; e < E; e += kThreads) {
+      if (lmm[2u * e] != 0xFFFFFFFFu || lmm[2u * e + 1u] != 0u) {
+        unsigned long long sum = 0;
+        for (uint32_t k = 0; k < kSumReps; ++k) sum += lsum[e * kSumReps + k];
+        atomicAdd(&tab.sum[e], sum);
+        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
+        atomicMin(&tab.mn[e], lmm[2u * e]);
+        atomicMax(&tab.mx[e], lmm[2u * e + 1u]);
+      }
+    }
+  }
+}
+
+// Traces longer than kStage do not fit a wave's staging area: the chunk walk
+// only lists them (big_list[j] = trace index, big[0] = count), and
+// edge_big_kernel resolves them afterwards, one workgroup per trace.  Its LDS
+// holds the same private histogram / per-edge stats tables as the chunk walk
+// (flushed once at the end) and, in the wave-staging area's place, a hash
+// table of kBigWin span ids at a time (id -> first position in the window,
+// atomicMin); the trace's spans are looked up kBigPer per thread against the
+// windows in trace order, so the first window holding a span's parent
+// reference gives the first match (the reference rule).
+// O(L * ceil(L / kBigWin)) work, O(L) for L <= kBigWin.
+constexpr int kBigThreads = kThreads;  // the tables' init / flush loops assume it
+constexpr uint32_t kBigWin = 2048;    // ids per table window
+constexpr uint32_t kBigSlots = 4096;  // table slots (load <= 0.5)
+constexpr int kBigPer = 8;            // spans per thread per lookup block
+constexpr int kOffBigKey = kOffWave;                          // u64 [kBigSlots], 0 = empty
+constexpr int kOffBigPos = kOffBigKey + (int)kBigSlots * 8;   // u32 [kBigSlots]
+constexpr int kBigLdsBytes = kOffBigPos + (int)kBigSlots * 4;
+static_assert(kBigLdsBytes <= 160 * 1024, "long-trace pass LDS budget");
+
+__device__ __forceinline__ uint32_t big_slot(uint64_t id) {
+  return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> (64 - 12)) & (kBigSlots - 1u);
+}
+
+template <int HT, int ST>
 __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
-    const uint64_t* __restrict__ trace_ptr, uint32_t S, Table tab) {
-  __shared__ unsigned long long bkey[kBigSlots];  // 0 = empty (id 0 is never a parent ref)
-  __shared__ uint32_t bpos[kBigSlots];
+    const uint64_t* __restrict__ trace_ptr, uint32_t S, uint32_t E, Table tab) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kBigLdsBytes];
   __shared__ unsigned long long s_j;
+  auto* bkey = reinterpret_cast<unsigned long long*>(smem + kOffBigKey);  // 0 = empty (id 0 is never a parent ref)
+  auto* bpos = reinterpret_cast<uint32_t*>(smem + kOffBigPos);
   const int tid = threadIdx.x;
   const uint64_t nbig = tab.big[0];
   if (nbig == 0) return;
+  tables_init<HT, ST>(smem, E, tid);
   for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
     bkey[k] = 0ull;
     bpos[k] = 0xFFFFFFFFu;
@@ -554,11 +670,13 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
         if constexpr (HT == kHtKeys) {
           tab.keys[lo + i] = ((unsigned long long)edge << 32) | dur[lo + i];
         } else {
-          record<kHtHbm, kStHbm>(nullptr, edge, dur[lo + i], sf >> 16, tab);
+          record<HT, ST>(smem, edge, dur[lo + i], sf >> 16, tab);
         }
       }
     }
   }
+  __syncthreads();
+  tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
 template <int HT, int ST>
@@ -572,44 +690,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   const int wid = tid / kWave;
   const Cols col{span_id, parent, svcfl, dur};
 
-  // ---- init LDS tables
-  {
-    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);  // both forms: 64 KiB of zeros
-    for (uint32_t s = tid; s < (uint32_t)kHtBytes / 4u; s += kThreads) hk[s] = 0u;
-    if constexpr (ST == kStDirect) {
-      auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
-      auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
-      auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
-      for (uint32_t e = tid; e < E * kSumReps; e += kThreads) lsum[e] = 0ull;
-      for (uint32_t e = tid; e < E; e += kThreads) {
-        lerr[e] = 0u;
-        lmm[2u * e] = 0xFFFFFFFFu;
-        lmm[2u * e + 1u] = 0u;
-      }
-    }
-    if constexpr (ST == kStWide) {
-      auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
-      auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
-      for (uint32_t e = tid; e < E; e += kThreads) {
-        ent[4u * e] = 0u;
-        ent[4u * e + 1u] = 0u;
-        ent[4u * e + 2u] = 0xFFFFFFFFu;
-        ent[4u * e + 3u] = 0u;
-        lerr[e] = 0u;
-      }
-    }
-    if constexpr (ST == kStSlot) {
-      auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
-      auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
-      for (uint32_t e = tid; e < kSlotEdges * kSlotSumReps; e += kThreads) lsum[e] = 0ull;
-      for (uint32_t e = tid; e < kSlotEdges; e += kThreads) {
-        st4[4u * e] = 0u;
-        st4[4u * e + 1u] = 0xFFFFFFFFu;
-        st4[4u * e + 2u] = 0u;
-        st4[4u * e + 3u] = 0u;
-      }
-    }
-  }
+  tables_init<HT, ST>(smem, E, tid);
   __syncthreads();
 
   unsigned char* wsm = smem + kOffWave + wid * kWBytes;
@@ -673,67 +754,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   }
   __syncthreads();
 
-  // ---- flush the workgroup's private tables (integer atomics, order-free)
-  if constexpr (HT == kHtPair) {
-    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
-    auto* hc = reinterpret_cast<uint32_t*>(smem + kOffHc);
-    for (uint32_t s = tid; s < kPairSlots; s += kThreads) {
-      const uint32_t cnt = hc[s];
-      if (cnt) atomicAdd(&tab.hist[hk[s] - 1u], (unsigned long long)cnt);
-    }
-  }
-  if constexpr (HT == kHtCompact) {
-    auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
-    const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
-    for (uint32_t s = tid; s < kCmpSlots; s += kThreads) {
-      const uint32_t w = hk[s];
-      if (w >> tab.kb) atomicAdd(&tab.hist[(w & kmask) - 1u], (unsigned long long)(w >> tab.kb));
-    }
-  }
-  if constexpr (ST == kStSlot) {
-    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
-    auto* st4 = reinterpret_cast<uint32_t*>(smem + kOffMm);
-    for (uint32_t s = tid; s < kSlotEdges; s += kThreads) {
-      const uint32_t key = st4[4u * s];
-      if (key) {
-        const uint32_t e = key - 1u;
-        unsigned long long sum = 0;
-        for (uint32_t k = 0; k < kSlotSumReps; ++k) sum += lsum[s * kSlotSumReps + k];
-        atomicAdd(&tab.sum[e], sum);
-        if (st4[4u * s + 3u]) atomicAdd(&tab.err[e], (unsigned long long)st4[4u * s + 3u]);
-        atomicMin(&tab.mn[e], st4[4u * s + 1u]);
-        atomicMax(&tab.mx[e], st4[4u * s + 2u]);
-      }
-    }
-  }
-  if constexpr (ST == kStWide) {
-    auto* ent = reinterpret_cast<uint32_t*>(smem + kOffSum);
-    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffWideErr);
-    for (uint32_t e = tid; e < E; e += kThreads) {
-      const uint32_t mn = ent[4u * e + 2u], mx = ent[4u * e + 3u];
-      if (mn != 0xFFFFFFFFu || mx != 0u) {
-        atomicAdd(&tab.sum[e], *reinterpret_cast<const unsigned long long*>(ent + 4u * e));
-        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
-        atomicMin(&tab.mn[e], mn);
-        atomicMax(&tab.mx[e], mx);
-      }
-    }
-  }
-  if constexpr (ST == kStDirect) {
-    auto* lsum = reinterpret_cast<unsigned long long*>(smem + kOffSum);
-    auto* lerr = reinterpret_cast<uint32_t*>(smem + kOffErr);
-    auto* lmm = reinterpret_cast<uint32_t*>(smem + kOffMm);
-    for (uint32_t e = tid; e < E; e += kThreads) {
-      if (lmm[2u * e] != 0xFFFFFFFFu || lmm[2u * e + 1u] != 0u) {
-        unsigned long long sum = 0;
-        for (uint32_t k = 0; k < kSumReps; ++k) sum += lsum[e * kSumReps + k];
-        atomicAdd(&tab.sum[e], sum);
-        if (lerr[e]) atomicAdd(&tab.err[e], (unsigned long long)lerr[e]);
-        atomicMin(&tab.mn[e], lmm[2u * e]);
-        atomicMax(&tab.mx[e], lmm[2u * e + 1u]);
-      }
-    }
-  }
+  tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
 // Count + nearest-rank quantiles per edge from the merged histogram: one
@@ -875,13 +896,31 @@ uint64_t big_capacity(const anomod_spans* s) {
   return by_spans < s->n_traces ? by_spans : s->n_traces;
 }
 
-// The long-trace pass after the chunk walk (no-op when nothing was listed).
-template <int HT>
-hipError_t launch_big(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S, const Table& tab) {
-  hipLaunchKernelGGL(edge_big_kernel<HT>, dim3((unsigned)ctx->num_cus), dim3(kBigThreads), 0,
-                     ctx->stream, spans->span_id, spans->parent_span_id, spans->svc_flags,
-                     spans->dur_us, spans->trace_ptr, S, tab);
+// The long-trace pass after the chunk walk (no-op when nothing was listed),
+// with the chunk walk's table forms.
+template <int HT, int ST>
+hipError_t launch_big(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S, uint32_t E,
+                      const Table& tab) {
+  hipLaunchKernelGGL((edge_big_kernel<HT, ST>), dim3((unsigned)ctx->num_cus), dim3(kBigThreads),
+                     0, ctx->stream, spans->span_id, spans->parent_span_id, spans->svc_flags,
+                     spans->dur_us, spans->trace_ptr, S, E, tab);
   return hipGetLastError();
+}
+
+hipError_t launch_big_for(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S, uint32_t E,
+                          const Table& tab) {
+  // the LDS tables' u32 counters hold < 2^32 records per workgroup: a set
+  // whose listed traces could exceed a launch's bound records to HBM
+  if (spans->n_spans >= max_launch_spans()) return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
+  const char* name = nullptr;
+  const KernelFn fn = pick_kernel(E, &name);
+  if (fn == edge_agg_kernel<kHtPair, kStDirect>)
+    return launch_big<kHtPair, kStDirect>(ctx, spans, S, E, tab);
+  if (fn == edge_agg_kernel<kHtCompact, kStWide>)
+    return launch_big<kHtCompact, kStWide>(ctx, spans, S, E, tab);
+  if (fn == edge_agg_kernel<kHtCompact, kStSlot>)
+    return launch_big<kHtCompact, kStSlot>(ctx, spans, S, E, tab);
+  return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
 }
 
 }  // namespace
@@ -959,7 +998,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
                          spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
       ANOMOD_HIP(ctx, hipGetLastError());
     }
-    if (big_cap) ANOMOD_HIP(ctx, (launch_big<kHtHbm>(ctx, spans, S, tab)));
+    if (big_cap) ANOMOD_HIP(ctx, launch_big_for(ctx, spans, S, E, tab));
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
 
@@ -1076,7 +1115,8 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
                          spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
       e = hipGetLastError();
     }
-    if (e == hipSuccess && rc == ANOMOD_OK && big_cap) e = launch_big<kHtKeys>(ctx, spans, S, tab);
+    if (e == hipSuccess && rc == ANOMOD_OK && big_cap)
+      e = launch_big<kHtKeys, kStHbm>(ctx, spans, S, E, tab);
     if (e == hipSuccess && rc == ANOMOD_OK)
       e = hipcub::DeviceRadixSort::SortKeys(tmp, sort_tmp, keys, sorted, n, 0, 32 + kbits,
                                              ctx->stream);

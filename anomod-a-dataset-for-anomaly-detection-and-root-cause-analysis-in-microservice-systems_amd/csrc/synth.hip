@@ -274,8 +274,39 @@ HostTopo build_tt() {
   return b.finish();
 }
 
+// --- LONG: SocialNetwork services in traces of 16 .. 4000 spans -----------
+// Not a reference topology: the length / depth stress case beside SN and TT
+// (batch jobs, fan-out crawls, retried chains).  Random trees from a fixed
+// seed: each span's parent is the previous span with p = 0.6 (long chains),
+// else a uniformly drawn earlier span.  Span shares by trace length: 16 / 48
+// / 128 spans 20 % each, 256 / 600 / 1500 / 4000 spans 10 % each, so 30 % of
+// the spans sit in traces longer than a 256-span wave chunk.
+HostTopo build_long() {
+  static const char* kSvc[] = {"compose-post-service", "home-timeline-service", "media-service",
+                               "nginx-web-server",     "post-storage-service",  "social-graph-service",
+                               "text-service",         "unique-id-service",     "url-shorten-service",
+                               "user-mention-service", "user-service",          "user-timeline-service"};
+  static const double kMedian[] = {8000, 1900, 150, 2500, 1200, 900, 2500, 120, 900, 800, 400, 1800};
+  std::vector<std::string> names(std::begin(kSvc), std::end(kSvc));
+  Builder b(names);
+  static const struct { int len; double share; } kLen[] = {
+      {16, 0.2}, {48, 0.2}, {128, 0.2}, {256, 0.1}, {600, 0.1}, {1500, 0.1}, {4000, 0.1}};
+  uint64_t st = 0x4C4F4E47ull;  // "LONG"
+  auto next = [&]() { st += 0x9E3779B97F4A7C15ull; return splitmix64(st); };
+  for (const auto& t : kLen) {
+    std::vector<SpanDef> spans;
+    for (int j = 0; j < t.len; ++j) {
+      const int par = j == 0 ? -1 : (next() % 10 < 6 ? j - 1 : (int)(next() % (uint64_t)j));
+      const int sv = j == 0 ? 3 : (int)(next() % 12);
+      spans.push_back({par, kSvc[sv], kMedian[sv], 0.5});
+    }
+    b.add_template(spans, t.share / t.len);
+  }
+  return b.finish();
+}
+
 std::once_flag g_topo_once;
-std::unique_ptr<HostTopo> g_topo[2];
+std::unique_ptr<HostTopo> g_topo[3];
 
 }  // namespace
 
@@ -283,8 +314,9 @@ const HostTopo* host_topo(uint32_t topology) {
   std::call_once(g_topo_once, [] {
     g_topo[0].reset(new HostTopo(build_sn()));
     g_topo[1].reset(new HostTopo(build_tt()));
+    g_topo[2].reset(new HostTopo(build_long()));
   });
-  if (topology > 1) return nullptr;
+  if (topology > 2) return nullptr;
   return g_topo[topology].get();
 }
 

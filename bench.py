@@ -34,7 +34,7 @@ import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
 LEGS = ("trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped", "tt_width",
-        "pagerank", "ewma", "tt_config2", "tt_config2_files")
+        "long_traces", "pagerank", "ewma", "tt_config2", "tt_config2_files")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
 
@@ -457,6 +457,15 @@ def main() -> int:
                           args.traces_per_gpu, shard=rank)
         result["tt_width"] = edge_leg(ctx, tt, 3, "edge kernel on synthetic TrainTicket spans")
         tt.free()
+    if "long_traces" in legs:
+        # --- trace length / depth stress (SynthSpec LONG: SN services, traces
+        # of 16..4000 spans, 30 % of the spans in traces longer than a wave
+        # chunk -> the workgroup-per-trace pass), 2^23 traces (~4.4e8 spans)
+        lt = ctx.generate(anomod.SynthSpec("LONG", seed=args.seed, p_orphan_ppm=100),
+                          max(1, args.traces_per_gpu // 16), shard=rank)
+        result["long_traces"] = edge_leg(ctx, lt, 3, "edge kernel on LONG spans (traces of "
+                                         "16..4000 spans; > 256 via the workgroup-per-trace pass)")
+        lt.free()
 
     if "pagerank" in legs:
         # --- PageRank RCA: replicas (one graph + personalization per GPU)

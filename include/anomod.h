@@ -160,6 +160,7 @@ int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* grouped, uint64_t 
 /* ---- synthetic workload ----------------------*/
 #define ANOMOD_TOPO_SN 0 /* DeathStarBench SocialNetwork, 12 services        */
 #define ANOMOD_TOPO_TT 1 /* TrainTicket, 46 services                         */
+#define ANOMOD_TOPO_LONG 2 /* SN services, traces of 16..4000 spans (stress) */
 
 typedef struct {
   uint32_t topology;          /* ANOMOD_TOPO_*                               */
