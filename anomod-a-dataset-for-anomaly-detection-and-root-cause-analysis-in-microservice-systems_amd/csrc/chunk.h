@@ -62,13 +62,20 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 }
 
 // lo/hi = trace_ptr[t + lane], trace_ptr[t + lane + 1] (see load_bounds).
+// A trace longer than big_min (<= kStage) is a chunk of its own (k == 0):
+// the kernels hand such traces to their workgroup-per-trace pass.
 __device__ __forceinline__ Chunk make_chunk(uint64_t t, uint64_t t_end, int lane, uint64_t lo,
-                                            uint64_t hi) {
+                                            uint64_t hi, uint32_t big_min = kStage) {
   Chunk c;
   const bool valid = t + lane < t_end;
   c.base = readlane64(lo, 0);
   const bool fits = valid && (hi - c.base) <= (uint64_t)kStage;
   c.k = (uint32_t)__popcll(__ballot(fits));  // fits is a prefix of the lanes
+  if (big_min < (uint32_t)kStage) {
+    const uint64_t lm = __ballot(valid && (hi - lo) > (uint64_t)big_min);
+    const uint32_t first = lm ? (uint32_t)__ffsll((unsigned long long)lm) - 1u : 64u;
+    c.k = first < c.k ? first : c.k;  // 0 when the first trace is long: a chunk of its own
+  }
   c.n = (uint32_t)(readlane64(hi, c.k ? (int)c.k - 1 : 0) - c.base);
   c.start = (uint32_t)(lo - c.base);
   return c;

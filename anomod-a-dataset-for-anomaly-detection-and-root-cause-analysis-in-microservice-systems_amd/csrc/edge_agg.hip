@@ -579,6 +579,11 @@ __device__ __forceinline__ void tables_flush(unsigned char* smem, uint32_t E, co
 // reference gives the first match (the reference rule).
 // O(L * ceil(L / kBigWin)) work, O(L) for L <= kBigWin.
 constexpr int kBigThreads = kThreads;  // the tables' init / flush loops assume it
+#ifndef ANOMOD_BIG_MIN
+#define ANOMOD_BIG_MIN 256
+#endif
+// traces longer than this take the long-trace pass (<= kStage)
+constexpr uint32_t kBigMin = ANOMOD_BIG_MIN;
 constexpr uint32_t kBigWin = 2048;    // ids per table window
 constexpr uint32_t kBigSlots = 4096;  // table slots (load <= 0.5)
 constexpr int kBigPer = 8;            // spans per thread per lookup block
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     // in flight while chunk c is resolved and recorded.
     uint64_t lo, hi;
     load_bounds(trace_ptr, t_begin, t_end, lane, lo, hi);
-    Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi);
+    Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi, kBigMin);
     Regs R;
     load_regs(col, cur, lane, R);
     uint64_t t_cur = t_begin;
@@ -728,7 +733,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       Chunk nxt{};
       Regs Rn;
       if (has_next) {
-        nxt = make_chunk(t_next, t_end, lane, lo, hi);
+        nxt = make_chunk(t_next, t_end, lane, lo, hi, kBigMin);
         load_regs(col, nxt, lane, Rn);
         t_next += nxt.k ? nxt.k : 1u;
         load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
@@ -888,11 +893,11 @@ struct Layout {
   size_t off_list() const { return (end_small + 7) & ~size_t(7); }
 };
 
-// Long traces (> kStage spans) a span set can hold: 0 when its longest trace
+// Long traces (> kBigMin spans) a span set can hold: 0 when its longest trace
 // is known to fit a chunk.
 uint64_t big_capacity(const anomod_spans* s) {
-  if (s->max_trace_len <= (uint64_t)kStage) return 0;
-  const uint64_t by_spans = s->n_spans / (uint64_t)(kStage + 1);
+  if (s->max_trace_len <= (uint64_t)kBigMin) return 0;
+  const uint64_t by_spans = s->n_spans / (uint64_t)(kBigMin + 1);
   return by_spans < s->n_traces ? by_spans : s->n_traces;
 }
 

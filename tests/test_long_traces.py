@@ -139,3 +139,28 @@ def test_gpu_long_traces_duplicates_and_cycles(ctx):
     for k in ("count", "errors", "sum_us", "min_us", "max_us"):
         np.testing.assert_array_equal(getattr(got, k), ref[k], err_msg=k)
     np.testing.assert_array_equal(got.hist, ref["hist"])
+
+
+@pytest.mark.gpu
+def test_gpu_long_topology_device_generation_and_parity(ctx):
+    """SynthSpec LONG (SN services, traces of 16..4000 spans, 30 % of the spans
+    past the wave path): device generation == host generation, edge table and
+    trace structure == the C oracle."""
+    spec = anomod.SynthSpec("LONG", seed=4, p_orphan_ppm=2000)
+    n = 3000
+    dev = ctx.generate(spec, n)
+    host = anomod.synth_generate_host(spec, n)
+    got = dev.download()
+    for k in ("trace_ptr", "span_id", "parent_span_id", "svc", "flags", "dur_us"):
+        np.testing.assert_array_equal(getattr(got, k), getattr(host, k), err_msg=k)
+    assert np.diff(host.trace_ptr).max() > 1000
+    ref = native.edge_aggregate(host)
+    t = ctx.edge_aggregate(dev)
+    for k in ("count", "errors", "sum_us", "min_us", "max_us"):
+        np.testing.assert_array_equal(getattr(t, k), ref[k], err_msg=k)
+    np.testing.assert_array_equal(t.hist, ref["hist"])
+    ref = native.trace_structure(host)
+    ts = ctx.trace_structure(dev)
+    for k in TS_FIELDS:
+        np.testing.assert_array_equal(getattr(ts, k), ref[k], err_msg=k)
+
