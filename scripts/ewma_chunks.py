@@ -11,17 +11,23 @@ sys.path[:0] = [str(ROOT / "anomod-a-dataset-for-anomaly-detection-and-root-caus
 import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
+import time
+
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 131040
 chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+gap_s = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0  # idle time between fill and scoring
 with anomod.Context(0) as ctx:
     ser = anomod.DeviceSeries(ctx, steps, 100000)
     out = []
     for c in range(chunks):
         ser.fill_synthetic(7, c * steps)
+        ctx.synchronize()
+        if gap_s:
+            time.sleep(gap_s)
         ms = []
         for _ in range(3):
             ser.ewma_z(2 / 61, 60, download=False)
             ms.append(round(ctx.stage_ms(L.STAGE_EWMA), 3))
         out.append(ms)
-        print(json.dumps({"chunk": c, "ms": ms}), flush=True)
+        print(json.dumps({"chunk": c, "gap_s": gap_s, "ms": ms}), flush=True)
     ser.free()
