@@ -436,6 +436,12 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
       break;
     }
   }
+  // Every row's final value (xr: the last vector this block computed, or x0
+  // when none) lands in x0, so the host copies one buffer without first
+  // reading `done` back.  Safe: every block leaves the loop at the same
+  // iteration, and a block still gathering for an abandoned iteration
+  // discards what it reads.
+  if (r < N) __hip_atomic_store(&x0[r], xr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == 0 && threadIdx.x == 0) bar[2] = done;
 }
 
@@ -716,8 +722,8 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   // (the host-side copy, division and pageable DMA were ~30 % of a
   // 100-iteration solve at N = 10^5)
   if (!g->h_pin)
-    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&g->h_pin), N * 8ull,
-                                  hipHostMallocDefault));
+    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&g->h_pin), N * 8ull + 16,
+                                  hipHostMallocDefault));  // + the barrier words
   memcpy(g->h_pin, p, N * 8ull);
   ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, g->h_pin, N * 8ull, hipMemcpyHostToDevice, ctx->stream));
   // x0 = 1/N; its dangling mass n_dangling/N seeds iteration 0 (slot 0); the
@@ -804,19 +810,21 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     done = iters;
   }
   if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+  // the persistent solve leaves its result in x[0]: one copy, one wait
+  unsigned int* hb = reinterpret_cast<unsigned int*>(g->h_pin + N);  // pinned, past the vector
+  if (persistent)
+    ANOMOD_HIP(ctx, hipMemcpyAsync(hb, g->bar, 4 * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[persistent ? 0 : (done & 1)], N * 8ull,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (persistent) {
-    unsigned int hb[4] = {0, 0, 0, 0};
-    ANOMOD_HIP(ctx, hipMemcpyAsync(hb, g->bar, sizeof(hb), hipMemcpyDeviceToHost, ctx->stream));
-    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (hb[1]) {
       set_error(ctx, "PageRank grid barrier timed out (iteration %u)", hb[2]);
       return ANOMOD_EHIP;
     }
     done = hb[2];
   }
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
-                                 ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   memcpy(x_out, g->h_pin, N * 8ull);
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;

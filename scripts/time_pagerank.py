@@ -21,9 +21,12 @@ with anomod.Context(0) as ctx:
     p = np.random.default_rng(0).random(g.N)
     ref = {}
     for mode, sub in [(m, s) for m in os.environ.get("PPR_MODES", "0,1,2").split(",")
-                      for s in (os.environ.get("PPR_SUBS", "1,2,4").split(",") if m == "2" else ["4"])]:
+                      for s in (os.environ.get("PPR_SUBS", "1,2,4").split(",") if m == "2" else ["default"])]:
         os.environ["ANOMOD_PPR_MODE"] = mode
-        os.environ["ANOMOD_PPR_SUB"] = sub
+        if sub == "default":
+            os.environ.pop("ANOMOD_PPR_SUB", None)
+        else:
+            os.environ["ANOMOD_PPR_SUB"] = sub
         for iters, tol in ((100, 0.0), (1000, 1e-10)):
             x, _ = g.pagerank(p, iters=iters, tol=tol)
             same = bool(np.array_equal(ref.setdefault((iters, tol), x), x))
