@@ -37,12 +37,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
                                            0x00020000);
 }
 
+// Cache policy of the streamed span-column loads (aux bits: 1 = sc0, 2 = nt,
+// 16 = sc1); every column is read once per launch.
+#ifndef ANOMOD_LOAD_AUX
+#define ANOMOD_LOAD_AUX 0
+#endif
+
 __device__ __forceinline__ uint64_t bload64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return (uint64_t)__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return (uint64_t)__builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, ANOMOD_LOAD_AUX);
 }
 
 __device__ __forceinline__ uint32_t bload32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, ANOMOD_LOAD_AUX);
+}
+
+// Streamed per-span output stores (written once, never re-read by the
+// kernel): plain, or nontemporal with ANOMOD_STORE_NT.
+#ifndef ANOMOD_STORE_NT
+#define ANOMOD_STORE_NT 0
+#endif
+template <class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+  if constexpr (ANOMOD_STORE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 // One wave's chunk: up to 64 consecutive traces holding <= kStage spans, or a

@@ -271,11 +271,11 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
     const uint32_t i = lane + r * kWave;
     if (i < c.n) {
       const uint64_t g = c.base + i;
-      o.parent_pos[g] = np[r] >= 0 ? (uint32_t)np[r] - a[r] : ANOMOD_NO_PARENT;
-      o.depth[g] = (nxt[r] & kDone) ? dst[r] : 0u;
-      o.n_children[g] = lcnt[f[r]];
-      o.flags[g] = (uint8_t)((np[r] < 0 ? ANOMOD_SPAN_ROOT : 0u) |
-                             (f[r] == (int)i ? ANOMOD_SPAN_FIRST : 0u));
+      st_out(&o.parent_pos[g], np[r] >= 0 ? (uint32_t)np[r] - a[r] : ANOMOD_NO_PARENT);
+      st_out(&o.depth[g], (nxt[r] & kDone) ? dst[r] : 0u);
+      st_out(&o.n_children[g], (uint32_t)lcnt[f[r]]);
+      st_out(&o.flags[g], (uint8_t)((np[r] < 0 ? ANOMOD_SPAN_ROOT : 0u) |
+                                    (f[r] == (int)i ? ANOMOD_SPAN_FIRST : 0u)));
     }
   }
   // Per trace: lane l < k owns trace t0 + l.  Span-parallel words (complete:

@@ -41,7 +41,7 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--one":
         one(traces, 7)
         return
-    libs = [None] + sorted(str(p) for p in (PKG / "csrc/build/variants").glob("libanomod_*.so"))
+    libs = [None] + sorted(str(p) for p in (PKG / "csrc/build/variants").glob(os.environ.get("ABL_GLOB", "libanomod_*.so")))
     print("libs:", [Path(l).name if l else "main" for l in libs], flush=True)
     for lib in libs * int(os.environ.get("ABL_ROUNDS", 1)):
         env = dict(os.environ)
