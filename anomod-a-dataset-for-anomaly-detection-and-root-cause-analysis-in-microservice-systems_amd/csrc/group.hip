@@ -14,29 +14,28 @@
 // the reference would (first match, trace_collector.py:424-443).
 //
 // Design (MI355X):
-//  * one histogram pass over trace_hash (8 B/span) gives the digit counts of
-//    every radix pass;
-//  * P LSD passes over 8-bit digits of the top 8P bits of k, each ONE kernel
-//    (onesweep): a 4096-record tile is ranked stably with wave ballots (8
-//    ballots give each lane its same-digit peers; rank = popc of the lower
-//    peers; a per-wave LDS counter per digit carries the running count down
-//    the wave's 4 rows), the tile's digit totals are published with a
-//    decoupled look-back over tiles (tile ids from an atomic ticket, so a
-//    tile only ever waits on running predecessors; state words carry an
-//    8-bit epoch so the array is never cleared between passes), the tile is
-//    staged in LDS in digit order and written as coalesced digit runs of
-//    32-B records (AoS: hash, span_id, parent, svc|flags, dur);
+//  * P LSD passes over 8-bit digits of the top 8P bits of k.  Per pass: the
+//    digit counts of every 4096-record tile (a read of trace_hash for the
+//    first pass, of the 1-B digits the previous pass wrote beside its
+//    records for the others), an exclusive scan of those counts over tiles
+//    (reduce-then-scan: no chained look-back, no per-tile ticket), then ONE
+//    scatter kernel: a tile is ranked stably with wave ballots (8 ballots
+//    give each lane its same-digit peers; rank = popc of the lower peers; a
+//    per-wave LDS counter per digit carries the running count down the
+//    wave's 4 rows), staged in LDS in digit order and written as coalesced
+//    digit runs — 32-B records (hash, span_id, parent, svc|flags, dur), the
+//    last pass the grouped SoA columns themselves;
 //  * with P = ceil(log2(n) / 8) the top 8P bits nearly always separate
-//    traces; a copy pass writes the grouped SoA columns and lists every key
-//    change inside a bucket of equal top bits; one wave per such bucket
-//    sorts it in LDS by (k, arrival) — rank = #{smaller k} + #{equal k
-//    earlier} — and rewrites its rows; a list overflow or a mixed bucket
-//    larger than the wave's LDS reruns the sort with P + 1 (at P = 8 no
-//    bucket is mixed), so the output never depends on P;
+//    traces; a scan over the grouped hashes lists every key change inside a
+//    bucket of equal top bits; one wave per such bucket sorts it by (k,
+//    arrival) — rank = #{smaller k} + #{equal k earlier} — into a scratch
+//    copy that is then written back; a list overflow or a mixed bucket larger
+//    than the wave's LDS reruns the sort with P + 1 (at P = 8 no bucket is
+//    mixed), so the output never depends on P;
 //  * trace_ptr: one pass over the grouped hashes, trace starts compacted
-//    with a block scan and a decoupled look-back over 4096-span tiles.
-// Bytes per span: 8 (histogram) + 64 per radix pass + 64 (copy) + 8
-// (trace_ptr) + 8 per trace.
+//    with ballot ranks and a decoupled look-back over 4096-span tiles.
+// Bytes per span: 8 + 2 (P - 1) (tile counts) + 64 per radix pass + 8 (bucket
+// list) + 8 (trace_ptr) + 8 per trace.
 #include <algorithm>
 #include <cmath>
 
@@ -57,8 +56,12 @@ struct GroupWs {
   uint64_t* tptr = nullptr;           // [cap + 1]
   uint64_t* state = nullptr;          // look-back words
   uint64_t state_words = 0;
-  unsigned long long* misc = nullptr; // hist | tickets | counters
+  unsigned long long* misc = nullptr; // counters
   unsigned long long* list = nullptr; // key changes inside buckets
+  unsigned long long* owned = nullptr;  // mixed buckets sorted into scratch (start << 11 | size)
+  uint32_t* tcnt = nullptr;           // [tiles][256] digit counts, then run starts
+  uint32_t* bsum = nullptr;           // [tiles / 256 + 1][256] block sums of tcnt
+  uint8_t* dig = nullptr;             // [cap + 16] every record's digit of the next pass
   uint64_t list_cap = 0;
   uint32_t epoch = 0;
   unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
@@ -67,6 +70,11 @@ struct GroupWs {
 namespace {
 
 using chunk::wave_sync;
+// Experiment-only ablation (never set in the shipped build; timing only,
+// wrong output): 1 = every pass writes its staged tile to the tile's own rows.
+#ifndef ANOMOD_GRP_ABL
+#define ANOMOD_GRP_ABL 0
+#endif
 constexpr int kWv = 64;
 constexpr int kSThreads = 1024;              // scatter workgroup
 constexpr int kSWaves = kSThreads / kWv;
@@ -84,9 +92,8 @@ constexpr uint64_t kValMask = (1ull << 54) - 1;
 constexpr uint32_t kSpinLimit = 1u << 26;
 
 // misc layout (u64 words)
-constexpr int kMiscHist = 0;                          // [kMaxPasses][256]
-constexpr int kMiscTicket = kMiscHist + kMaxPasses * kDig;  // [kMaxPasses + 1]
-constexpr int kMiscListCnt = kMiscTicket + kMaxPasses + 1;
+constexpr int kMiscTicket = 0;                        // [2] tiles of the two scans
+constexpr int kMiscListCnt = kMiscTicket + 2;         // key changes inside buckets
 constexpr int kMiscOver = kMiscListCnt + 1;           // oversized mixed buckets
 constexpr int kMiscTraces = kMiscOver + 1;            // n_traces
 constexpr int kMiscErr = kMiscTraces + 1;             // look-back timeout
@@ -151,58 +158,127 @@ struct SoaOut {
   uint32_t* __restrict__ dur;
 };
 
-// ---- digit histograms of every pass (one read of trace_hash) -------------
-__global__ __launch_bounds__(256) void group_hist_kernel(const uint64_t* __restrict__ h,
-                                                         uint64_t n, int passes, int shift0,
-                                                         unsigned long long* __restrict__ hist) {
-  __shared__ uint32_t lh[kMaxPasses * kDig];
-  for (int i = threadIdx.x; i < passes * kDig; i += 256) lh[i] = 0u;
+// ---- per-tile digit counts and their exclusive scan over tiles -------------
+// Reduce-then-scan instead of a decoupled look-back: a chained look-back over
+// ~n/4096 tiles waits on predecessors' L2 round trips (measured: 36 % of the
+// grouping time at 2^25 traces), while counting a tile's digits costs one
+// more read of 1 B/span (8 B/span from trace_hash for the first pass): the
+// previous pass writes every record's next digit beside it.
+template <bool FROM_H>
+__global__ __launch_bounds__(256) void group_tcount_kernel(const uint64_t* __restrict__ h,
+                                                           const uint8_t* __restrict__ dig,
+                                                           uint64_t n, int shift,
+                                                           uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t lh[kDig];
+  const int tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kSTile;
+  lh[tid] = 0u;
   __syncthreads();
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const uint64_t k = mix64(h[i]);
-    for (int p = 0; p < passes; ++p)
-      atomicAdd(&lh[p * kDig + (uint32_t)((k >> (shift0 + 8 * p)) & 255u)], 1u);
+  if constexpr (FROM_H) {
+#pragma unroll
+    for (int j = 0; j < kSTile / 256; ++j) {
+      const uint64_t p = t0 + (uint64_t)(j * 256 + tid);
+      if (p < n) atomicAdd(&lh[(uint32_t)(mix64(h[p]) >> shift) & 255u], 1u);
+    }
+  } else {
+    // 16 consecutive digits per thread (one 16-B load), 4096 per tile
+    const uint64_t p0 = t0 + (uint64_t)tid * 16u;
+    if (p0 + 16u <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(dig + p0);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) atomicAdd(&lh[(wv[q >> 2] >> (8 * (q & 3))) & 255u], 1u);
+    } else {
+      for (uint64_t p = p0; p < n && p < p0 + 16u; ++p) atomicAdd(&lh[dig[p]], 1u);
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < passes * kDig; i += 256)
-    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+  tcnt[(uint64_t)blockIdx.x * kDig + tid] = lh[tid];
 }
 
-// ---- one stable LSD pass (onesweep) ---------------------------------------
-template <bool SOA_IN>
+constexpr int kTScanRows = 256;  // tiles per block of the tile-count scan
+
+// column sums of kTScanRows tiles (one thread per digit)
+__global__ __launch_bounds__(kDig) void group_tscan_up_kernel(const uint32_t* __restrict__ tcnt,
+                                                              uint64_t tiles,
+                                                              uint32_t* __restrict__ bsum) {
+  const uint64_t a = (uint64_t)blockIdx.x * kTScanRows;
+  const uint64_t b = a + kTScanRows < tiles ? a + kTScanRows : tiles;
+  uint32_t s = 0;
+#pragma unroll 8
+  for (uint64_t t = a; t < b; ++t) s += tcnt[t * kDig + threadIdx.x];
+  bsum[(uint64_t)blockIdx.x * kDig + threadIdx.x] = s;
+}
+
+// one block: exclusive scan of the block sums down every digit, digit starts
+// (exclusive scan of the digit totals) added in
+__global__ __launch_bounds__(kDig) void group_tscan_top_kernel(uint32_t* __restrict__ bsum,
+                                                               uint64_t nb) {
+  __shared__ uint32_t wsum[kDig / kWv];
+  const int d = threadIdx.x, lane = d & (kWv - 1), w = d / kWv;
+  uint32_t run = 0;
+  for (uint64_t b = 0; b < nb; ++b) {
+    const uint32_t x = bsum[b * kDig + d];
+    bsum[b * kDig + d] = run;
+    run += x;
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < kWv; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWv - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t start = inc - run;
+  for (int ww = 0; ww < w; ++ww) start += wsum[ww];
+  for (uint64_t b = 0; b < nb; ++b) bsum[b * kDig + d] += start;
+}
+
+// every tile's count replaced by the global start of its digit run
+__global__ __launch_bounds__(kDig) void group_tscan_down_kernel(uint32_t* __restrict__ tcnt,
+                                                                uint64_t tiles,
+                                                                const uint32_t* __restrict__ bsum) {
+  const uint64_t a = (uint64_t)blockIdx.x * kTScanRows;
+  const uint64_t b = a + kTScanRows < tiles ? a + kTScanRows : tiles;
+  uint32_t run = bsum[(uint64_t)blockIdx.x * kDig + threadIdx.x];
+#pragma unroll 8
+  for (uint64_t t = a; t < b; ++t) {
+    const uint32_t x = tcnt[t * kDig + threadIdx.x];
+    tcnt[t * kDig + threadIdx.x] = run;
+    run += x;
+  }
+}
+
+// ---- one stable LSD pass ----------------------------------------------------
+// Tile = 4096 records (1024 threads x 4), ranked stably with wave ballots (8
+// ballots give each lane its same-digit peers; rank = popc of the lower
+// peers; a per-wave LDS counter per digit carries the count down the wave's
+// 4 rows), staged in LDS in digit order and written as digit runs from the
+// global run starts of the tile-count scan.  The last pass writes the grouped
+// SoA columns; the others 32-B records plus the next pass's digit.
+template <bool SOA_IN, bool SOA_OUT>
 __global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
-    SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
-    const unsigned long long* __restrict__ hist, uint64_t* __restrict__ state, uint32_t epoch,
-    unsigned long long* __restrict__ ticket, unsigned long long* __restrict__ err) {
+    SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, SoaOut sout, uint64_t n,
+    int shift, const uint32_t* __restrict__ toff, uint8_t* __restrict__ dnext) {
   __shared__ GRec stage[kSTile];                 // 128 KiB
   __shared__ uint16_t wcnt[kSWaves][kDig];       // per-wave digit counts, then wave offsets
   __shared__ uint8_t sdig[kSTile];
   __shared__ uint32_t tstart[kDig];              // tile-local start of each digit
-  __shared__ unsigned long long gbase[kDig];     // global start of each digit's run
-  __shared__ unsigned long long hbase[kDig];
+  __shared__ uint32_t gbase[kDig];               // global start of each digit's run
   __shared__ uint32_t wsum_t[kDig / kWv];
-  __shared__ unsigned long long wsum_h[kDig / kWv];
-  __shared__ unsigned long long s_tile;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1ull);
-  for (int i = tid; i < kSWaves * kDig / 2; i += kSThreads)
-    reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0u;
-  __syncthreads();
-  const uint64_t tile = s_tile;
-  const uint64_t base = tile * kSTile;
 
   // a record as two 16-B halves: (h, sid) and (pid, sf | dur << 32)
+  const uint64_t tile = blockIdx.x;
+  const uint64_t base = tile * kSTile;
   uint4 ra[kSPer], rb[kSPer];
-  uint32_t d[kSPer];
-  bool v[kSPer];
 #pragma unroll
   for (int k = 0; k < kSPer; ++k) {
     const uint64_t i = base + (uint64_t)(w * (kRowsPerWave * kWv) + k * kWv + lane);
-    v[k] = i < n;
     ra[k] = make_uint4(0, 0, 0, 0);
     rb[k] = make_uint4(0, 0, 0, 0);
-    if (v[k]) {
+    if (i < n) {
       if constexpr (SOA_IN) {
         const uint64_t h = sin.h[i], sid = sin.sid[i], pid = sin.pid[i];
         ra[k] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)sid, (uint32_t)(sid >> 32));
@@ -213,6 +289,16 @@ __global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
         rb[k] = q[1];
       }
     }
+  }
+  for (int i = tid; i < kSWaves * kDig / 2; i += kSThreads)
+    reinterpret_cast<uint32_t*>(&wcnt[0][0])[i] = 0u;
+  if (tid < kDig) gbase[tid] = toff[tile * kDig + tid];
+  __syncthreads();
+  uint32_t d[kSPer];
+  bool v[kSPer];
+#pragma unroll
+  for (int k = 0; k < kSPer; ++k) {
+    v[k] = base + (uint64_t)(w * (kRowsPerWave * kWv) + k * kWv + lane) < n;
     d[k] = (uint32_t)(mix64(((uint64_t)ra[k].y << 32) | ra[k].x) >> shift) & 255u;
   }
 
@@ -241,8 +327,7 @@ __global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
   __syncthreads();
 
   // Per digit (threads 0..255): wave offsets + tile total, then the tile's
-  // digit starts and the pass's global digit starts (two block scans).
-  uint32_t total = 0;
+  // digit starts (block scan).
   if (tid < kDig) {
     uint32_t run = 0;
     for (int ww = 0; ww < kSWaves; ++ww) {
@@ -250,43 +335,19 @@ __global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
       wcnt[ww][tid] = (uint16_t)run;
       run += c;
     }
-    total = run;
-    const unsigned long long hcount = hist[tid];
+    const uint32_t total = run;
     uint32_t inc = total;
-    unsigned long long hinc = hcount;
 #pragma unroll
     for (int o = 1; o < kWv; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o);
-      const unsigned long long hy = __shfl_up(hinc, o);
-      if (lane >= o) {
-        inc += y;
-        hinc += hy;
-      }
+      if (lane >= o) inc += y;
     }
     tstart[tid] = inc - total;
-    hbase[tid] = hinc - hcount;
-    if (lane == kWv - 1) {
-      wsum_t[w] = inc;
-      wsum_h[w] = hinc;
-    }
+    if (lane == kWv - 1) wsum_t[w] = inc;
   }
   __syncthreads();
-  if (tid < kDig) {
-    for (int ww = 0; ww < w; ++ww) {
-      tstart[tid] += wsum_t[ww];
-      hbase[tid] += wsum_h[ww];
-    }
-    uint64_t* st = state + tile * kDig + tid;
-    uint64_t excl = 0;
-    if (tile == 0) {
-      publish(st, pack_state(epoch, 2u, total));
-    } else {
-      publish(st, pack_state(epoch, 1u, total));
-      excl = look_back(state, kDig, tile, (uint32_t)tid, epoch, err);
-      publish(st, pack_state(epoch, 2u, excl + total));
-    }
-    gbase[tid] = hbase[tid] + excl;
-  }
+  if (tid < kDig)
+    for (int ww = 0; ww < w; ++ww) tstart[tid] += wsum_t[ww];
   __syncthreads();
 
   // Stage the tile in digit order.
@@ -308,54 +369,130 @@ __global__ __launch_bounds__(kSThreads) void group_scatter_kernel(
     if (p < nvalid) {
       const uint32_t dd = sdig[p];
       const uint4* q = reinterpret_cast<const uint4*>(&stage[p]);
-      uint4* o = reinterpret_cast<uint4*>(aout + gbase[dd] + (p - tstart[dd]));
+      const uint64_t g = (uint64_t)gbase[dd] + (p - tstart[dd]);
       const uint4 x0 = q[0], x1 = q[1];
-      o[0] = x0;
-      o[1] = x1;
+      if (dnext)
+        dnext[g] = (uint8_t)(mix64(((uint64_t)x0.y << 32) | x0.x) >> (shift + 8));
+      if constexpr (SOA_OUT) {  // the last pass writes the grouped columns
+        sout.h[g] = ((uint64_t)x0.y << 32) | x0.x;
+        sout.sid[g] = ((uint64_t)x0.w << 32) | x0.z;
+        sout.pid[g] = ((uint64_t)x1.y << 32) | x1.x;
+        sout.sf[g] = x1.z;
+        sout.dur[g] = x1.w;
+      } else {
+        uint4* o = reinterpret_cast<uint4*>(aout + g);
+        o[0] = x0;
+        o[1] = x1;
+      }
     }
   }
 }
 
-// ---- copy to SoA columns + list key changes inside buckets ----------------
-__global__ __launch_bounds__(256) void group_copy_kernel(const GRec* __restrict__ a, uint64_t n,
-                                                         int top_shift, SoaOut out,
-                                                         unsigned long long* __restrict__ list,
-                                                         uint64_t list_cap,
-                                                         unsigned long long* __restrict__ cnt) {
-  const int lane = threadIdx.x & (kWv - 1);
-  const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWv;
-  const uint64_t nwaves = (uint64_t)gridDim.x * 256 / kWv;
-  for (uint64_t b = wave * kWv; b < n; b += nwaves * kWv) {
-    const uint64_t i = b + lane;
-    const bool v = i < n;
-    GRec r = v ? a[i] : GRec{0, 0, 0, 0, 0};
-    const uint64_t k = mix64(r.h);
-    uint64_t kp = __shfl_up(k, 1);
-    if (lane == 0) kp = (i > 0 && v) ? mix64(a[i - 1].h) : k;
-    const bool change = v && i > 0 && k != kp && (k >> top_shift) == (kp >> top_shift);
-    const uint64_t bal = __ballot(change);
-    if (bal) {
-      unsigned long long at = 0;
-      if (lane == 0) at = atomicAdd(cnt, (unsigned long long)__popcll(bal));
-      at = __shfl(at, 0);
-      const uint64_t pos = at + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
-      if (change && pos < list_cap) list[pos] = i;
+// ---- key changes inside buckets (LIST) / trace_ptr (!LIST) ----------------
+// One pass over the grouped hashes in 4096-span tiles (tile ids from a
+// ticket, so a tile only waits on running predecessors): row j of a tile is
+// 256 consecutive spans, one per thread (coalesced loads; the predecessor of
+// a lane's span from its neighbour lane, across waves through LDS).  Events:
+// LIST — a key that differs from its predecessor's while their top bits
+// agree (a bucket holding several traces, sorted by group_fix_kernel);
+// !LIST — a trace start.  Events are compacted in position order (ballot
+// ranks, a scan over the tile's 64 (row, wave) counts, decoupled look-back
+// over tiles; no same-address atomics) into `out` (list / trace_ptr); the
+// total lands in *total (and closes trace_ptr).
+template <bool LIST>
+__global__ __launch_bounds__(kTThreads) void group_scan_kernel(
+    const uint64_t* __restrict__ h, uint64_t n, int top_shift, uint64_t* __restrict__ out,
+    uint64_t out_cap, uint64_t* __restrict__ state, uint32_t epoch,
+    unsigned long long* __restrict__ ticket, unsigned long long* __restrict__ total,
+    unsigned long long* __restrict__ err) {
+  constexpr int kW = kTThreads / kWv;  // waves per block
+  __shared__ uint64_t s_last[kTPer][kW];
+  __shared__ uint32_t s_cnt[kTPer * kW];
+  __shared__ unsigned long long s_tile, s_excl;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1ull);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t ntiles = (n + kTTile - 1) / kTTile;
+  const uint64_t t0 = tile * kTTile;
+  uint64_t x[kTPer];
+#pragma unroll
+  for (int j = 0; j < kTPer; ++j) {
+    const uint64_t p = t0 + (uint64_t)(j * kTThreads + tid);
+    x[j] = p < n ? h[p] : 0ull;
+  }
+  const uint64_t before = (tid == 0 && t0 > 0) ? h[t0 - 1] : ~0ull;
+  if (lane == kWv - 1) {
+#pragma unroll
+    for (int j = 0; j < kTPer; ++j) s_last[j][w] = x[j];
+  }
+  __syncthreads();
+  uint32_t ev = 0, below[kTPer];
+#pragma unroll
+  for (int j = 0; j < kTPer; ++j) {
+    const uint64_t p = t0 + (uint64_t)(j * kTThreads + tid);
+    uint64_t prev = __shfl_up(x[j], 1);
+    if (lane == 0) prev = w > 0 ? s_last[j][w - 1] : (j > 0 ? s_last[j - 1][kW - 1] : before);
+    bool e = false;
+    if (p < n) {
+      if constexpr (LIST)
+        e = p > 0 && x[j] != prev && (mix64(x[j]) >> top_shift) == (mix64(prev) >> top_shift);
+      else
+        e = p == 0 || x[j] != prev;
     }
-    if (v) {
-      out.h[i] = r.h;
-      out.sid[i] = r.sid;
-      out.pid[i] = r.pid;
-      out.sf[i] = r.sf;
-      out.dur[i] = r.dur;
+    const uint64_t b = __ballot(e);
+    below[j] = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    ev |= (e ? 1u : 0u) << j;
+    if (lane == 0) s_cnt[j * kW + w] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  if (w == 0) {  // exclusive scan of the 64 (row, wave) counts in position order
+    const uint32_t c = s_cnt[lane];
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < kWv; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    s_cnt[lane] = inc - c;
+    if (lane == kWv - 1) {
+      const uint64_t tot = inc;
+      uint64_t* st = state + tile;
+      uint64_t excl = 0;
+      if (tile == 0) {
+        publish(st, pack_state(epoch, 2u, tot));
+      } else {
+        publish(st, pack_state(epoch, 1u, tot));
+        excl = look_back(state, 1, tile, 0u, epoch, err);
+        publish(st, pack_state(epoch, 2u, excl + tot));
+      }
+      s_excl = excl;
+      if (tile == ntiles - 1) {
+        *total = excl + tot;
+        if (!LIST) out[excl + tot] = n;  // closes trace_ptr
+      }
     }
   }
+  __syncthreads();
+  const uint64_t ex = s_excl;
+#pragma unroll
+  for (int j = 0; j < kTPer; ++j)
+    if ((ev >> j) & 1u) {
+      const uint64_t idx = ex + s_cnt[j * kW + w] + below[j];
+      if (!LIST || idx < out_cap) out[idx] = t0 + (uint64_t)(j * kTThreads + tid);
+    }
 }
 
-// ---- one wave per mixed bucket: sort it by (k, arrival) in LDS ------------
+// ---- one wave per mixed bucket: sort it by (k, arrival) ------------------
+// Reads the grouped columns (not written here) and writes the bucket's
+// records in (k, arrival) order to the same rows of a scratch SoA, listing
+// the bucket as owned[e] = start << 11 | size for group_fixback_kernel
+// (0: entry e is not its bucket's first key change; its owner sorts it).
 __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
-    const GRec* __restrict__ a, uint64_t n, int top_shift, SoaOut out,
-    const unsigned long long* __restrict__ list, uint64_t list_cap,
-    const unsigned long long* __restrict__ cnt, unsigned long long* __restrict__ over) {
+    SoaOut a, uint64_t n, int top_shift, SoaOut out, const unsigned long long* __restrict__ list,
+    uint64_t list_cap, const unsigned long long* __restrict__ cnt,
+    unsigned long long* __restrict__ over, unsigned long long* __restrict__ owned) {
   __shared__ uint64_t lk[kFixWaves][kFixCap];
   const int lane = threadIdx.x & (kWv - 1), w = threadIdx.x / kWv;
   uint64_t m_list = *cnt;
@@ -364,7 +501,8 @@ __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
   for (uint64_t e = (uint64_t)blockIdx.x * kFixWaves + w; e < m_list;
        e += (uint64_t)gridDim.x * kFixWaves) {
     const uint64_t i = list[e];
-    const uint64_t ki = mix64(a[i].h), kprev = mix64(a[i - 1].h);
+    if (lane == 0) owned[e] = 0ull;  // set below when this entry owns its bucket
+    const uint64_t ki = mix64(a.h[i]), kprev = mix64(a.h[i - 1]);
     const uint64_t top = ki >> top_shift;
     // bucket start: walk back from i - 1; this entry owns the bucket only if
     // it is the bucket's first key change (everything before it = kprev)
@@ -373,7 +511,7 @@ __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
     for (uint64_t s0 = 0;; s0 += kWv) {
       const uint64_t off = s0 + lane + 1;  // position i - off
       const bool valid = off <= i;
-      const uint64_t kj = valid ? mix64(a[i - off].h) : 0;
+      const uint64_t kj = valid ? mix64(a.h[i - off]) : 0;
       const bool same_top = valid && (kj >> top_shift) == top;
       const uint64_t end_m = __ballot(!same_top);
       const uint64_t bad_m = __ballot(same_top && kj != kprev);
@@ -392,7 +530,7 @@ __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
     uint64_t be = n;
     for (uint64_t j0 = i + 1; j0 < n; j0 += kWv) {
       const uint64_t j = j0 + lane;
-      const bool same_top = j < n && (mix64(a[j].h) >> top_shift) == top;
+      const bool same_top = j < n && (mix64(a.h[j]) >> top_shift) == top;
       const uint64_t end_m = __ballot(!same_top);
       if (end_m) {
         be = j0 + (uint64_t)(__ffsll((long long)end_m) - 1);
@@ -404,7 +542,7 @@ __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
       if (lane == 0) atomicAdd(over, 1ull);
       continue;
     }
-    for (uint32_t q = lane; q < m; q += kWv) keys[q] = mix64(a[bs + q].h);
+    for (uint32_t q = lane; q < m; q += kWv) keys[q] = mix64(a.h[bs + q]);
     wave_sync();
     for (uint32_t q0 = 0; q0 < m; q0 += kWv) {
       const uint32_t q = q0 + lane;
@@ -416,77 +554,37 @@ __global__ __launch_bounds__(kFixWaves * kWv) void group_fix_kernel(
         rank += (kt < kq || (kt == kq && t < q)) ? 1u : 0u;
       }
       if (act) {
-        const GRec r = a[bs + q];
-        const uint64_t p = bs + rank;
-        out.h[p] = r.h;
-        out.sid[p] = r.sid;
-        out.pid[p] = r.pid;
-        out.sf[p] = r.sf;
-        out.dur[p] = r.dur;
+        const uint64_t src = bs + q, p = bs + rank;
+        out.h[p] = a.h[src];
+        out.sid[p] = a.sid[src];
+        out.pid[p] = a.pid[src];
+        out.sf[p] = a.sf[src];
+        out.dur[p] = a.dur[src];
       }
     }
+    if (lane == 0) owned[e] = (bs << 11) | m;
     wave_sync();
   }
 }
 
-// ---- trace_ptr from the grouped hashes --------------------------------------
-__global__ __launch_bounds__(kTThreads) void group_tptr_kernel(
-    const uint64_t* __restrict__ h, uint64_t n, uint64_t* __restrict__ tptr,
-    uint64_t* __restrict__ state, uint32_t epoch, unsigned long long* __restrict__ ticket,
-    unsigned long long* __restrict__ n_traces, unsigned long long* __restrict__ err) {
-  __shared__ unsigned long long s_tile, s_excl;
-  __shared__ uint32_t wtot[kTThreads / kWv];
-  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1ull);
-  __syncthreads();
-  const uint64_t tile = s_tile;
-  const uint64_t p0 = tile * kTTile + (uint64_t)tid * kTPer;
-  uint32_t starts = 0;
-  uint64_t prev = p0 > 0 && p0 - 1 < n ? h[p0 - 1] : ~0ull;
-#pragma unroll
-  for (int j = 0; j < kTPer; ++j) {
-    const uint64_t p = p0 + j;
-    if (p < n) {
-      const uint64_t x = h[p];
-      if (p == 0 || x != prev) starts |= 1u << j;
-      prev = x;
+// ---- sorted mixed buckets back into the grouped columns --------------------
+__global__ __launch_bounds__(256) void group_fixback_kernel(
+    SoaOut cols, SoaOut sorted, const unsigned long long* __restrict__ owned, uint64_t list_cap,
+    const unsigned long long* __restrict__ cnt) {
+  const int lane = threadIdx.x & (kWv - 1);
+  const uint64_t nb = *cnt < list_cap ? *cnt : list_cap;
+  for (uint64_t e = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWv; e < nb;
+       e += (uint64_t)gridDim.x * 256 / kWv) {
+    const uint64_t bs = owned[e] >> 11, m = owned[e] & 2047u;  // m = 0: not an owner
+    for (uint64_t q = lane; q < m; q += kWv) {
+      const uint64_t p = bs + q;
+      cols.h[p] = sorted.h[p];
+      cols.sid[p] = sorted.sid[p];
+      cols.pid[p] = sorted.pid[p];
+      cols.sf[p] = sorted.sf[p];
+      cols.dur[p] = sorted.dur[p];
     }
   }
-  const uint32_t c = (uint32_t)__popc(starts);
-  uint32_t inc = c;
-#pragma unroll
-  for (int o = 1; o < kWv; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o);
-    if (lane >= o) inc += y;
-  }
-  if (lane == kWv - 1) wtot[w] = inc;
-  __syncthreads();
-  uint32_t wadd = 0, tot = 0;
-  for (int ww = 0; ww < kTThreads / kWv; ++ww) {
-    if (ww < w) wadd += wtot[ww];
-    tot += wtot[ww];
-  }
-  if (tid == 0) {
-    uint64_t* st = state + tile;
-    uint64_t excl = 0;
-    if (tile == 0) {
-      publish(st, pack_state(epoch, 2u, tot));
-    } else {
-      publish(st, pack_state(epoch, 1u, tot));
-      excl = look_back(state, 1, tile, 0u, epoch, err);
-      publish(st, pack_state(epoch, 2u, excl + tot));
-    }
-    s_excl = excl;
-    if ((tile + 1) * kTTile >= n) {  // the last tile closes trace_ptr
-      *n_traces = excl + tot;
-      tptr[excl + tot] = n;
-    }
-  }
-  __syncthreads();
-  uint64_t idx = s_excl + wadd + inc - c;
-#pragma unroll
-  for (int j = 0; j < kTPer; ++j)
-    if ((starts >> j) & 1u) tptr[idx++] = p0 + j;
 }
 
 // ---- synthetic arrival orders (bench / tests; not a product path) --------
@@ -567,6 +665,10 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ok = ok && hipMalloc(&ws->state, ws->state_words * 8) == hipSuccess;
   ok = ok && hipMalloc(&ws->misc, kMiscWords * 8) == hipSuccess;
   ok = ok && hipMalloc(&ws->list, ws->list_cap * 8) == hipSuccess;
+  ok = ok && hipMalloc(&ws->owned, ws->list_cap * 8) == hipSuccess;
+  ok = ok && hipMalloc(&ws->tcnt, tiles * kDig * 4) == hipSuccess;
+  ok = ok && hipMalloc(&ws->bsum, (tiles / kTScanRows + 1) * kDig * 4) == hipSuccess;
+  ok = ok && hipMalloc(&ws->dig, cap + 16) == hipSuccess;
   ok = ok && hipHostMalloc(reinterpret_cast<void**>(&ws->h_misc), kMiscWords * 8,
                            hipHostMallocDefault) == hipSuccess;
   if (!ok) {
@@ -600,6 +702,11 @@ struct GroupResult {
 
 int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
   const uint64_t n = in->n_spans;
+  if (n > 0xFFFFFFFFull - kSTile) {  // u32 run starts (the workspace alone would be > 300 GB)
+    set_error(ctx, "trace grouping of %llu spans: at most 2^32 - %d per call",
+              (unsigned long long)n, kSTile);
+    return ANOMOD_EINVAL;
+  }
   if (int rc = ensure_group_ws(ctx, n)) return rc;
   GroupWs* ws = ctx->group_ws;
   int P = 1;
@@ -609,46 +716,65 @@ int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
   for (;; ++P) {
     ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc, 0, kMiscWords * 8, ctx->stream));
     const int shift0 = 64 - 8 * P;
-    GRec* src = nullptr;
-    GRec* dst = ws->aos[0];
+    // The last pass writes the grouped SoA columns into the buffer it would
+    // have written records to; the other buffer (the last pass's input) is
+    // the scratch group_fix_kernel sorts mixed buckets into.
+    const uint64_t cap = ws->cap;
+    auto soa_of = [cap](GRec* buf) {
+      char* ob = reinterpret_cast<char*>(buf);
+      return SoaOut{reinterpret_cast<uint64_t*>(ob), reinterpret_cast<uint64_t*>(ob + 8 * cap),
+                    reinterpret_cast<uint64_t*>(ob + 16 * cap),
+                    reinterpret_cast<uint32_t*>(ob + 24 * cap),
+                    reinterpret_cast<uint32_t*>(ob + 28 * cap)};
+    };
+    const SoaOut cols = soa_of(ws->aos[(P - 1) & 1]);
+    const SoaOut scratch = soa_of(ws->aos[P & 1]);
     if (n > 0) {
-      hipLaunchKernelGGL(group_hist_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
-                         in->trace_hash, n, P, shift0, ws->misc + kMiscHist);
-      ANOMOD_HIP(ctx, hipGetLastError());
+      const uint64_t nb = (tiles + kTScanRows - 1) / kTScanRows;
+      const GRec* src = nullptr;
       for (int p = 0; p < P; ++p) {
-        dst = ws->aos[p & 1];
-        const uint32_t ep = next_epoch(ctx);
-        auto fn = p == 0 ? group_scatter_kernel<true> : group_scatter_kernel<false>;
+        GRec* dst = ws->aos[p & 1];
+        const int shift = shift0 + 8 * p;
+        if (p == 0)
+          hipLaunchKernelGGL(group_tcount_kernel<true>, dim3((unsigned)tiles), dim3(256), 0,
+                             ctx->stream, in->trace_hash, nullptr, n, shift, ws->tcnt);
+        else
+          hipLaunchKernelGGL(group_tcount_kernel<false>, dim3((unsigned)tiles), dim3(256), 0,
+                             ctx->stream, nullptr, ws->dig, n, shift, ws->tcnt);
+        hipLaunchKernelGGL(group_tscan_up_kernel, dim3((unsigned)nb), dim3(kDig), 0, ctx->stream,
+                           ws->tcnt, tiles, ws->bsum);
+        hipLaunchKernelGGL(group_tscan_top_kernel, dim3(1), dim3(kDig), 0, ctx->stream, ws->bsum,
+                           nb);
+        hipLaunchKernelGGL(group_tscan_down_kernel, dim3((unsigned)nb), dim3(kDig), 0,
+                           ctx->stream, ws->tcnt, tiles, ws->bsum);
+        auto fn = p == 0 ? (p == P - 1 ? group_scatter_kernel<true, true>
+                                       : group_scatter_kernel<true, false>)
+                         : (p == P - 1 ? group_scatter_kernel<false, true>
+                                       : group_scatter_kernel<false, false>);
         hipLaunchKernelGGL(fn, dim3((unsigned)tiles), dim3(kSThreads), 0, ctx->stream, sin, src,
-                           dst, n, shift0 + 8 * p, ws->misc + kMiscHist + p * kDig, ws->state, ep,
-                           ws->misc + kMiscTicket + p, ws->misc + kMiscErr);
+                           dst, cols, n, shift, ws->tcnt, p == P - 1 ? nullptr : ws->dig);
         ANOMOD_HIP(ctx, hipGetLastError());
         src = dst;
       }
-    }
-    // SoA output carved from the other record buffer
-    char* ob = reinterpret_cast<char*>(ws->aos[P & 1]);
-    const uint64_t cap = ws->cap;
-    SoaOut cols{reinterpret_cast<uint64_t*>(ob), reinterpret_cast<uint64_t*>(ob + 8 * cap),
-                reinterpret_cast<uint64_t*>(ob + 16 * cap), reinterpret_cast<uint32_t*>(ob + 24 * cap),
-                reinterpret_cast<uint32_t*>(ob + 28 * cap)};
-    if (n > 0) {
       const int top_shift = 64 - 8 * P;  // 0 at P = 8: every bucket is one key
-      const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256,
-                                                         (uint64_t)ctx->num_cus * 16);
-      hipLaunchKernelGGL(group_copy_kernel, dim3(grid), dim3(256), 0, ctx->stream, src, n,
-                         top_shift, cols, ws->list, ws->list_cap,
-                         ws->misc + kMiscListCnt);
+      const unsigned scan_grid = (unsigned)((n + kTTile - 1) / kTTile);
+      uint32_t ep = next_epoch(ctx);
+      hipLaunchKernelGGL(group_scan_kernel<true>, dim3(scan_grid), dim3(kTThreads), 0,
+                         ctx->stream, cols.h, n, top_shift, reinterpret_cast<uint64_t*>(ws->list),
+                         ws->list_cap, ws->state, ep, ws->misc + kMiscTicket,
+                         ws->misc + kMiscListCnt, ws->misc + kMiscErr);
       ANOMOD_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(group_fix_kernel, dim3(ctx->num_cus * 4), dim3(kFixWaves * kWv), 0,
-                         ctx->stream, src, n, top_shift, cols, ws->list, ws->list_cap,
-                         ws->misc + kMiscListCnt, ws->misc + kMiscOver);
+                         ctx->stream, cols, n, top_shift, scratch, ws->list, ws->list_cap,
+                         ws->misc + kMiscListCnt, ws->misc + kMiscOver, ws->owned);
       ANOMOD_HIP(ctx, hipGetLastError());
-      const uint32_t ep = next_epoch(ctx);
-      hipLaunchKernelGGL(group_tptr_kernel, dim3((unsigned)((n + kTTile - 1) / kTTile)),
-                         dim3(kTThreads), 0, ctx->stream, cols.h, n, ws->tptr, ws->state, ep,
-                         ws->misc + kMiscTicket + kMaxPasses, ws->misc + kMiscTraces,
-                         ws->misc + kMiscErr);
+      hipLaunchKernelGGL(group_fixback_kernel, dim3(ctx->num_cus * 4), dim3(256), 0, ctx->stream,
+                         cols, scratch, ws->owned, ws->list_cap, ws->misc + kMiscListCnt);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      ep = next_epoch(ctx);
+      hipLaunchKernelGGL(group_scan_kernel<false>, dim3(scan_grid), dim3(kTThreads), 0,
+                         ctx->stream, cols.h, n, top_shift, ws->tptr, n + 1, ws->state, ep,
+                         ws->misc + kMiscTicket + 1, ws->misc + kMiscTraces, ws->misc + kMiscErr);
       ANOMOD_HIP(ctx, hipGetLastError());
     } else {
       ANOMOD_HIP(ctx, hipMemsetAsync(ws->tptr, 0, 8, ctx->stream));
@@ -694,7 +820,8 @@ void free_group_ws(anomod_ctx* ctx) {
   GroupWs* ws = ctx->group_ws;
   if (!ws) return;
   (void)hipStreamSynchronize(ctx->stream);
-  void* p[] = {ws->aos[0], ws->aos[1], ws->tptr, ws->state, ws->misc, ws->list};
+  void* p[] = {ws->aos[0], ws->aos[1], ws->tptr, ws->state, ws->misc, ws->list, ws->owned,
+               ws->tcnt, ws->bsum, ws->dig};
   for (void* q : p)
     if (q) (void)hipFree(q);
   if (ws->h_misc) (void)hipHostFree(ws->h_misc);

@@ -251,10 +251,12 @@ def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
         g.append(ctx.stage_ms(L.STAGE_GROUP))
         e.append(ctx.stage_ms(L.STAGE_EDGE_AGG))
     n, P = inter.n_spans, group_passes(inter.n_spans)
-    # bytes the grouping moves: trace_hash read by the histogram pass, each
-    # radix pass reads and writes 32-B records, the copy reads records and
-    # writes the 32-B SoA columns, trace_ptr reads the hashes + writes 8 B/trace
-    gbytes = 8 * n + 64 * P * n + 64 * n + 8 * n + 8 * n_traces
+    # bytes the grouping moves (csrc/group.hip): the first pass's tile counts
+    # read trace_hash, later passes' the 1-B digits the previous pass wrote
+    # (written + read: 2 B); each radix pass reads and writes 32 B (records,
+    # the last one the SoA columns); the bucket-list and trace_ptr scans read
+    # the grouped hashes; trace_ptr writes 8 B/trace
+    gbytes = 8 * n + 2 * (P - 1) * n + 64 * P * n + 16 * n + 8 * n_traces
     g_ms, e_ms = float(np.mean(g)), float(np.mean(e))
     return {"what": "SN spans of every 4096 consecutive traces interleaved (ES start_time "
                     "order); step = device grouping + edge aggregation",
