@@ -69,7 +69,8 @@ static_assert(kPairSlots * 8 == kHtBytes && kCmpSlots * 4 == kHtBytes, "64 KiB t
 constexpr uint32_t kLdsEdges = ANOMOD_LDS_EDGES;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
-// 2 = no histogram, 4 = no parent lookup, 16 = stream the columns only.
+// 2 = no histogram, 4 = no parent lookup, 16 = stream the columns only,
+// 32 = compact histogram adds without the wrap check (non-returning).
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
 #endif
@@ -352,7 +353,7 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
                       (y.y == 0u) | (y.z == 0u) | (y.w == 0u);
     stat_add<ST>(smem, edge, d, fl, tab, pk);
     if (hit) {
-      ht_wrap(old, key, tab.kb, tab.hist);
+      if (!(ANOMOD_ABL & 32)) ht_wrap(old, key, tab.kb, tab.hist);
     } else if (room) {
       ht_insert_cmp(hk, key, s0, s1, tab.kb, tab.hist);
     } else {
