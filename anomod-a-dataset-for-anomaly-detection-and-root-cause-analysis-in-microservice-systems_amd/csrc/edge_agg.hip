@@ -70,7 +70,8 @@ constexpr uint32_t kLdsEdges = ANOMOD_LDS_EDGES;
 constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 // Experiment-only ablations (never set in the shipped build): 1 = no stats,
 // 2 = no histogram, 4 = no parent lookup, 16 = stream the columns only,
-// 32 = compact histogram adds without the wrap check (non-returning).
+// 32 = compact histogram adds without the wrap check (non-returning), 64 =
+// compact-form spans whose two buckets are full are dropped (not counted).
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
 #endif
@@ -356,7 +357,7 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
       if (!(ANOMOD_ABL & 32)) ht_wrap(old, key, tab.kb, tab.hist);
     } else if (room) {
       ht_insert_cmp(hk, key, s0, s1, tab.kb, tab.hist);
-    } else {
+    } else if (!(ANOMOD_ABL & 64)) {
       atomicAdd(&tab.hist[key - 1u], 1ull);
     }
   }
