@@ -147,7 +147,10 @@ __global__ __launch_bounds__(64) void ewma_z_kernel(const float* __restrict__ X,
 // per load block, two blocks in flight; blocks wholly inside T run without
 // per-step bounds checks.
 constexpr int kTile = 16;
-constexpr int kZtTiles = 4;
+#ifndef ANOMOD_ZT_TILES
+#define ANOMOD_ZT_TILES 4
+#endif
+constexpr int kZtTiles = ANOMOD_ZT_TILES;  // tiles per load block (two blocks in flight)
 constexpr int kPadTiles = 2 * kZtTiles;  // slack tiles past ceil(T/16) read by the prefetch
 
 template <int kTiles>
