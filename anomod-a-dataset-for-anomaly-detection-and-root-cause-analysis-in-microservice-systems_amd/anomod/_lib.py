@@ -180,6 +180,7 @@ _SIGS = {
     "anomod_decoded_free": (_i32, [_vp]),
     "anomod_hash64": (_u64, [C.c_char_p, _u64]),
     "anomod_decode_metric_long_csv": (_i32, [C.c_char_p, _u64, _P(_vp)]),
+    "anomod_decode_metric_long_csv_file": (_i32, [C.c_char_p, _P(_vp)]),
     "anomod_decode_prometheus_csvs": (_i32, [_P(C.c_char_p), _P(_u64), _P(C.c_char_p), _u32,
                                              _P(_vp)]),
     "anomod_metrics_info": (_i32, [_vp, _P(_u64), _P(_u64)]),

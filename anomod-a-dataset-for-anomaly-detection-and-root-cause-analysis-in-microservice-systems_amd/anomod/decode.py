@@ -17,6 +17,8 @@ import csv
 import ctypes as C
 import json
 import math
+import mmap
+import os
 import re
 from dataclasses import dataclass
 from datetime import datetime
@@ -385,13 +387,35 @@ def _metrics_from_handle(h) -> MetricMatrix:
     return MetricMatrix(X, ts, series)
 
 
+def map_file(path):
+    """A file's bytes for the native decoders without a copy into Python: a
+    private, pre-faulted (MAP_POPULATE) read-only-in-practice mapping, as a
+    ctypes char array (the mapping lives as long as the array).  Empty files
+    give b''."""
+    with open(path, "rb") as fh:
+        n = os.fstat(fh.fileno()).st_size
+        if n == 0:
+            return b""
+        mm = mmap.mmap(fh.fileno(), n, flags=mmap.MAP_PRIVATE | getattr(mmap, "MAP_POPULATE", 0),
+                       prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    return (C.c_char * n).from_buffer(mm)
+
+
 def decode_metric_long_csv_native(path_or_bytes) -> MetricMatrix:
     """decode_metric_long_csv in libanomod (csrc/metrics_decode.cpp): the
-    same matrix, without a Python dict per row."""
-    data = (path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray))
-            else Path(path_or_bytes).read_bytes())
+    same matrix, without a Python dict per row.  A path is mapped, not read
+    (anomod_decode_metric_long_csv_file)."""
+    if isinstance(path_or_bytes, bytearray):
+        data = bytes(path_or_bytes)
+    elif isinstance(path_or_bytes, bytes):
+        data = path_or_bytes
+    else:  # mapped by the library: its parser threads fault their own pieces
+        h = C.c_void_p()
+        L.check(L.lib().anomod_decode_metric_long_csv_file(os.fsencode(path_or_bytes),
+                                                           C.byref(h)))
+        return _metrics_from_handle(h)
     h = C.c_void_p()
-    L.check(L.lib().anomod_decode_metric_long_csv(bytes(data), len(data), C.byref(h)))
+    L.check(L.lib().anomod_decode_metric_long_csv(data, len(data), C.byref(h)))
     return _metrics_from_handle(h)
 
 
@@ -452,13 +476,13 @@ def load_trace_file(path, services: list[str] | None = None) -> SpanSet:
     and collector payloads ({"metadata": ..., "traces": ...}) go through the
     native decoder; anything else (raw GraphQL span lists) through the
     Python decoders."""
-    data = Path(path).read_bytes()
-    key = _first_key(data)
+    data = map_file(path)
+    key = _first_key(data[:4096])
     if key == "data":
         return decode_native(data, "jaeger", services)
     if key in ("metadata", "traces"):
         return decode_native(data, "skywalking", services)
-    doc = json.loads(data)
+    doc = json.loads(data[:])
     if isinstance(doc, dict) and "traces" in doc:
         return decode_skywalking_payload(doc, services)
     if isinstance(doc, dict) and "data" in doc:

@@ -31,6 +31,10 @@
 #include <ctime>
 #include <deque>
 #include <string>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <string_view>
 #include <thread>
 #include <unordered_map>
@@ -258,11 +262,17 @@ bool iso_timestamp(std::string_view s, double& out) {
   return true;
 }
 
-struct Sample {
+struct Sample {  // kept in row order: the first occurrence of a cell wins
   double t;
   float v;
   uint32_t series;
-  uint64_t order;  // row order: first occurrence wins
+};
+
+// A run of samples in row order whose series ids go through `map` (nullptr:
+// the builder's own ids).
+struct SampleRun {
+  const std::vector<Sample>* samples;
+  const std::vector<uint32_t>* map;
 };
 
 struct Builder {
@@ -270,6 +280,9 @@ struct Builder {
   std::vector<std::string> keys;                      // by series id (the fast path's keys)
   std::vector<anomod_metrics::Series> series;
   std::vector<Sample> samples;
+  std::vector<SampleRun> runs;  // set by the threaded decode: the pieces' samples, in file order
+  std::deque<std::vector<Sample>> part_samples;  // (deque: stable addresses for runs)
+  std::deque<std::vector<uint32_t>> part_maps;
   std::string key;
 
   // Series id of a key already serialised as name \0 k1 \0 v1 ...; `make`
@@ -315,15 +328,27 @@ struct Builder {
     out->series.reserve(series.size());
     for (uint32_t i : order) out->series.push_back(std::move(series[i]));
     // distinct timestamps: a hash map to a provisional column, then sorted
+    if (runs.empty()) runs.push_back({&samples, nullptr});
+    size_t n_samples = 0;
+    for (const SampleRun& r : runs) n_samples += r.samples->size();
     std::unordered_map<double, uint32_t> col_of;
     col_of.reserve(1024);
-    std::vector<uint32_t> col(samples.size());
+    std::vector<uint32_t> col(n_samples);
     double last = std::nan("");
     uint32_t last_c = 0;
-    for (size_t i = 0; i < samples.size(); ++i) {
-      const double t = samples[i].t;
+    size_t i = 0;
+    for (const SampleRun& r : runs)
+    for (const Sample& sm : *r.samples) {
+      const double t = sm.t;
       if (t == last) {  // (NaN never matches: timestamps are never NaN)
-        col[i] = last_c;
+        col[i++] = last_c;
+        continue;
+      }
+      // series-major files repeat the first series' timestamps in order: the
+      // column after the previous row's is the usual answer (no hash lookup)
+      if (last_c + 1 < out->ts.size() && out->ts[last_c + 1] == t) {
+        last = t;
+        col[i++] = ++last_c;
         continue;
       }
       auto it = col_of.find(t);
@@ -332,7 +357,7 @@ struct Builder {
         out->ts.push_back(t);
       }
       last = t;
-      last_c = col[i] = it->second;
+      last_c = col[i++] = it->second;
     }
     std::vector<uint32_t> ord(out->ts.size());
     for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
@@ -348,12 +373,15 @@ struct Builder {
     out->X.assign(T * S, std::nanf(""));
     // first occurrence per (series, t): later rows of the same cell skipped
     std::vector<uint8_t> seen(T * S, 0);
-    for (size_t i = 0; i < samples.size(); ++i) {  // samples are in row order
-      const size_t cell = (size_t)crank[col[i]] * S + rank[samples[i].series];
-      if (seen[cell]) continue;
-      seen[cell] = 1;
-      out->X[cell] = samples[i].v;
-    }
+    i = 0;
+    for (const SampleRun& r : runs)  // samples in row order
+      for (const Sample& sm : *r.samples) {
+        const uint32_t sid = r.map ? (*r.map)[sm.series] : sm.series;
+        const size_t cell = (size_t)crank[col[i++]] * S + rank[sid];
+        if (seen[cell]) continue;
+        seen[cell] = 1;
+        out->X[cell] = sm.v;
+      }
     return out;
   }
 };
@@ -425,7 +453,7 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
       }
       return anomod_metrics::Series{std::string(nm), labels};
     });
-    b.samples.push_back({t, (float)v, s, b.samples.size()});
+    b.samples.push_back({t, (float)v, s});
   }
   return ANOMOD_OK;
 }
@@ -464,7 +492,9 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
   // Large files without any quote character (every record ends at a newline)
   // parse in newline-aligned pieces on several threads; the pieces' series
   // and samples are merged in file order, so the result is the one-thread one.
-  if (threads > 1 && end - body > (8 << 20) && !memchr(body, '"', (size_t)(end - body))) {
+  // (every piece checks itself for quotes in parallel; with one anywhere the
+  // parallel result is dropped and the file parses on one thread)
+  if (threads > 1 && end - body > (8 << 20)) {
     std::vector<const char*> cut{body};
     for (int t = 1; t < threads; ++t) {
       const char* c = body + (size_t)(end - body) * (size_t)t / (size_t)threads;
@@ -477,23 +507,29 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
     const size_t np = cut.size() - 1;
     std::vector<Builder> part(np);
     std::vector<int> rc(np, ANOMOD_OK);
+    std::vector<uint8_t> quoted(np, 0);
     std::vector<std::thread> th;
     for (size_t k = 0; k < np; ++k)
-      th.emplace_back([&, k] { rc[k] = decode_long_rows(H, cut[k], cut[k + 1], part[k], 0); });
+      th.emplace_back([&, k] {
+        quoted[k] = memchr(cut[k], '"', (size_t)(cut[k + 1] - cut[k])) != nullptr;
+        if (!quoted[k]) rc[k] = decode_long_rows(H, cut[k], cut[k + 1], part[k], 0);
+      });
     for (auto& x : th) x.join();
+    bool any_quote = false;
+    for (size_t k = 0; k < np; ++k) any_quote |= quoted[k] != 0;
+    if (any_quote) return decode_long_rows(H, body, end, b, 0);
     for (size_t k = 0; k < np; ++k)
       if (rc[k] != ANOMOD_OK) return rc[k];  // (row numbers in the message are per piece)
-    size_t total = 0;
-    for (const Builder& pb : part) total += pb.samples.size();
-    b.samples.reserve(total);
-    for (Builder& pb : part) {
-      std::vector<uint32_t> map(pb.series.size());
-      for (size_t s = 0; s < pb.series.size(); ++s) {
-        Builder* src = &pb;
-        map[s] = b.series_of_key(pb.keys[s], [&] { return std::move(src->series[s]); });
-      }
-      for (const Sample& sm : pb.samples)
-        b.samples.push_back({sm.t, sm.v, map[sm.series], b.samples.size()});
+    // the pieces' series into the builder (file order), their samples
+    // referenced in place, not copied
+    for (size_t k = 0; k < np; ++k) {
+      Builder& pb = part[k];
+      b.part_maps.emplace_back(pb.series.size());
+      std::vector<uint32_t>& map = b.part_maps.back();
+      for (size_t s = 0; s < pb.series.size(); ++s)
+        map[s] = b.series_of_key(pb.keys[s], [&] { return std::move(pb.series[s]); });
+      b.part_samples.push_back(std::move(pb.samples));
+      b.runs.push_back({&b.part_samples.back(), &map});
     }
     return ANOMOD_OK;
   }
@@ -534,7 +570,7 @@ int decode_prom(const char* data, uint64_t len, const std::string& stem, Builder
     }
     labels[0].second.assign(field(c_met));
     const uint32_t s = b.series_of(stem, labels);
-    b.samples.push_back({t, (float)v, s, b.samples.size()});
+    b.samples.push_back({t, (float)v, s});
   }
   return ANOMOD_OK;
 }
@@ -558,6 +594,40 @@ int anomod_decode_metric_long_csv(const char* data, uint64_t len, anomod_metrics
     return ANOMOD_ENOMEM;
   }
   return ANOMOD_OK;
+}
+
+int anomod_decode_metric_long_csv_file(const char* path, anomod_metrics** out) {
+  if (!path || !out) {
+    anomod::set_error(nullptr, "anomod_decode_metric_long_csv_file: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  *out = nullptr;
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    anomod::set_error(nullptr, "metric CSV %s: %s", path, strerror(errno));
+    return ANOMOD_EINVAL;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    anomod::set_error(nullptr, "metric CSV %s: %s", path, strerror(errno));
+    close(fd);
+    return ANOMOD_EINVAL;
+  }
+  const uint64_t len = (uint64_t)st.st_size;
+  if (len == 0) {
+    close(fd);
+    return anomod_decode_metric_long_csv(nullptr, 0, out);
+  }
+  // mapped, not read: the parser threads fault their own pieces in parallel
+  void* m = mmap(nullptr, (size_t)len, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) {
+    anomod::set_error(nullptr, "metric CSV %s: mmap: %s", path, strerror(errno));
+    return ANOMOD_EINVAL;
+  }
+  const int rc = anomod_decode_metric_long_csv(static_cast<const char*>(m), len, out);
+  munmap(m, (size_t)len);
+  return rc;
 }
 
 int anomod_decode_prometheus_csvs(const char* const* data, const uint64_t* lens,

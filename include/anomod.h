@@ -228,6 +228,9 @@ uint64_t anomod_hash64(const char* s, uint64_t len);
  * by (name, labels).  The same rules as anomod/decode.py's Python decoders. */
 typedef struct anomod_metrics anomod_metrics;
 int anomod_decode_metric_long_csv(const char* data, uint64_t len, anomod_metrics** out);
+/* the same from a file path (mapped, not read; pieces faulted in by the
+ * parser threads) */
+int anomod_decode_metric_long_csv_file(const char* path, anomod_metrics** out);
 int anomod_decode_prometheus_csvs(const char* const* data, const uint64_t* lens,
                                   const char* const* stems, uint32_t n_files,
                                   anomod_metrics** out);
