@@ -552,6 +552,13 @@ int relayout(anomod_ctx* ctx, anomod_series* ser, bool to_tiles) {
   return ANOMOD_OK;
 }
 
+// Steps per launch of the sequential tiled kernel (ANOMOD_EWMA_SEG, 0 = one
+// launch for the whole T).
+uint64_t ewma_seg_steps() {
+  const char* e = getenv("ANOMOD_EWMA_SEG");
+  return e ? strtoull(e, nullptr, 10) : 16384ull;
+}
+
 }  // namespace
 }  // namespace anomod
 
@@ -686,8 +693,21 @@ int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint3
                          ser->X, ser->T, ser->S, (double)alpha, W, U, eps, ser->Z, ser->m, ser->v,
                          ser->n);
   } else if (kern == EwmaKernel::kSeqTiles) {
-    hipLaunchKernelGGL(ewma_zt_kernel<kZtTiles>, dim3(strips), dim3(64), 0, ctx->stream, ser->X,
-                       ser->T, ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);
+    // Long T in time segments (state carried through HBM between launches,
+    // segment = a multiple of lcm(W, 64) steps so windows and dense blocks
+    // line up): one lane walks its series sequentially and the waves drift
+    // apart over a long launch; measured at S = 10^5: 4.9-5.0 TB/s for
+    // T = 32 760 against 3.7-4.6 TB/s for T = 131 040 in one launch.
+    uint64_t l = 64;
+    while (l % W) l += 64;  // lcm(W, 64)
+    const uint64_t seg_env = ewma_seg_steps();
+    const uint64_t seg = seg_env ? std::max<uint64_t>(l, seg_env / l * l) : ser->T;
+    for (uint64_t t0 = 0; t0 < ser->T; t0 += seg) {
+      const uint64_t Ts = std::min<uint64_t>(seg, ser->T - t0);
+      hipLaunchKernelGGL(ewma_zt_kernel<kZtTiles>, dim3(strips), dim3(64), 0, ctx->stream,
+                         ser->X + t0 / kTile * ser->S * kTile, Ts, ser->S, (double)alpha, W, eps,
+                         ser->Z + t0 / W * ser->S, ser->m, ser->v, ser->n);
+    }
   } else {
     hipLaunchKernelGGL(ewma_z_kernel, dim3(strips), dim3(64), 0, ctx->stream, ser->X, ser->T,
                        ser->S, (double)alpha, W, eps, ser->Z, ser->m, ser->v, ser->n);

@@ -55,6 +55,25 @@ def test_ewma_streaming_chunks_equal_one_pass(ctx, ewma_mode):
     ser.free()
 
 
+@pytest.mark.parametrize("T,S,W,seg", [(4800, 300, 60, 960), (4800, 300, 60, 2000),
+                                       (3136, 200, 7, 448), (1000, 65, 1, 64)])
+def test_ewma_time_segments_equal_one_launch(ctx, monkeypatch, T, S, W, seg):
+    """The sequential tiled kernel runs a long T as launches of a multiple of
+    lcm(W, 64) steps (ANOMOD_EWMA_SEG rounded down to one), the state carried
+    through HBM: bit-equal to one launch, with NaN runs and late starts."""
+    monkeypatch.setenv("ANOMOD_EWMA_MODE", "1")
+    rng = np.random.default_rng(T + W)
+    X = (100 + rng.standard_normal((T, S))).astype(np.float32)
+    X[: T // 3, : S // 4] = np.nan
+    X[rng.random((T, S)) < 0.05] = np.nan
+    a = 2.0 / (W + 1) if W > 1 else 0.3
+    monkeypatch.setenv("ANOMOD_EWMA_SEG", "0")
+    one = ctx.ewma_z(X, a, W)
+    monkeypatch.setenv("ANOMOD_EWMA_SEG", str(seg))
+    np.testing.assert_array_equal(ctx.ewma_z(X, a, W), one)
+    np.testing.assert_allclose(one, native.ewma_z(X, a, W), rtol=Z_RTOL, atol=Z_ATOL)
+
+
 def test_ewma_time_parallel_nan_runs_and_fresh_start(ctx, monkeypatch):
     """Leading all-NaN sub-chunks, NaN runs across sub-chunk and super-chunk
     boundaries, series that never see a sample: the fresh-start and carried
