@@ -83,9 +83,9 @@ constexpr int kSTile = kSThreads * kSPer;    // 4096 records per tile
 constexpr int kRowsPerWave = kSTile / kSWaves / kWv;  // 4
 constexpr int kDig = 256;
 constexpr int kMaxPasses = 8;
-constexpr int kTThreads = 256;               // trace_ptr workgroup
+constexpr int kTThreads = 1024;              // scan workgroup (bucket list / trace_ptr)
 constexpr int kTPer = 16;
-constexpr int kTTile = kTThreads * kTPer;    // 4096 spans
+constexpr int kTTile = kTThreads * kTPer;    // 16384 spans: fewer tiles, fewer tickets
 constexpr int kFixCap = 1024;                // records of a mixed bucket one wave sorts
 constexpr int kFixWaves = 4;
 constexpr uint64_t kValMask = (1ull << 54) - 1;
@@ -447,15 +447,26 @@ __global__ __launch_bounds__(kTThreads) void group_scan_kernel(
     if (lane == 0) s_cnt[j * kW + w] = (uint32_t)__popcll(b);
   }
   __syncthreads();
-  if (w == 0) {  // exclusive scan of the 64 (row, wave) counts in position order
-    const uint32_t c = s_cnt[lane];
-    uint32_t inc = c;
+  if (w == 0) {  // exclusive scan of the (row, wave) counts in position order
+    constexpr int kE = kTPer * kW / kWv;  // entries per lane
+    uint32_t c[kE], sum = 0;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      c[e] = s_cnt[lane * kE + e];
+      sum += c[e];
+    }
+    uint32_t inc = sum;
 #pragma unroll
     for (int o = 1; o < kWv; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o);
       if (lane >= o) inc += y;
     }
-    s_cnt[lane] = inc - c;
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      s_cnt[lane * kE + e] = run;
+      run += c[e];
+    }
     if (lane == kWv - 1) {
       const uint64_t tot = inc;
       uint64_t* st = state + tile;
