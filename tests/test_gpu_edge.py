@@ -103,6 +103,27 @@ def test_low_word_aliases(ctx, S, max_len):
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
 
 
+@pytest.mark.parametrize("S,lens", [(46, (30, 200)), (46, (1, 25)), (12, (30, 200))])
+def test_fingerprint_collisions(ctx, S, lens):
+    """The compact-histogram (TrainTicket-width) kernel scans 16-bit id
+    fingerprints of lo ^ hi: ids crafted so that EVERY id of the set — orphan
+    references included — shares one fingerprint (lo ^ hi constant), with
+    duplicated ids, so every candidate but the true first match is a
+    collision and the exact scan past it decides."""
+    rng = np.random.default_rng(S * 31 + lens[1])
+    sp = _random_spanset(rng, S, 3000, 0, dup=0.05,
+                         lens=rng.integers(lens[0], lens[1] + 1, 3000))
+
+    def one_fp(x):
+        hi = x >> np.uint64(32)
+        return (hi << np.uint64(32)) | (hi ^ np.uint64(0x5A5A5A5A))
+
+    sp.span_id[:] = one_fp(sp.span_id)
+    nz = sp.parent_span_id != 0
+    sp.parent_span_id[nz] = one_fp(sp.parent_span_id[nz])
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+
+
 def test_big_traces(ctx):
     rng = np.random.default_rng(7)
     parts = [_random_spanset(rng, 12, 50, 10), _random_spanset(rng, 12, 3, 3000),
