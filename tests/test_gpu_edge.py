@@ -105,11 +105,10 @@ def test_low_word_aliases(ctx, S, max_len):
 
 @pytest.mark.parametrize("S,lens", [(46, (30, 200)), (46, (1, 25)), (12, (30, 200))])
 def test_fingerprint_collisions(ctx, S, lens):
-    """The compact-histogram (TrainTicket-width) kernel scans 16-bit id
-    fingerprints of lo ^ hi: ids crafted so that EVERY id of the set — orphan
-    references included — shares one fingerprint (lo ^ hi constant), with
-    duplicated ids, so every candidate but the true first match is a
-    collision and the exact scan past it decides."""
+    """Ids crafted so that EVERY id of the set — orphan references included —
+    shares lo ^ hi (the value any fingerprint, bucket or hash scheme over the
+    ids would key on; DESIGN §7 logs the ones measured), with duplicated ids:
+    the first-match rule has to be decided on the full 64-bit ids."""
     rng = np.random.default_rng(S * 31 + lens[1])
     sp = _random_spanset(rng, S, 3000, 0, dup=0.05,
                          lens=rng.integers(lens[0], lens[1] + 1, 3000))
