@@ -591,6 +591,7 @@ constexpr uint32_t kBigSlots = 4096;  // table slots (load <= 0.5)
 constexpr int kBigPer = 8;            // spans per thread per lookup block
 constexpr int kOffBigKey = kOffWave;                          // u64 [kBigSlots], 0 = empty
 constexpr int kOffBigPos = kOffBigKey + (int)kBigSlots * 8;   // u32 [kBigSlots]
+static_assert(kBigWin % kBigThreads == 0 && kBigWin <= 65536, "window: whole rows, position << 16 | svc");
 constexpr int kBigLdsBytes = kOffBigPos + (int)kBigSlots * 4;
 static_assert(kBigLdsBytes <= 160 * 1024, "long-trace pass LDS budget");
 
@@ -604,44 +605,72 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
     const uint64_t* __restrict__ trace_ptr, uint32_t S, uint32_t E, Table tab) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[kBigLdsBytes];
-  __shared__ unsigned long long s_j;
+  __shared__ unsigned long long s_tr[3];  // ticket, first span, length of this iteration's trace
   auto* bkey = reinterpret_cast<unsigned long long*>(smem + kOffBigKey);  // 0 = empty (id 0 is never a parent ref)
-  auto* bpos = reinterpret_cast<uint32_t*>(smem + kOffBigPos);
+  auto* bval = reinterpret_cast<uint32_t*>(smem + kOffBigPos);  // (first position in window) << 16 | svc
   const int tid = threadIdx.x;
   const uint64_t nbig = tab.big[0];
   if (nbig == 0) return;
   tables_init<HT, ST>(smem, E, tid);
   for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
     bkey[k] = 0ull;
-    bpos[k] = 0xFFFFFFFFu;
+    bval[k] = 0xFFFFFFFFu;
+  }
+  // Thread 0 keeps the NEXT trace in flight (ticket, list entry, bounds),
+  // each load issued a phase after the one it depends on, so a trace's
+  // dependent latency overlaps the previous trace's work.
+  unsigned long long nj = 0, nt = 0, nlo = 0, nhi = 0;
+  if (tid == 0) {
+    nj = atomicAdd(&tab.big[1], 1ull);
+    nt = nj < nbig ? tab.big_list[nj] : 0ull;
+    nlo = nj < nbig ? trace_ptr[nt] : 0ull;
+    nhi = nj < nbig ? trace_ptr[nt + 1] : 0ull;
   }
   while (true) {
-    __syncthreads();  // table clear / s_j reuse
-    if (tid == 0) s_j = atomicAdd(&tab.big[1], 1ull);
+    __syncthreads();  // table clear / s_tr reuse
+    if (tid == 0) {
+      s_tr[0] = nj;
+      s_tr[1] = nlo;
+      s_tr[2] = nhi - nlo;
+      nj = atomicAdd(&tab.big[1], 1ull);
+    }
     __syncthreads();
-    const uint64_t j = s_j;
+    const uint64_t j = s_tr[0];
     if (j >= nbig) break;
-    const uint64_t t = tab.big_list[j];
-    const uint64_t lo = trace_ptr[t], L = trace_ptr[t + 1] - lo;
+    const uint64_t lo = s_tr[1], L = s_tr[2];
     for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kBigThreads * kBigPer) {
-      uint64_t pid[kBigPer], q[kBigPer];  // q: first position of the parent ref (~0: none yet)
+      uint64_t pid[kBigPer];
+      uint32_t sf[kBigPer], dr[kBigPer], psv[kBigPer];  // psv: parent's service (~0: none yet)
       bool need = false;
 #pragma unroll
       for (int r = 0; r < kBigPer; ++r) {
         const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
         pid[r] = i < L ? parent[lo + i] : 0ull;
-        q[r] = ~0ull;
+        sf[r] = i < L ? svcfl[lo + i] : 0u;
+        dr[r] = i < L ? dur[lo + i] : 0u;
+        psv[r] = 0xFFFFFFFFu;
         need |= pid[r] != 0ull;
       }
+      if (tid == 0 && b0 == 0 && nj < nbig) nt = tab.big_list[nj];  // next trace, phase 2
       for (uint64_t w0 = 0; w0 < L; w0 += kBigWin) {
         if (!__syncthreads_or(need)) break;  // also orders the previous clear
-        for (uint32_t k = tid; k < kBigWin && w0 + k < L; k += kBigThreads) {
-          const uint64_t id = span_id[lo + w0 + k];
-          if (id == 0ull) continue;
-          for (uint32_t sl = big_slot(id);; sl = (sl + 1u) & (kBigSlots - 1u)) {
-            const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id);
-            if (prev == 0ull || prev == id) {
-              atomicMin(&bpos[sl], k);
+        constexpr int kIns = kBigWin / kBigThreads;
+        uint64_t id[kIns];
+        uint32_t sv[kIns];
+#pragma unroll
+        for (int u = 0; u < kIns; ++u) {
+          const uint32_t k = (uint32_t)(u * kBigThreads + tid);
+          id[u] = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
+          sv[u] = w0 + k < L ? svcfl[lo + w0 + k] & 0xFFFFu : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kIns; ++u) {
+          if (id[u] == 0ull) continue;
+          const uint32_t k = (uint32_t)(u * kBigThreads + tid);
+          for (uint32_t sl = big_slot(id[u]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+            const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id[u]);
+            if (prev == 0ull || prev == id[u]) {
+              atomicMin(&bval[sl], (k << 16) | sv[u]);  // the first position wins, with its service
               break;
             }
           }
@@ -650,34 +679,37 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
         need = false;
 #pragma unroll
         for (int r = 0; r < kBigPer; ++r) {
-          if (pid[r] == 0ull || q[r] != ~0ull) continue;
+          if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
           for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
             const unsigned long long key = bkey[sl];
             if (key == pid[r]) {
-              q[r] = w0 + bpos[sl];
+              psv[r] = bval[sl] & 0xFFFFu;
               break;
             }
             if (key == 0ull) break;
           }
-          need |= q[r] == ~0ull;
+          need |= psv[r] == 0xFFFFFFFFu;
         }
         __syncthreads();
         for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
           bkey[k] = 0ull;
-          bpos[k] = 0xFFFFFFFFu;
+          bval[k] = 0xFFFFFFFFu;
         }
+      }
+      if (tid == 0 && b0 == 0 && nj < nbig) {  // next trace, phase 3
+        nlo = trace_ptr[nt];
+        nhi = trace_ptr[nt + 1];
       }
 #pragma unroll
       for (int r = 0; r < kBigPer; ++r) {
         const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
         if (i >= L) continue;
-        const uint32_t sf = svcfl[lo + i];
-        const uint32_t p = pid[r] == 0ull ? S : q[r] == ~0ull ? S + 1u : (svcfl[lo + q[r]] & 0xFFFFu);
-        const uint32_t edge = p * S + (sf & 0xFFFFu);
+        const uint32_t p = pid[r] == 0ull ? S : psv[r] == 0xFFFFFFFFu ? S + 1u : psv[r];
+        const uint32_t edge = p * S + (sf[r] & 0xFFFFu);
         if constexpr (HT == kHtKeys) {
-          tab.keys[lo + i] = ((unsigned long long)edge << 32) | dur[lo + i];
+          tab.keys[lo + i] = ((unsigned long long)edge << 32) | dr[r];
         } else {
-          record<HT, ST>(smem, edge, dur[lo + i], sf >> 16, tab);
+          record<HT, ST>(smem, edge, dr[r], sf[r] >> 16, tab);
         }
       }
     }
