@@ -668,7 +668,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   const uint64_t cap = n ? n : 1;
   const uint64_t tiles = (cap + kSTile - 1) / kSTile;
   ws->cap = cap;
-  ws->state_words = std::max<uint64_t>(tiles * kDig, (cap + kTTile - 1) / kTTile);
+  ws->state_words = (cap + kTTile - 1) / kTTile;  // look-back words of the scans
   ws->list_cap = cap / 8 + 65536;
   bool ok = hipMalloc(&ws->aos[0], cap * sizeof(GRec)) == hipSuccess;
   ok = ok && hipMalloc(&ws->aos[1], cap * sizeof(GRec)) == hipSuccess;
@@ -686,7 +686,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
     free_group_ws(ctx);
     set_error(ctx, "hipMalloc failed for the trace-grouping workspace of %llu spans "
               "(~%llu GB)", (unsigned long long)n,
-              (unsigned long long)((cap * 81ull) >> 30));
+              (unsigned long long)((cap * 76ull) >> 30));
     return ANOMOD_ENOMEM;
   }
   ANOMOD_HIP(ctx, hipMemsetAsync(ws->state, 0, ws->state_words * 8, ctx->stream));
