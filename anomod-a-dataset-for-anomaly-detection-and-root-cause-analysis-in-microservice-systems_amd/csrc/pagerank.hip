@@ -15,6 +15,7 @@
 // cooperative launch with a grid barrier per iteration and the stopping test
 // on the device.
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -126,12 +127,17 @@ __global__ __launch_bounds__(kPprThreads) void ppr_init_kernel(uint32_t N, doubl
 }
 
 // x = x0 everywhere and p /= psum in place (the same IEEE division the host
-// did before: identical bits).
-__global__ __launch_bounds__(kPprThreads) void ppr_init_norm_kernel(uint32_t N, double x0,
-                                                                    double* __restrict__ x,
-                                                                    double* __restrict__ p,
-                                                                    double psum) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+// did before: identical bits); also seeds the accumulator slots (acc[0] =
+// acc0, the rest zero) and clears the grid-barrier words, so a solve issues
+// no host->device copy or memset besides p itself.
+__global__ __launch_bounds__(kPprThreads) void ppr_init_norm_kernel(
+    uint32_t N, double x0, double* __restrict__ x, double* __restrict__ p, double psum,
+    unsigned long long* __restrict__ acc, uint32_t n_acc, unsigned long long acc0,
+    unsigned int* __restrict__ bar, uint32_t n_bar) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t i = gid; i < n_acc; i += gridDim.x * blockDim.x) acc[i] = i == 0 ? acc0 : 0ull;
+  for (uint32_t i = gid; i < n_bar; i += gridDim.x * blockDim.x) bar[i] = 0u;
+  for (uint32_t i = gid; i < N; i += gridDim.x * blockDim.x) {
     x[i] = x0;
     p[i] = p[i] / psum;
   }
@@ -589,6 +595,36 @@ int ensure_shard_x(anomod_ctx* ctx, anomod_graph* g, uint32_t G) {
   return ANOMOD_OK;
 }
 
+// Sum of a personalization vector in the one order every solve entry uses
+// (8 interleaved partial sums joined by a fixed tree: eight independent add
+// chains instead of one N long), copied to `dst` in the same pass when COPY.
+// Returns the index of the first entry that is negative or not finite, or N.
+template <bool COPY>
+uint32_t personalization_sum(const double* __restrict__ p, uint32_t N, double* __restrict__ dst,
+                             double& sum) {
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  unsigned bad = 0;
+  uint32_t i = 0;
+  for (; i + 8 <= N; i += 8)
+    for (int j = 0; j < 8; ++j) {
+      const double v = p[i + j];
+      if constexpr (COPY) dst[i + j] = v;
+      bad |= !(v >= 0.0 && v <= DBL_MAX);
+      a[j] += v;
+    }
+  for (; i < N; ++i) {
+    const double v = p[i];
+    if constexpr (COPY) dst[i] = v;
+    bad |= !(v >= 0.0 && v <= DBL_MAX);
+    a[i & 7] += v;
+  }
+  sum = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  if (!bad) return N;
+  for (uint32_t k = 0; k < N; ++k)
+    if (!(p[k] >= 0.0 && p[k] <= DBL_MAX)) return k;
+  return N;
+}
+
 }  // namespace
 }  // namespace anomod
 
@@ -711,29 +747,27 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   ANOMOD_REQUIRE(ctx, iters >= 1, "iters must be >= 1");
   ANOMOD_REQUIRE(ctx, g->device == ctx->device, "graph lives on another device");
   const uint32_t N = g->N;
-  double psum = 0.0;
-  for (uint32_t i = 0; i < N; ++i) {
-    ANOMOD_REQUIRE(ctx, std::isfinite(p[i]) && p[i] >= 0.0, "personalization[%u] invalid", i);
-    psum += p[i];
-  }
-  ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
   if (int rc = bind(ctx)) return rc;
   // p goes up raw through pinned staging and is normalised on the device
   // (the host-side copy, division and pageable DMA were ~30 % of a
-  // 100-iteration solve at N = 10^5)
+  // 100-iteration solve at N = 10^5); the copy to staging is the checking
+  // and summing pass.
   if (!g->h_pin)
     ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&g->h_pin), N * 8ull + 16,
                                   hipHostMallocDefault));  // + the barrier words
-  memcpy(g->h_pin, p, N * 8ull);
+  double psum = 0.0;
+  const uint32_t bad = personalization_sum<true>(p, N, g->h_pin, psum);
+  ANOMOD_REQUIRE(ctx, bad == N, "personalization[%u] invalid", bad);
+  ANOMOD_REQUIRE(ctx, psum > 0.0, "personalization sums to zero");
   ANOMOD_HIP(ctx, hipMemcpyAsync(g->p, g->h_pin, N * 8ull, hipMemcpyHostToDevice, ctx->stream));
   // x0 = 1/N; its dangling mass n_dangling/N seeds iteration 0 (slot 0); the
-  // slots iteration 0 adds into must start at zero.
-  for (unsigned long long& v : g->host_acc) v = 0ull;
-  g->host_acc[0] = (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->acc, g->host_acc.data(), g->host_acc.size() * 8,
-                                 hipMemcpyHostToDevice, ctx->stream));
+  // slots iteration 0 adds into must start at zero (the init kernel writes
+  // them, and clears the barrier words).
+  const unsigned long long acc0 =
+      (unsigned long long)std::llround((double)g->n_dangling / N * kDScale);
   hipLaunchKernelGGL(ppr_init_norm_kernel, dim3(std::min<uint32_t>(g->grid, 1024)),
-                     dim3(kPprThreads), 0, ctx->stream, N, 1.0 / N, g->x[0], g->p, psum);
+                     dim3(kPprThreads), 0, ctx->stream, N, 1.0 / N, g->x[0], g->p, psum, g->acc,
+                     (uint32_t)g->host_acc.size(), acc0, g->bar, (uint32_t)kBarWords);
   ANOMOD_HIP(ctx, hipGetLastError());
   uint32_t done = 0;
   // One persistent launch for the whole solve when every workgroup fits on
@@ -769,7 +803,6 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   const bool persistent = (int)pgrid <= g->coop_blocks && mode != 1;
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
   if (persistent) {
-    ANOMOD_HIP(ctx, hipMemsetAsync(g->bar, 0, kBarWords * sizeof(unsigned int), ctx->stream));
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
     hipLaunchKernelGGL(persistent_fn(sub), dim3(pgrid), dim3(kPprThreads * sub), 0, ctx->stream,
@@ -845,11 +878,8 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   for (uint32_t k = 0; k < kb; ++k) {
     const double* pk = P + (size_t)(k < K ? k : 0) * N;
     double s = 0.0;
-    for (uint32_t i = 0; i < N; ++i) {
-      ANOMOD_REQUIRE(ctx, std::isfinite(pk[i]) && pk[i] >= 0.0,
-                     "personalization[%u][%u] invalid", k, i);
-      s += pk[i];
-    }
+    const uint32_t bad = personalization_sum<false>(pk, N, nullptr, s);
+    ANOMOD_REQUIRE(ctx, bad == N, "personalization[%u][%u] invalid", k, bad);
     ANOMOD_REQUIRE(ctx, s > 0.0, "personalization %u sums to zero", k);
     for (uint32_t i = 0; i < N; ++i) pn[(size_t)i * kb + k] = pk[i] / s;
   }
@@ -949,13 +979,10 @@ int anomod_graph_pagerank_sharded(anomod_ctx* ctx, anomod_graph* g, const double
   // (the other ranks would otherwise wait in the first exchange forever).
   int local = ANOMOD_OK;
   double psum = 0.0;
-  for (uint32_t i = 0; i < N && local == ANOMOD_OK; ++i) {
-    ANOMOD_CHECK_LOCAL(ctx, local, std::isfinite(p[i]) && p[i] >= 0.0,
-                       "personalization[%u] invalid", i);
-    psum += p[i];
-  }
+  std::vector<double> pn(N);
+  const uint32_t bad = personalization_sum<true>(p, N, pn.data(), psum);
+  ANOMOD_CHECK_LOCAL(ctx, local, bad == N, "personalization[%u] invalid", bad);
   ANOMOD_CHECK_LOCAL(ctx, local, psum > 0.0, "personalization sums to zero");
-  std::vector<double> pn(p, p + N);
   for (double& v : pn) v /= psum;
   if (local == ANOMOD_OK) local = bind(ctx);
   if (local == ANOMOD_OK) local = ensure_shard_x(ctx, g, G);
