@@ -153,7 +153,16 @@ constexpr int kTile = 16;
 constexpr int kZtTiles = ANOMOD_ZT_TILES;  // tiles per load block (two blocks in flight)
 constexpr int kPadTiles = 2 * kZtTiles;  // slack tiles past ceil(T/16) read by the prefetch
 
-template <int kTiles>
+// kChk: steps between window-end checks in dense blocks — 4 when W % 4 == 0
+// (every window then ends on a float4 boundary: the window position starts at
+// 0 and a block advances it by a multiple of 4), else 1.  The per-step max
+// sequence is the same either way; only the scalar compare-and-branch of the
+// window end runs once per 4 steps.
+#ifndef ANOMOD_EWMA_CHK
+#define ANOMOD_EWMA_CHK 4
+#endif
+constexpr int kEwmaChk = ANOMOD_EWMA_CHK;  // 1: check every step (experiment builds)
+template <int kTiles, int kChk>
 __global__ __launch_bounds__(64) void ewma_zt_kernel(const float* __restrict__ Xt, uint64_t T,
                                                       uint64_t S, double alpha, uint32_t W,
                                                       float eps, float* __restrict__ Z,
@@ -190,6 +199,18 @@ __global__ __launch_bounds__(64) void ewma_zt_kernel(const float* __restrict__ X
       wmax = 0.f;
     }
   };
+  auto step_dense_nc = [&](float x) {  // window end checked by the caller
+    wmax = fmaxf(wmax, fabsf(ewma_step_dense(st, x, alpha, beta, eps)));
+  };
+  auto check4 = [&]() {
+    wpos += 4;
+    if (wpos == W) {
+      *zp = wmax;
+      zp += S;
+      wpos = 0;
+      wmax = 0.f;
+    }
+  };
   auto step_dense = [&](float x) {
     wmax = fmaxf(wmax, fabsf(ewma_step_dense(st, x, alpha, beta, eps)));
     if (++wpos == W) {
@@ -213,7 +234,17 @@ __global__ __launch_bounds__(64) void ewma_zt_kernel(const float* __restrict__ X
         for (int i = 0; i < kTiles * kV; ++i) acc += (buf[i].x + buf[i].y) + (buf[i].z + buf[i].w);
         dense = __all(acc == acc);
       }
-      if (dense) {
+      if (dense && kChk == 4) {
+#pragma unroll
+        for (int i = 0; i < kTiles * kV; ++i) {
+          step_dense_nc(buf[i].x);
+          step_dense_nc(buf[i].y);
+          step_dense_nc(buf[i].z);
+          step_dense_nc(buf[i].w);
+          check4();
+        }
+        st.n += kTiles * kTile;
+      } else if (dense) {
 #pragma unroll
         for (int i = 0; i < kTiles * kV; ++i) {
           step_dense(buf[i].x);
@@ -704,7 +735,9 @@ int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint3
     const uint64_t seg = seg_env ? std::max<uint64_t>(l, seg_env / l * l) : ser->T;
     for (uint64_t t0 = 0; t0 < ser->T; t0 += seg) {
       const uint64_t Ts = std::min<uint64_t>(seg, ser->T - t0);
-      hipLaunchKernelGGL(ewma_zt_kernel<kZtTiles>, dim3(strips), dim3(64), 0, ctx->stream,
+      hipLaunchKernelGGL((W % 4 == 0 && kEwmaChk == 4 ? ewma_zt_kernel<kZtTiles, 4>
+                                                       : ewma_zt_kernel<kZtTiles, 1>),
+                         dim3(strips), dim3(64), 0, ctx->stream,
                          ser->X + t0 / kTile * ser->S * kTile, Ts, ser->S, (double)alpha, W, eps,
                          ser->Z + t0 / W * ser->S, ser->m, ser->v, ser->n);
     }
