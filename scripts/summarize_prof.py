@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import csv
 import json
+import math
 import shutil
 import sys
 from pathlib import Path
@@ -50,6 +51,7 @@ def main() -> int:
     # scripts/profile.sh), against the algorithmic bytes of the same launch
     # from the bench line of the same box
     alg = {}
+    per_unit = {}  # launches per algorithmic unit (EWMA: a chunk runs as time segments)
     if bench:
         alg["edge_agg_kernel"] = bench["roofline"]["bytes_per_launch"]
         if "trace_structure" in bench:
@@ -58,15 +60,21 @@ def main() -> int:
             e = bench["ewma"]
             samples = e["steps_per_chunk"] * e["S"]
             alg["ewma_zt_kernel"] = 4 * samples + 4 * samples // e["W"] + 40 * e["S"]
+            # ewma.hip: segments of floor(16384 / lcm(W, 64)) * lcm(W, 64) steps
+            l = e["W"] * 64 // math.gcd(e["W"], 64)
+            seg = max(l, 16384 // l * l)
+            per_unit["ewma_zt_kernel"] = -(-e["steps_per_chunk"] // seg)
     kernels = {}
     for k, a in alg.items():
         fetch = counter(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)
         write = counter(prof / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE", k)
         if not fetch:
             continue
-        f_b = sum(fetch) / len(fetch) * 1024 * 2
-        w_b = sum(write) / len(write) * 1024 if write else 0.0
-        kernels[k] = {"launches": len(fetch), "fetch_size_kib": sum(fetch) / len(fetch),
+        u = per_unit.get(k, 1)  # launches summed per algorithmic unit
+        f_b = sum(fetch) / len(fetch) * u * 1024 * 2
+        w_b = sum(write) / len(write) * u * 1024 if write else 0.0
+        kernels[k] = {"launches": len(fetch), "launches_per_unit": u,
+                      "fetch_size_kib": sum(fetch) / len(fetch),
                       "write_size_kib": sum(write) / len(write) if write else None,
                       "read_bytes_per_launch": f_b, "write_bytes_per_launch": w_b,
                       "hbm_bytes_per_launch": f_b + w_b, "algorithmic_bytes_per_launch": a,
