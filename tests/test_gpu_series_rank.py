@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 import anomod
+from anomod import _lib as L
 from oracle import native, spec
 
 pytestmark = pytest.mark.gpu
@@ -296,3 +297,32 @@ def test_one_shot_ewma_chunked_equals_one_pass(ctx, ewma_mode, monkeypatch, T, S
     monkeypatch.setenv("ANOMOD_EWMA_CHUNK_STEPS", str(chunk))
     np.testing.assert_array_equal(ctx.ewma_z(X, a, W), one)
     np.testing.assert_allclose(one, native.ewma_z(X, a, W), rtol=Z_RTOL, atol=Z_ATOL)
+
+
+def test_pagerank_rejects_invalid_personalization(ctx):
+    """Negative / NaN / inf entries and an all-zero vector are refused with the
+    first bad index (the staging copy is the checking pass); a valid solve
+    afterwards gives the same bits as before."""
+    g = anomod.DeviceGraph(ctx, synthetic=(5000, 6, 9))
+    p = np.random.default_rng(9).random(g.N)
+    x0, _ = g.pagerank(p, iters=20)
+    for bad_at, v in ((7, -1.0), (4999, np.nan), (0, np.inf), (4093, -np.inf)):
+        q = p.copy()
+        q[bad_at] = v
+        q[bad_at + 1:] = np.where(np.arange(bad_at + 1, g.N) % 2 == 0, -2.0, q[bad_at + 1:])
+        with pytest.raises(L.AnomodError, match=rf"personalization\[{bad_at}\] invalid"):
+            g.pagerank(q, iters=20)
+        with pytest.raises(L.AnomodError, match=rf"personalization\[{bad_at}\] invalid"):
+            g.pagerank_sharded(q, iters=20, virtual_shards=2)
+        P = np.stack([p, p, q])
+        with pytest.raises(L.AnomodError, match=rf"personalization\[2\]\[{bad_at}\] invalid"):
+            g.pagerank_batch(P, iters=20)
+    with pytest.raises(L.AnomodError, match="sums to zero"):
+        g.pagerank(np.zeros(g.N), iters=20)
+    x1, _ = g.pagerank(p, iters=20)
+    np.testing.assert_array_equal(x0, x1)
+    # -0.0 is a valid (zero) weight
+    q = p.copy()
+    q[3] = -0.0
+    g.pagerank(q, iters=5)
+    g.free()
