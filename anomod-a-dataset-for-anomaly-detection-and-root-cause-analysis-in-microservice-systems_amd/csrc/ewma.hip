@@ -146,7 +146,11 @@ __global__ __launch_bounds__(64) void ewma_z_kernel(const float* __restrict__ X,
 // Sequential recurrence over the tiled layout.  kTiles tiles (16 steps each)
 // per load block, two blocks in flight; blocks wholly inside T run without
 // per-step bounds checks.
-constexpr int kTile = 16;
+#ifndef ANOMOD_EWMA_TILE
+#define ANOMOD_EWMA_TILE 16
+#endif
+constexpr int kTile = ANOMOD_EWMA_TILE;  // steps per tile (one lane's contiguous run)
+static_assert(kTile % 16 == 0 && 64 % kTile == 0, "tile steps");
 #ifndef ANOMOD_ZT_TILES
 #define ANOMOD_ZT_TILES 4
 #endif
@@ -160,6 +164,9 @@ constexpr int kPadTiles = 2 * kZtTiles;  // slack tiles past ceil(T/16) read by 
 // window end runs once per 4 steps.
 #ifndef ANOMOD_EWMA_CHK
 #define ANOMOD_EWMA_CHK 4
+#endif
+#ifndef ANOMOD_EWMA_ABL
+#define ANOMOD_EWMA_ABL 0
 #endif
 constexpr int kEwmaChk = ANOMOD_EWMA_CHK;  // 1: check every step (experiment builds)
 template <int kTiles, int kChk>
@@ -200,7 +207,11 @@ __global__ __launch_bounds__(64) void ewma_zt_kernel(const float* __restrict__ X
     }
   };
   auto step_dense_nc = [&](float x) {  // window end checked by the caller
+#if ANOMOD_EWMA_ABL & 1  // timing only: the loads and window stores without the recurrence
+    wmax = fmaxf(wmax, x);
+#else
     wmax = fmaxf(wmax, fabsf(ewma_step_dense(st, x, alpha, beta, eps)));
+#endif
   };
   auto check4 = [&]() {
     wpos += 4;
