@@ -4,12 +4,15 @@
 // metrics.py:53-67 per-query CSV).
 //
 // X lives in one of two layouts, chosen per call by the kernel that reads it:
-//  * tiled  Xt[ceil(T/16)][S][16] — 16 consecutive steps of a series are
-//    contiguous (64 B), so one load instruction of a wave fetches 1 KiB
-//    (4 x float4 per lane per tile).  The sequential kernel (one series per
-//    lane down T) reads it; with S/64 waves on the chip the row-major form
-//    (one 256-B row segment per instruction) tops out near 2 TB/s, the tiled
-//    one is ~1.4x faster.  Steps past T in the last tile hold NaN.
+//  * tiled  Xt[ceil(T/16)][4][S][4] — a tile holds 16 steps of every series
+//    as four planes of float4 (steps 4q .. 4q+3 of series s at plane q), so
+//    one load instruction of a wave reads 1 KiB contiguously (series-major
+//    tiles [S][16], each lane's 64 B contiguous, read the same bytes at a
+//    64-B lane stride: 1.5 % slower at the config-4 chunk, 5-10 % at
+//    T = 7680).  The sequential kernel (one series per lane down T) reads
+//    it; with S/64 waves on the chip the row-major form (one 256-B row
+//    segment per instruction) tops out near 2 TB/s, the tiled one is ~1.4x
+//    faster.  Steps past T in the last tile hold NaN.
 //  * rows   X[T][S] — the time-parallel kernel (small S) gives each wave U
 //    consecutive rows, which a 16-step tiling would misalign for W % 16 != 0.
 // Upload takes row-major host data and tiles it on the device in bounded
@@ -151,6 +154,19 @@ __global__ __launch_bounds__(64) void ewma_z_kernel(const float* __restrict__ X,
 #endif
 constexpr int kTile = ANOMOD_EWMA_TILE;  // steps per tile (one lane's contiguous run)
 static_assert(kTile % 16 == 0 && 64 % kTile == 0, "tile steps");
+#ifndef ANOMOD_EWMA_QMAJOR
+#define ANOMOD_EWMA_QMAJOR 1
+#endif
+// Float index of steps 4q .. 4q+3 of series s in tile `tile` (a tile holds
+// kTile steps of every series: S * kTile floats).  q-major (default): the
+// float4 groups of one q for all series contiguous, so a wave's load
+// instruction reads 1 KiB contiguously; series-major (ANOMOD_EWMA_QMAJOR=0,
+// the r01/r02 layout): each series' kTile steps contiguous.
+__host__ __device__ __forceinline__ uint64_t tile_off(uint64_t tile, uint64_t S, uint64_t s,
+                                                      uint64_t q) {
+  if constexpr (ANOMOD_EWMA_QMAJOR) return tile * S * kTile + (q * S + s) * 4;
+  else return (tile * S + s) * kTile + 4 * q;
+}
 #ifndef ANOMOD_ZT_TILES
 #define ANOMOD_ZT_TILES 4
 #endif
@@ -164,6 +180,9 @@ constexpr int kPadTiles = 2 * kZtTiles;  // slack tiles past ceil(T/16) read by 
 // window end runs once per 4 steps.
 #ifndef ANOMOD_EWMA_CHK
 #define ANOMOD_EWMA_CHK 4
+#endif
+#ifndef ANOMOD_EWMA_NT
+#define ANOMOD_EWMA_NT 0
 #endif
 #ifndef ANOMOD_EWMA_ABL
 #define ANOMOD_EWMA_ABL 0
@@ -189,9 +208,17 @@ __global__ __launch_bounds__(64) void ewma_zt_kernel(const float* __restrict__ X
   auto load = [&](float4* buf, uint64_t tile0) {
 #pragma unroll
     for (int k = 0; k < kTiles; ++k) {
-      const float4* p = reinterpret_cast<const float4*>(Xt + ((tile0 + k) * S + s) * kTile);
 #pragma unroll
-      for (int q = 0; q < kV; ++q) buf[k * kV + q] = p[q];
+      for (int q = 0; q < kV; ++q) {
+        const float4* p = reinterpret_cast<const float4*>(Xt + tile_off(tile0 + k, S, s, q));
+#if ANOMOD_EWMA_NT  // experiment builds: nontemporal sample loads
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        buf[k * kV + q] = make_float4(v.x, v.y, v.z, v.w);
+#else
+        buf[k * kV + q] = *p;
+#endif
+      }
     }
   };
   float wmax = 0.f;
@@ -320,15 +347,15 @@ __global__ void series_relayout_kernel(const float* __restrict__ src, float* __r
         const uint64_t r = k * kTile + e;
         v[e] = (r < R && r0 + r < T) ? src[r * S + s] : NAN;
       }
-      float4* o = reinterpret_cast<float4*>(dst + (tile * S + s) * kTile);
 #pragma unroll
-      for (int q = 0; q < kTile / 4; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      for (int q = 0; q < kTile / 4; ++q)
+        *reinterpret_cast<float4*>(dst + tile_off(tile, S, s, q)) =
+            make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     } else {
-      const float4* p = reinterpret_cast<const float4*>(src + (tile * S + s) * kTile);
       float v[kTile];
 #pragma unroll
       for (int q = 0; q < kTile / 4; ++q) {
-        const float4 f = p[q];
+        const float4 f = *reinterpret_cast<const float4*>(src + tile_off(tile, S, s, q));
         v[4 * q] = f.x;
         v[4 * q + 1] = f.y;
         v[4 * q + 2] = f.z;
@@ -509,8 +536,14 @@ __global__ void series_fill_kernel(float* X, uint64_t T, uint64_t S, uint64_t se
     uint64_t tl, s;  // step within this matrix, series
     if (tiled) {
       const uint64_t st = (uint64_t)kTile * S;
-      tl = i / st * kTile + i % kTile;
-      s = i % st / kTile;
+      const uint64_t r = i % st;
+      if constexpr (ANOMOD_EWMA_QMAJOR) {
+        tl = i / st * kTile + r / (4 * S) * 4 + r % 4;
+        s = r % (4 * S) / 4;
+      } else {
+        tl = i / st * kTile + r % kTile;
+        s = r / kTile;
+      }
       if (tl >= T) {
         X[i] = NAN;
         continue;
