@@ -815,6 +815,22 @@ __device__ __forceinline__ double quantile_from(uint64_t r, uint64_t excl, uint6
   return 0.0;
 }
 
+// Clears the table before a launch: words [0, nz) to zero (hist | err | sum |
+// mx | ctr | big) and the E minima to all ones.  One launch in place of two
+// memsets, which the runtime splits into several fill kernels (~40 us of
+// launches per aggregation, against ~4 us for this).
+__global__ __launch_bounds__(256) void edge_table_init_kernel(unsigned long long* __restrict__ z,
+                                                              uint64_t nz,
+                                                              unsigned int* __restrict__ mn,
+                                                              uint32_t E) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4* z4 = reinterpret_cast<uint4*>(z);  // the table base is 256-B aligned
+  for (uint64_t i = i0; i < nz / 2; i += stride) z4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if ((nz & 1u) && i0 == 0) z[nz - 1] = 0ull;
+  for (uint64_t i = i0; i < E; i += stride) mn[i] = 0xFFFFFFFFu;
+}
+
 __global__ __launch_bounds__(kWave) void edge_finalize_kernel(Table tab,
                                                               unsigned long long* count,
                                                               double* p50, double* p99) {
@@ -1010,8 +1026,13 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
   auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
 
-  ANOMOD_HIP(ctx, hipMemsetAsync(base, 0, L.off_count, ctx->stream));  // hist|err|sum|mx|ctr|big
-  ANOMOD_HIP(ctx, hipMemsetAsync(tab.mn, 0xFF, E * 4ull, ctx->stream));
+  {
+    const uint64_t nz = L.off_count / 8;  // hist|err|sum|mx|ctr|big
+    const uint64_t blocks = std::min<uint64_t>((nz / 2 + 255) / 256 + 1, 4ull * ctx->num_cus);
+    hipLaunchKernelGGL(edge_table_init_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<unsigned long long*>(base), nz, tab.mn, E);
+    ANOMOD_HIP(ctx, hipGetLastError());
+  }
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
