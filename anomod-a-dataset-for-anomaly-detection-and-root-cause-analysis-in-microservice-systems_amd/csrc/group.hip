@@ -65,11 +65,20 @@ struct GroupWs {
   uint64_t list_cap = 0;
   uint32_t epoch = 0;
   unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
+  void* block = nullptr;  // one allocation the device buffers are carved from (ANOMOD_GRP_ONEALLOC)
 };
 
 namespace {
 
 using chunk::wave_sync;
+// The workspace's device buffers are carved (2-MiB aligned) from one
+// allocation; 0 = one hipMalloc per buffer.  The radix passes' scattered runs
+// land across ~37 GB at 2^27 traces, and their time varies by process with
+// where the pages land: 4 processes each at 2^27 traces, one allocation
+// 99.4-103.2 ms vs 99.7-107.7 ms.
+#ifndef ANOMOD_GRP_ONEALLOC
+#define ANOMOD_GRP_ONEALLOC 1
+#endif
 // Experiment-only ablation (never set in the shipped build; timing only,
 // wrong output): 1 = every pass writes its staged tile to the tile's own rows.
 #ifndef ANOMOD_GRP_ABL
@@ -670,6 +679,28 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ws->cap = cap;
   ws->state_words = (cap + kTTile - 1) / kTTile;  // look-back words of the scans
   ws->list_cap = cap / 8 + 65536;
+#if ANOMOD_GRP_ONEALLOC
+  {
+    const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
+                            ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
+                            ws->list_cap * 8, tiles * kDig * 4,
+                            (tiles / kTScanRows + 1) * kDig * 4, cap + 16};
+    void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
+                     (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
+                     (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum, (void**)&ws->dig};
+    constexpr size_t kAlign = size_t(2) << 20;
+    size_t total = 0;
+    for (size_t z : sizes) total += (z + kAlign - 1) / kAlign * kAlign;
+    bool ok1 = hipMalloc(&ws->block, total) == hipSuccess;
+    size_t off = 0;
+    for (int i = 0; ok1 && i < 10; ++i) {
+      *ptrs[i] = static_cast<char*>(ws->block) + off;
+      off += (sizes[i] + kAlign - 1) / kAlign * kAlign;
+    }
+    if (!ok1) ws->block = nullptr;
+  }
+  bool ok = ws->block != nullptr;
+#else
   bool ok = hipMalloc(&ws->aos[0], cap * sizeof(GRec)) == hipSuccess;
   ok = ok && hipMalloc(&ws->aos[1], cap * sizeof(GRec)) == hipSuccess;
   ok = ok && hipMalloc(&ws->tptr, (cap + 1) * 8) == hipSuccess;
@@ -680,6 +711,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ok = ok && hipMalloc(&ws->tcnt, tiles * kDig * 4) == hipSuccess;
   ok = ok && hipMalloc(&ws->bsum, (tiles / kTScanRows + 1) * kDig * 4) == hipSuccess;
   ok = ok && hipMalloc(&ws->dig, cap + 16) == hipSuccess;
+#endif
   ok = ok && hipHostMalloc(reinterpret_cast<void**>(&ws->h_misc), kMiscWords * 8,
                            hipHostMallocDefault) == hipSuccess;
   if (!ok) {
@@ -833,8 +865,12 @@ void free_group_ws(anomod_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* p[] = {ws->aos[0], ws->aos[1], ws->tptr, ws->state, ws->misc, ws->list, ws->owned,
                ws->tcnt, ws->bsum, ws->dig};
-  for (void* q : p)
-    if (q) (void)hipFree(q);
+  if (ws->block) {
+    (void)hipFree(ws->block);
+  } else {
+    for (void* q : p)
+      if (q) (void)hipFree(q);
+  }
   if (ws->h_misc) (void)hipHostFree(ws->h_misc);
   delete ws;
   ctx->group_ws = nullptr;
