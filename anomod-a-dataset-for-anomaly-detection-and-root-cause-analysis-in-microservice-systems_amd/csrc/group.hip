@@ -72,10 +72,10 @@ namespace {
 
 using chunk::wave_sync;
 // The workspace's device buffers are carved (2-MiB aligned) from one
-// allocation; 0 = one hipMalloc per buffer.  The radix passes' scattered runs
-// land across ~37 GB at 2^27 traces, and their time varies by process with
-// where the pages land: 4 processes each at 2^27 traces, one allocation
-// 99.4-103.2 ms vs 99.7-107.7 ms.
+// allocation; 0 = one hipMalloc per buffer.  The radix passes' time varies by
+// process (98.8-113.4 ms at 2^27 traces over 12 processes of this form,
+// 100.0-112.6 over 8 of the other: no measurable difference); a physically
+// contiguous allocation (hipDeviceMallocContiguous) ran 138-153 ms.
 #ifndef ANOMOD_GRP_ONEALLOC
 #define ANOMOD_GRP_ONEALLOC 1
 #endif
