@@ -5,7 +5,7 @@
 // must decode or fail with a status, never touch memory it does not own.
 //
 // usage: decode_fuzz ITERS SEED kind:path ...   (kind: jaeger | skywalking |
-//        long | prom); prints "ok <decoded> <rejected>" on success.
+//        long | longfile | prom); prints "ok <decoded> <rejected>" on success.
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -15,6 +15,8 @@
 #include <random>
 #include <string>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../../include/anomod.h"
 
@@ -76,6 +78,46 @@ int run(const Seed& sd, const std::string& data) {
     anomod_decoded_columns(d, &o, ptr.data());
     for (uint32_t i = 0; i < nsv; ++i) (void)strlen(anomod_decoded_service(d, i));
     anomod_decoded_free(d);
+    return 1;
+  }
+  if (sd.kind == "longfile") {
+    // The file API maps the file: no terminator past its last byte.  Sizes
+    // are padded (newlines) to a whole number of pages so a read past the
+    // end faults instead of landing in the page's zero slack; the result
+    // must equal the buffer API's on the same bytes.
+    std::string body = data + std::string((4096 - data.size() % 4096) % 4096, '\n');
+    char path[] = "/tmp/anomod_fuzz_XXXXXX";
+    const int fd = mkstemp(path);
+    if (fd < 0) return 0;
+    const bool wrote = write(fd, body.data(), body.size()) == (ssize_t)body.size();
+    close(fd);
+    anomod_metrics *mf = nullptr, *mb = nullptr;
+    const int rf = wrote ? anomod_decode_metric_long_csv_file(path, &mf) : ANOMOD_EINVAL;
+    unlink(path);
+    const int rb = anomod_decode_metric_long_csv(body.data(), body.size(), &mb);
+    if (wrote && (rf == ANOMOD_OK) != (rb == ANOMOD_OK)) {
+      fprintf(stderr, "file and buffer decodes disagree: %d vs %d\n", rf, rb);
+      abort();
+    }
+    if (rf != ANOMOD_OK) {
+      if (mb) anomod_metrics_free(mb);
+      return 0;
+    }
+    uint64_t T1 = 0, S1 = 0, T2 = 0, S2 = 0;
+    anomod_metrics_info(mf, &T1, &S1);
+    anomod_metrics_info(mb, &T2, &S2);
+    if (T1 != T2 || S1 != S2) abort();
+    std::vector<float> X1(T1 * S1), X2(T2 * S2);
+    std::vector<double> t1(T1), t2(T2);
+    anomod_metrics_matrix(mf, X1.data(), t1.data());
+    anomod_metrics_matrix(mb, X2.data(), t2.data());
+    if ((!X1.empty() && memcmp(X1.data(), X2.data(), X1.size() * 4)) ||
+        (T1 && memcmp(t1.data(), t2.data(), T1 * 8)))
+      abort();
+    for (uint64_t s = 0; s < S1; ++s)
+      if (strcmp(anomod_metrics_series_name(mf, s), anomod_metrics_series_name(mb, s))) abort();
+    anomod_metrics_free(mf);
+    anomod_metrics_free(mb);
     return 1;
   }
   anomod_metrics* m = nullptr;

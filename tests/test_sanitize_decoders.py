@@ -43,6 +43,7 @@ def _seeds(golden, tmp_path):
     return [f"jaeger:{tmp_path / 'j_small.json'}", f"jaeger:{tmp_path / 'j_big.json'}",
             f"skywalking:{tmp_path / 's_small.json'}", f"skywalking:{tmp_path / 's_big.json'}",
             f"long:{golden / 'metric_long.csv'}",
+            f"longfile:{golden / 'metric_long.csv'}",
             f"prom:{golden / 'prom_dir' / 'socialnet_container_memory.csv'}",
             f"prom:{golden / 'prom_dir' / 'mongodb_operations_rate.csv'}"]
 
