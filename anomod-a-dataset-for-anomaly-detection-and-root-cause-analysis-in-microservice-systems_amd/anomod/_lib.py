@@ -201,6 +201,7 @@ _SIGS = {
     "anomod_graph_create": (_i32, [_vp, _P(_u32), _P(_u32), _P(_f32), _u32, _P(_vp)]),
     "anomod_graph_synthetic": (_i32, [_vp, _u32, _u32, _u64, _P(_vp)]),
     "anomod_graph_info": (_i32, [_vp, _P(_u32), _P(_u64)]),
+    "anomod_graph_last_solve": (_i32, [_vp, _P(_u32), _P(_u32)]),
     "anomod_graph_pagerank": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _P(_f64), _P(_u32)]),
     "anomod_graph_pagerank_sharded": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _u32,
                                              _P(_f64), _P(_u32)]),

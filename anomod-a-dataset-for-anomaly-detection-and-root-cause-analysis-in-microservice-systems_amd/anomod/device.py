@@ -377,6 +377,18 @@ class DeviceGraph:
                                                       L.ptr(x, C.c_double), C.byref(done)))
         return x, done.value
 
+    PATHS = {1: "graph", 2: "readback", 3: "persistent"}
+
+    def last_solve(self) -> tuple[str, int]:
+        """(path of the last pagerank() solve, persistent-launch fallbacks so
+        far); the path is "graph" / "readback" / "persistent", with a
+        "fallback:" prefix when a persistent launch timed out at its grid
+        barrier and the solve was rerun per launch."""
+        path, fb = C.c_uint32(), C.c_uint32()
+        L.check(L.lib().anomod_graph_last_solve(self.handle, C.byref(path), C.byref(fb)))
+        name = self.PATHS.get(path.value & 3, "none")
+        return ("fallback:" + name if path.value & 4 else name), fb.value
+
     def pagerank_sharded(self, p, alpha=0.85, iters=100, tol=0.0, virtual_shards=0):
         """Row-sharded solve: over the ranks of the attached RCCL communicator,
         or over ``virtual_shards`` row shards on this device when none is

@@ -6,13 +6,31 @@ set shards by ``trace_hash % world`` with no data exchange; the only
 collective is the integer all-reduce (sum / min / max) of the edge table
 that libanomod issues itself once a communicator is attached.  The
 reference has no distributed backend at all.
+
+The host side needs no framework: ``HostGroup`` is a stdlib TCP group
+(rank 0 serves, the other ranks connect) that carries the 128-B RCCL unique
+id, the bench's barriers and scalar reductions, and — for ranks that share
+one device, where RCCL refuses to run — libanomod's host collective
+transport.  Rendezvous: rank 0 binds an ephemeral port and publishes it in a
+file keyed by MASTER_PORT and the launcher's pid (every rank of one
+``torch.distributed.run`` / test launch is a child of the same process), so
+nothing collides with the launcher's own store on MASTER_PORT.
 """
 from __future__ import annotations
 
+import json
 import os
+import socket
+import struct
+import tempfile
+import time
 from dataclasses import dataclass
+from pathlib import Path
 from typing import Callable
 
+import numpy as np
+
+from ._lib import OP_MAX, OP_MIN, OP_SUM
 from .device import Context
 from .spans import SpanSet
 
@@ -34,61 +52,217 @@ def shard_spans(spans: SpanSet, info: RankInfo) -> SpanSet:
     return spans if info.world == 1 else spans.shard(info.world, info.rank)
 
 
-def torch_exchange(uid: bytes | None) -> bytes:
-    """Broadcast rank 0's RCCL unique id over an initialised torch.distributed
-    group (any backend; the host-side rendezvous only)."""
-    import torch.distributed as tdist
+# ---- stdlib TCP group ---------------------------------------------------------
 
-    obj = [uid]
-    tdist.broadcast_object_list(obj, src=0)
-    return obj[0]
+_MAGIC = b"ANMD"
 
+
+def _send(sock: socket.socket, data: bytes) -> None:
+    sock.sendall(struct.pack("<Q", len(data)) + data)
+
+
+def _recv_exact(sock: socket.socket, n: int) -> bytes:
+    buf = bytearray(n)
+    view = memoryview(buf)
+    got = 0
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if k == 0:
+            raise ConnectionError("peer closed the anomod host group")
+        got += k
+    return bytes(buf)
+
+
+def _recv(sock: socket.socket) -> bytes:
+    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
+    return _recv_exact(sock, n)
+
+
+def _reduce(parts: list[np.ndarray], op: int) -> np.ndarray:
+    if op == OP_SUM:
+        out = parts[0].copy()
+        for p in parts[1:]:
+            out += p  # unsigned integers wrap mod 2^bits, as the device sums do
+        return out
+    if op == OP_MIN:
+        return np.minimum.reduce(parts)
+    if op == OP_MAX:
+        return np.maximum.reduce(parts)
+    raise ValueError(f"unknown reduction op {op}")
+
+
+class HostGroup:
+    """A star-shaped TCP process group over the ranks of one node.
+
+    Every collective gathers the ranks' payloads at rank 0, which combines
+    them in rank order and sends the result back, so all ranks hold the same
+    bytes.  Payloads here are tiny (an RCCL unique id, scalars) or the
+    host-transport buffers of tests on one device."""
+
+    def __init__(self, rank: int, world: int, key: str | None = None,
+                 timeout_s: float | None = None, rdzv_dir: str | None = None):
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"bad rank {rank} of world {world}")
+        self.rank, self.world = rank, world
+        self.timeout_s = float(timeout_s if timeout_s is not None
+                               else os.environ.get("ANOMOD_RCCL_TIMEOUT_S", "300"))
+        self._peers: list[socket.socket] = []  # rank 0: ranks 1..world-1 in order
+        self._sock: socket.socket | None = None  # other ranks: the link to rank 0
+        self._file: Path | None = None
+        if world == 1:
+            return
+        if key is None:
+            key = f"{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"
+        d = Path(rdzv_dir or os.environ.get("ANOMOD_RDZV_DIR") or tempfile.gettempdir())
+        path = d / f"anomod-rdzv-{key}.json"
+        host = os.environ.get("ANOMOD_RDZV_ADDR", "127.0.0.1")
+        deadline = time.monotonic() + self.timeout_s
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.bind((host, 0))
+            srv.listen(world)
+            tmp = path.with_suffix(f".tmp{os.getpid()}")
+            tmp.write_text(json.dumps({"addr": host, "port": srv.getsockname()[1],
+                                       "world": world, "pid": os.getpid()}))
+            os.replace(tmp, path)
+            self._file = path
+            peers: dict[int, socket.socket] = {}
+            try:
+                while len(peers) < world - 1:
+                    srv.settimeout(max(0.1, deadline - time.monotonic()))
+                    try:
+                        c, _ = srv.accept()
+                    except socket.timeout:
+                        raise TimeoutError(f"anomod host group: {len(peers) + 1} of {world} "
+                                           f"ranks joined within {self.timeout_s:.0f} s") from None
+                    c.settimeout(self.timeout_s)
+                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    hello = _recv(c)
+                    magic, r, w = hello[:4], *struct.unpack("<ii", hello[4:12])
+                    if magic != _MAGIC or w != world or not 0 < r < world or r in peers:
+                        c.close()
+                        continue
+                    peers[r] = c
+            finally:
+                srv.close()
+            self._peers = [peers[r] for r in range(1, world)]
+            for c in self._peers:
+                _send(c, b"ok")
+        else:
+            while True:
+                try:
+                    info = json.loads(path.read_text())
+                    s = socket.create_connection((info["addr"], info["port"]), timeout=5.0)
+                    s.settimeout(self.timeout_s)
+                    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    _send(s, _MAGIC + struct.pack("<ii", rank, world))
+                    if _recv(s) == b"ok":
+                        self._sock = s
+                        break
+                    s.close()
+                except (OSError, ValueError, KeyError, ConnectionError):
+                    pass  # not published yet, or a stale file of an earlier run
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"anomod host group: rank {rank} found no rank 0 at "
+                                       f"{path} within {self.timeout_s:.0f} s")
+                time.sleep(0.05)
+
+    @classmethod
+    def from_env(cls, **kw) -> "HostGroup":
+        info = rank_from_env()
+        return cls(info.rank, info.world, **kw)
+
+    # -- primitives
+    def _gather_bcast(self, payload: bytes, combine: Callable[[list[bytes]], bytes]) -> bytes:
+        """Every rank's payload to rank 0, combine(payloads in rank order) back
+        to every rank."""
+        if self.world == 1:
+            return combine([payload])
+        if self.rank == 0:
+            out = combine([payload] + [_recv(c) for c in self._peers])
+            for c in self._peers:
+                _send(c, out)
+            return out
+        _send(self._sock, payload)
+        return _recv(self._sock)
+
+    def broadcast(self, data: bytes | None, src: int = 0) -> bytes:
+        """src's bytes on every rank."""
+        mine = (b"\x01" + data) if self.rank == src else b"\x00"
+        return self._gather_bcast(mine, lambda ps: next(p[1:] for p in ps if p[:1] == b"\x01"))
+
+    def barrier(self) -> None:
+        self._gather_bcast(b"", lambda ps: b"")
+
+    def allreduce(self, a: np.ndarray, op: int = OP_SUM) -> None:
+        """Reduce a numpy array in place over all ranks (same shape/dtype)."""
+        dt, shape = a.dtype, a.shape
+
+        def combine(ps):
+            return _reduce([np.frombuffer(p, dtype=dt) for p in ps], op).tobytes()
+
+        a[...] = np.frombuffer(self._gather_bcast(np.ascontiguousarray(a).tobytes(), combine),
+                               dtype=dt).reshape(shape)
+
+    def allgather(self, a: np.ndarray, block: int) -> None:
+        """Every rank's ``block``-byte slice of the u8 array ``a`` (rank r's is
+        a[r*block:(r+1)*block], set by rank r) on every rank."""
+        mine = a[self.rank * block:(self.rank + 1) * block].tobytes()
+        out = self._gather_bcast(mine, lambda ps: b"".join(ps))
+        a[:block * self.world] = np.frombuffer(out, dtype=np.uint8)
+
+    def allreduce_scalar(self, v: float, op: int = OP_SUM) -> float:
+        t = np.array([v], dtype=np.float64)
+        self.allreduce(t, op)
+        return float(t[0])
+
+    def close(self) -> None:
+        for c in self._peers:
+            c.close()
+        if self._sock is not None:
+            self._sock.close()
+        self._peers, self._sock = [], None
+        if self._file is not None:
+            try:
+                self._file.unlink()
+            except OSError:
+                pass
+            self._file = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+# ---- libanomod communicators ------------------------------------------------------
 
 def attach_rccl(ctx: Context, info: RankInfo,
-                exchange: Callable[[bytes | None], bytes] = torch_exchange) -> None:
-    """Create the RCCL communicator of this rank (no-op for world == 1)."""
+                exchange: Callable[[bytes | None], bytes] | HostGroup | None = None) -> None:
+    """Create the RCCL communicator of this rank (no-op for world == 1).
+    Rank 0's 128-B unique id travels through ``exchange``: a HostGroup (its
+    broadcast), any callable uid -> uid, or None = a HostGroup made from the
+    environment for this call."""
     if info.world <= 1:
         return
     uid = Context.unique_id() if info.rank == 0 else None
-    uid = exchange(uid)
+    if isinstance(exchange, HostGroup):
+        uid = exchange.broadcast(uid)
+    elif exchange is not None:
+        uid = exchange(uid)
+    else:
+        with HostGroup(info.rank, info.world) as g:
+            uid = g.broadcast(uid)
     ctx.attach_comm(uid, info.world, info.rank)
 
 
-def attach_gloo(ctx: Context, info: RankInfo) -> None:
-    """Host transport over an initialised torch.distributed group (gloo):
-    the libanomod collectives (status agreement, edge-table merge, sharded
-    PageRank exchange) go through host memory instead of RCCL — for ranks
-    that share one device, where RCCL refuses to run.  No-op for world == 1."""
-    if info.world <= 1:
+def attach_host(ctx: Context, group: HostGroup) -> None:
+    """Host collective transport over a HostGroup: the libanomod collectives
+    (status agreement, edge-table merge, sharded PageRank exchange) go
+    through host memory instead of RCCL — for ranks that share one device,
+    where RCCL refuses to run.  No-op for world == 1."""
+    if group.world <= 1:
         return
-    import numpy as np
-    import torch
-    import torch.distributed as tdist
-
-    from . import _lib as L
-
-    ops = {L.OP_SUM: tdist.ReduceOp.SUM, L.OP_MIN: tdist.ReduceOp.MIN,
-           L.OP_MAX: tdist.ReduceOp.MAX}
-
-    def allreduce(a: np.ndarray, dtype: int, op: int) -> None:
-        if dtype == L.DTYPE_U64:
-            if op != L.OP_SUM:
-                raise ValueError("u64 min/max is not used by libanomod")
-            t = torch.from_numpy(a.view(np.int64))  # two's complement: same bits mod 2^64
-            tdist.all_reduce(t, ops[op])
-        elif dtype == L.DTYPE_U32:  # widened: the u32 range is not a signed 32-bit one
-            t = torch.from_numpy(a.astype(np.int64))
-            tdist.all_reduce(t, ops[op])
-            a[:] = t.numpy().astype(np.uint32)
-        else:
-            tdist.all_reduce(torch.from_numpy(a), ops[op])
-
-    def allgather(a: np.ndarray, block: int) -> None:
-        mine = torch.from_numpy(a[info.rank * block:(info.rank + 1) * block].copy())
-        parts = [torch.empty(block, dtype=torch.uint8) for _ in range(info.world)]
-        tdist.all_gather(parts, mine)
-        for r, t in enumerate(parts):
-            a[r * block:(r + 1) * block] = t.numpy()
-
-    ctx.attach_host_comm(info.world, info.rank, allreduce, allgather)
-
+    ctx.attach_host_comm(group.world, group.rank, lambda a, _dtype, op: group.allreduce(a, op),
+                         group.allgather)

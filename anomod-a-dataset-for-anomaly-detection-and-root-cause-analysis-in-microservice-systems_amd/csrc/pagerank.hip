@@ -52,6 +52,8 @@ struct anomod_graph {
   unsigned int* bar = nullptr;
   int coop_blocks = -1;  // co-resident workgroups of the persistent kernel (-1: not queried)
   int coop_sub = 0;      // its 256-row blocks per workgroup
+  uint32_t last_path = 0;   // ANOMOD_PPR_PATH_* of the last single-vector solve
+  uint32_t fallbacks = 0;   // persistent solves rerun per launch (barrier timed out)
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
@@ -238,7 +240,9 @@ __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
 // b % 8 (one 128-B line each); the group's last arriver adds to the top
 // counter, which every block polls.  Counters are monotonic (target =
 // arrivals x barriers passed).
-// Bounded: a wait past ~2^22 polls raises the flag and every block leaves.
+// Bounded: a wait past ~2^22 polls (ANOMOD_PPR_SPIN overrides: a test knob
+// that forces the timeout) raises the flag and every block leaves; the host
+// then reruns the solve through the per-launch path.
 constexpr uint32_t kSpinLimit = 1u << 22;
 constexpr int kBarGroups = 8;  // 16 / 32 groups measured slower
 constexpr int kBarStride = 32;  // u32 words between counters (128 B)
@@ -246,7 +250,8 @@ constexpr int kBarStride = 32;  // u32 words between counters (128 B)
 // bar[kBarStride * (1 + g)] group counters
 constexpr int kBarWords = kBarStride * (1 + kBarGroups);
 
-__device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int* s_flag) {
+__device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int* s_flag,
+                                             uint32_t spin_limit) {
   // Every wave drains its own stores (x written with agent-scope atomic
   // stores, i.e. through to the coherent level) before the workgroup meets;
   // no L2 write-back / invalidate is needed because every cross-block datum
@@ -268,7 +273,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
     int fail = 0;
     while (__hip_atomic_load(&bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
+      if (++spins > spin_limit) {
         atomicOr(&bar[1], 1u);
         fail = 1;
         break;
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
     const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
     const double* __restrict__ p, double alpha, double x0v, double* x0, double* x1,
-    unsigned long long* acc, uint32_t iters, double ntol, unsigned int* bar) {
+    unsigned long long* acc, uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit) {
   constexpr uint32_t kLdsE = SUB == 1 ? 6144u : kLdsEdgeBytes / 8u;  // SUB 1: 48 KB, 3 per CU
   __shared__ uint32_t lcol[kLdsE];
   __shared__ float lw[kLdsE];
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
       __hip_atomic_store(&acc[(3 + z) * S + threadIdx.x], 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!grid_barrier(bar, it, &s_flag)) {
+    if (!grid_barrier(bar, it, &s_flag, spin_limit)) {
       done = it;
       break;
     }
@@ -533,7 +538,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
 constexpr int kPprSub = ANOMOD_PPR_SUB;  // 256-row blocks per persistent workgroup
 using PersistentFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*,
                               const uint8_t*, const double*, double, double, double*, double*,
-                              unsigned long long*, uint32_t, double, unsigned int*);
+                              unsigned long long*, uint32_t, double, unsigned int*, uint32_t);
 PersistentFn persistent_fn(int sub) {
   return sub >= 4 ? ppr_persistent_kernel<4> : sub == 2 ? ppr_persistent_kernel<2>
                                                         : ppr_persistent_kernel<1>;
@@ -777,9 +782,11 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   // read-back per launch (r02, scripts/time_pagerank.py).  Larger graphs take
   // the graph (fixed iterations) or per-launch read-backs (tolerance).
   // ANOMOD_PPR_MODE=1 forces the per-launch paths, 2 the persistent one
-  // (tests: same bits).
+  // (tests: same bits).  ANOMOD_PPR_SUB = 256-row blocks per persistent
+  // workgroup: 1, 2 or 4 (anything else: the default).
   const char* sub_env = getenv("ANOMOD_PPR_SUB");
-  const int sub = sub_env ? atoi(sub_env) : kPprSub;
+  int sub = sub_env ? atoi(sub_env) : kPprSub;
+  if (sub != 1 && sub != 2 && sub != 4) sub = kPprSub;
   if (g->coop_blocks < 0 || g->coop_sub != sub) {
     // Workgroups resident at once.  The persistent solve is a PLAIN launch: the
     // cooperative launch API only adds a launch-time check of this same
@@ -787,9 +794,9 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     // one segfaulted at exit under rocprofv3 --kernel-trace (r01,
     // scripts/coop_exit_probe.py) — so the bound is checked here, one block
     // per CU below the occupancy answer (the hardware may admit one fewer
-    // than the API reports for 256-thread blocks), and the grid barrier's
-    // bounded spin turns a block that never became resident into an error,
-    // not a hang.
+    // than the API reports for 256-thread blocks).  Residency can still fail
+    // when another process holds CUs: the grid barrier's bounded spin then
+    // ends the launch and the solve reruns per launch (below), not a hang.
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_fn(sub),
                                                      kPprThreads * sub, 0) != hipSuccess)
@@ -799,67 +806,101 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   }
   const char* mode_env = getenv("ANOMOD_PPR_MODE");
   const int mode = mode_env ? atoi(mode_env) : 0;
+  // test knob: a tiny limit (0: no wait at all) forces the timeout and the rerun
+  const char* spin_env = getenv("ANOMOD_PPR_SPIN");
+  const long spin_v = spin_env && *spin_env ? atol(spin_env) : -1;
+  const uint32_t spin = spin_v >= 0 && spin_v < (long)kSpinLimit ? (uint32_t)spin_v : kSpinLimit;
   const uint32_t pgrid = (g->grid + sub - 1) / sub;
-  const bool persistent = (int)pgrid <= g->coop_blocks && mode != 1;
+  bool persistent = (int)pgrid <= g->coop_blocks && mode != 1;
+  unsigned int* hb = reinterpret_cast<unsigned int*>(g->h_pin + N);  // pinned, past the vector
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  g->last_path = 0;
+  bool fell_back = false;
   if (persistent) {
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
     hipLaunchKernelGGL(persistent_fn(sub), dim3(pgrid), dim3(kPprThreads * sub), 0, ctx->stream,
                        g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, x0v,
-                       g->x[0], g->x[1], g->acc, iters, ntol, g->bar);
+                       g->x[0], g->x[1], g->acc, iters, ntol, g->bar, spin);
     ANOMOD_HIP(ctx, hipGetLastError());
-  } else if (tol > 0.0) {
-    // Convergence mode: host reads the L1 change after every iteration.
-    for (uint32_t it = 0; it < iters; ++it) {
-      launch_iter(ctx, g, alpha, it);
-      ANOMOD_HIP(ctx, hipGetLastError());
-      const int w = (it + 1) % 3;
-      unsigned long long* eh = g->host_acc.data() + (3 + w) * kAccSlots;
-      ANOMOD_HIP(ctx, hipMemcpyAsync(eh, g->acc + (3 + w) * kAccSlots, kAccSlots * 8,
-                                     hipMemcpyDeviceToHost, ctx->stream));
-      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      done = it + 1;
-      unsigned long long et = 0;
-      for (int i = 0; i < kAccSlots; ++i) et += eh[i];
-      if ((double)et * (1.0 / kEScale) < (double)N * tol) break;
-    }
-  } else {
-    // Fixed-iteration mode: replay a captured graph of `iters` launches.
-    if (!g->exec || g->exec_iters != iters || g->exec_alpha != alpha) {
-      if (g->exec) ANOMOD_HIP(ctx, hipGraphExecDestroy(g->exec));
-      g->exec = nullptr;
-      hipGraph_t graph = nullptr;
-      ANOMOD_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-      for (uint32_t it = 0; it < iters; ++it) launch_iter(ctx, g, alpha, it);
-      ANOMOD_HIP(ctx, hipStreamEndCapture(ctx->stream, &graph));
-      hipError_t e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      ANOMOD_HIP(ctx, e);
-      g->exec_iters = iters;
-      g->exec_alpha = alpha;
-    }
-    ANOMOD_HIP(ctx, hipGraphLaunch(g->exec, ctx->stream));
-    done = iters;
-  }
-  if (int rc = stage_end(ctx, kStagePagerank)) return rc;
-  // the persistent solve leaves its result in x[0]: one copy, one wait
-  unsigned int* hb = reinterpret_cast<unsigned int*>(g->h_pin + N);  // pinned, past the vector
-  if (persistent)
+    if (int rc = stage_end(ctx, kStagePagerank)) return rc;  // the copies are not timed
+    // the persistent solve leaves its result in x[0]: one copy, one wait
     ANOMOD_HIP(ctx, hipMemcpyAsync(hb, g->bar, 4 * sizeof(unsigned int), hipMemcpyDeviceToHost,
                                    ctx->stream));
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[persistent ? 0 : (done & 1)], N * 8ull,
-                                 hipMemcpyDeviceToHost, ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (persistent) {
-    if (hb[1]) {
-      set_error(ctx, "PageRank grid barrier timed out (iteration %u)", hb[2]);
-      return ANOMOD_EHIP;
+    ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[0], N * 8ull, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (hb[1] == 0u) {
+      done = hb[2];
+      g->last_path = ANOMOD_PPR_PATH_PERSISTENT;
+    } else {
+      // A workgroup never became resident (another process held CUs) and the
+      // grid barrier gave up: start over from x0 on the per-launch path.  p
+      // is already normalised on the device (p / 1.0 is p); x, the slots and
+      // the barrier words are re-initialised.  Same bits as the persistent
+      // solve would have produced (tested).
+      ++g->fallbacks;
+      fell_back = true;
+      hipLaunchKernelGGL(ppr_init_norm_kernel, dim3(std::min<uint32_t>(g->grid, 1024)),
+                         dim3(kPprThreads), 0, ctx->stream, N, 1.0 / N, g->x[0], g->p, 1.0,
+                         g->acc, (uint32_t)g->host_acc.size(), acc0, g->bar,
+                         (uint32_t)kBarWords);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      persistent = false;
     }
-    done = hb[2];
+  }
+  if (!persistent) {
+    if (tol > 0.0) {
+      // Convergence mode: host reads the L1 change after every iteration.
+      for (uint32_t it = 0; it < iters; ++it) {
+        launch_iter(ctx, g, alpha, it);
+        ANOMOD_HIP(ctx, hipGetLastError());
+        const int w = (it + 1) % 3;
+        unsigned long long* eh = g->host_acc.data() + (3 + w) * kAccSlots;
+        ANOMOD_HIP(ctx, hipMemcpyAsync(eh, g->acc + (3 + w) * kAccSlots, kAccSlots * 8,
+                                       hipMemcpyDeviceToHost, ctx->stream));
+        ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        done = it + 1;
+        unsigned long long et = 0;
+        for (int i = 0; i < kAccSlots; ++i) et += eh[i];
+        if ((double)et * (1.0 / kEScale) < (double)N * tol) break;
+      }
+      g->last_path = ANOMOD_PPR_PATH_READBACK;
+    } else {
+      // Fixed-iteration mode: replay a captured graph of `iters` launches.
+      if (!g->exec || g->exec_iters != iters || g->exec_alpha != alpha) {
+        if (g->exec) ANOMOD_HIP(ctx, hipGraphExecDestroy(g->exec));
+        g->exec = nullptr;
+        hipGraph_t graph = nullptr;
+        ANOMOD_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        for (uint32_t it = 0; it < iters; ++it) launch_iter(ctx, g, alpha, it);
+        ANOMOD_HIP(ctx, hipStreamEndCapture(ctx->stream, &graph));
+        hipError_t e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        ANOMOD_HIP(ctx, e);
+        g->exec_iters = iters;
+        g->exec_alpha = alpha;
+      }
+      ANOMOD_HIP(ctx, hipGraphLaunch(g->exec, ctx->stream));
+      done = iters;
+      g->last_path = ANOMOD_PPR_PATH_GRAPH;
+    }
+    if (fell_back) g->last_path |= ANOMOD_PPR_PATH_FALLBACK;
+    // (after a fallback the stage spans the failed attempt and the rerun)
+    if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+    ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_pin, g->x[done & 1], N * 8ull, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   memcpy(x_out, g->h_pin, N * 8ull);
   if (iters_done) *iters_done = done;
+  return ANOMOD_OK;
+}
+
+int anomod_graph_last_solve(const anomod_graph* g, uint32_t* path, uint32_t* fallbacks) {
+  ANOMOD_REQUIRE(nullptr, g, "anomod_graph_last_solve: graph is NULL");
+  if (path) *path = g->last_path;
+  if (fallbacks) *fallbacks = g->fallbacks;
   return ANOMOD_OK;
 }
 

@@ -306,35 +306,25 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    tdist = None
+    group = None
     if world > 1:
-        import torch.distributed as tdist  # host-side control plane only (gloo)
+        # host-side control plane: a stdlib TCP group (no torch.distributed):
+        # the RCCL unique id, barriers and the scalar max/sum of the timings
+        from anomod import dist
 
-        tdist.init_process_group("gloo")
+        group = dist.HostGroup(rank, world)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     def barrier():
-        if tdist is not None:
-            tdist.barrier()
+        if group is not None:
+            group.barrier()
 
     def allmax(v: float) -> float:
-        if tdist is None:
-            return v
-        import torch
-
-        t = torch.tensor([v], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        return float(t.item())
+        return v if group is None else group.allreduce_scalar(v, L.OP_MAX)
 
     def allsum(v: float) -> float:
-        if tdist is None:
-            return v
-        import torch
-
-        t = torch.tensor([v], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
-        return float(t.item())
+        return v if group is None else group.allreduce_scalar(v, L.OP_SUM)
 
     staged = None
     if "tt_config2_files" in legs and world == 1:
@@ -348,9 +338,7 @@ def main() -> int:
 
     ctx = anomod.Context(local)
     if world > 1:
-        from anomod import dist
-
-        dist.attach_rccl(ctx, dist.RankInfo(rank, world, local))
+        dist.attach_rccl(ctx, dist.RankInfo(rank, world, local), group)
 
     spec = anomod.SynthSpec("SN", seed=args.seed, p_orphan_ppm=100)
     spans = ctx.generate(spec, args.traces_per_gpu, shard=rank)  # this rank's traces, in HBM
@@ -569,8 +557,8 @@ def main() -> int:
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if tdist is not None:
-        tdist.destroy_process_group()
+    if group is not None:
+        group.close()
     return 0
 
 

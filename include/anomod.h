@@ -413,6 +413,18 @@ int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, ui
 int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz);
 int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
                           uint32_t iters, double tol, double* x_out, uint32_t* iters_done);
+/* Which path the last anomod_graph_pagerank solve of g took: 1 = replayed
+ * hipGraph of per-iteration launches (fixed iterations), 2 = per-iteration
+ * launches with a host read-back of the L1 change (tolerance), 3 = one
+ * persistent launch (grid barrier); | 4 = the persistent launch timed out at
+ * its grid barrier (a workgroup never became resident, e.g. another process
+ * held CUs) and the solve was rerun from x0 on path 1 or 2 — same result
+ * bits.  fallbacks = such reruns over the graph's lifetime.              */
+#define ANOMOD_PPR_PATH_GRAPH 1
+#define ANOMOD_PPR_PATH_READBACK 2
+#define ANOMOD_PPR_PATH_PERSISTENT 3
+#define ANOMOD_PPR_PATH_FALLBACK 4
+int anomod_graph_last_solve(const anomod_graph* g, uint32_t* path, uint32_t* fallbacks);
 /* K (<= 16) personalizations solved together (replica mode, SURVEY.md §8e:
  * one vector per experiment / fault hypothesis): the CSR is read once per
  * iteration for all K.  P and X are [K][N]; every column equals its

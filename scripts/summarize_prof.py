@@ -12,6 +12,9 @@ profile summaries under profiles/:
                                     both KiB), read back by bench.py
 
 usage: python scripts/summarize_prof.py TAG [gpurun_out/prof] [gpurun_out/bench.log]
+       (scripts/profile_r03.sh layout: TAG gpurun_out/r03prof gpurun_out/r03prof/bench_profiled.log
+        — the bench line printed BY the profiled process, so the headline kernel's
+        rocprof dispatch times and ms_per_step come from one run)
 """
 from __future__ import annotations
 
@@ -25,13 +28,20 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
+# PMC runs: `bench.py --steps 2 --warmup 0 --legs ...` — the SN-width edge
+# kernel's first 2 dispatches are the headline's, later ones other legs'
+FIRST_N = {"edge_agg_kernel": 2}
+
+
 def counter(path: Path, name: str, kernel: str) -> list[float]:
     vals = []
     with open(path) as f:
         for r in csv.DictReader(f):
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == name:
-                vals.append(float(r["Counter_Value"]))
-    return vals
+                vals.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    vals.sort()
+    n = FIRST_N.get(kernel)
+    return [v for _, v in (vals[:n] if n else vals)]
 
 
 def main() -> int:
@@ -64,6 +74,12 @@ def main() -> int:
             l = e["W"] * 64 // math.gcd(e["W"], 64)
             seg = max(l, 16384 // l * l)
             per_unit["ewma_zt_kernel"] = -(-e["steps_per_chunk"] // seg)
+        if "ungrouped" in bench:
+            # a radix pass reads and writes one 32-B record per span; every pass
+            # but the last also writes the next pass's 1-B digit
+            u = bench["ungrouped"]
+            P = u["radix_passes"]
+            alg["group_scatter_kernel"] = (64 + (P - 1) / P) * u["spans"]
     kernels = {}
     for k, a in alg.items():
         fetch = counter(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)
@@ -90,8 +106,10 @@ def main() -> int:
                 acc: dict = {}
                 for r in csv.DictReader(f):
                     if k in r["Kernel_Name"]:
-                        acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+                        acc.setdefault(r["Counter_Name"], []).append(
+                            (int(r["Dispatch_Id"]), float(r["Counter_Value"])))
             for name, v in acc.items():
+                v = [x for _, x in sorted(v)][:FIRST_N.get(k, len(v))]
                 sq[name] = sum(v) / len(v)
         if sq:
             if sq.get("SQ_WAVE_CYCLES"):
@@ -122,8 +140,15 @@ def main() -> int:
                   "rocprof_min_ms": min(timed), "rocprof_max_ms": max(timed),
                   "bench_hipevent_kernel_ms": bench["roofline"]["kernel_ms"],
                   "bench_ms_per_step": bench["ms_per_step"],
-                  "note": "the profiled run repeats the bench command on the same box right "
+                  "bytes_per_launch": bench["roofline"]["bytes_per_launch"],
+                  "line_frac": bench["roofline"]["frac"],
+                  "note": "bench line and dispatch times from the same profiled process"
+                          if "bench_profiled" in blog.name else
+                          "the profiled run repeats the bench command on the same box right "
                           "after the unprofiled bench run"}
+            hk["frac_from_rocprof_avg"] = hk["bytes_per_launch"] / (hk["rocprof_avg_ms"] * 1e-3) / 8e12
+            hk["frac_rel_diff"] = hk["frac_from_rocprof_avg"] / hk["line_frac"] - 1.0
+            hk["avg_le_ms_per_step"] = hk["rocprof_avg_ms"] <= hk["bench_ms_per_step"]
             (out / f"{tag}_headline_kernel.json").write_text(json.dumps(hk, indent=1) + "\n")
             print(json.dumps(hk, indent=1))
     if kernels:

@@ -45,10 +45,11 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
         t = torch.from_numpy(tab[key].astype(np.int64))
         tdist.all_reduce(t, op=op)
         tab[key] = t.numpy()
-    # rendezvous of an RCCL-style unique id over the same group
-    uid = bytes(range(128)) if rank == 0 else None
-    got = dist.torch_exchange(uid)
-    assert got == bytes(range(128))
+    # an RCCL-style unique id handed to attach_rccl's exchange hook over gloo
+    # (the product's default is dist.HostGroup: tests/test_dist_host.py)
+    obj = [bytes(range(128)) if rank == 0 else None]
+    tdist.broadcast_object_list(obj, src=0)
+    assert obj[0] == bytes(range(128))
     if rank == 0:
         np.savez(os.path.join(out_dir, "merged.npz"), n_part=part.n_spans, **tab)
     tdist.barrier()

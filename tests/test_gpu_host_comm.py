@@ -1,6 +1,6 @@
 """GPU: libanomod's multi-rank path with two ranks on one device, through the
 host collective transport (anomod_ctx_attach_host_comm, driven by gloo via
-anomod.dist.attach_gloo) — RCCL refuses two ranks on a GPU, so this is how
+anomod.dist.attach_host over a stdlib TCP HostGroup) — RCCL refuses two ranks on a GPU, so this is how
 the 1-GPU box runs the collective sequence with nranks = 2:
 
 * edge table: traceId-hash shards, status agreement, u64 sum /
@@ -32,16 +32,15 @@ _WORKER = textwrap.dedent("""
     import os, sys
     sys.path[:0] = [{pkg!r}, {root!r}]
     import numpy as np
-    import torch.distributed as tdist
     import anomod
     from anomod import dist
-    tdist.init_process_group("gloo")
     info = dist.rank_from_env()
+    grp = dist.HostGroup(info.rank, info.world)
     out = {{}}
     sp = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=9, p_orphan_ppm=3000), 30000)
     part = dist.shard_spans(sp, info)
     with anomod.Context(0) as c:
-        dist.attach_gloo(c, info)
+        dist.attach_host(c, grp)
         assert c.comm_info() == (2, info.rank)
         t = c.edge_aggregate(part)
         for k in ("count", "errors", "sum_us", "min_us", "max_us", "hist", "p50_us", "p99_us"):
@@ -67,17 +66,20 @@ _WORKER = textwrap.dedent("""
         ug.free()
         dev.free()
         # row-sharded PageRank over the two ranks vs this rank's unsharded solve
-        os.environ["ANOMOD_PPR_MODE"] = "1"
+        # (default path: the persistent solve beside the other rank's process,
+        # rerun per launch if a workgroup cannot become resident)
         g = anomod.DeviceGraph(c, synthetic=(30000, 8, 6))
         p = np.random.default_rng(1).random(g.N)
         for iters, tol in ((37, 0.0), (1000, 1e-10)):
             xs, ds = g.pagerank_sharded(p, iters=iters, tol=tol)
             x, d = g.pagerank(p, iters=iters, tol=tol)
             out[f"ppr_eq_{{iters}}"] = int(np.array_equal(xs, x) and ds == d)
+            out[f"ppr_path_{{iters}}"] = g.last_solve()[0]
         g.free()
     np.savez(os.path.join({out!r}, f"rank{{info.rank}}.npz"), **out)
-    tdist.barrier()
-    tdist.destroy_process_group()
+    grp.barrier()
+    grp.close()
+    assert "torch" not in sys.modules
 """)
 
 

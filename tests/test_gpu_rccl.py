@@ -4,7 +4,7 @@ own communicator.
 * one rank: a 1-rank communicator runs the same ncclGroupStart / AllReduce
   (u64 sum, u32 min, u32 max) / GroupEnd sequence as N ranks;
 * two ranks: two processes (one per GPU when the box has two, else both on
-  GPU 0), gloo rendezvous of the unique id (as bench.py does), traceId-hash
+  GPU 0), the unique id through a stdlib TCP HostGroup (as bench.py does), traceId-hash
   shards, merged table == the oracle's unsharded table bit for bit.  RCCL
   refuses two ranks on one device ("invalid usage", measured on the 1-GPU
   box); that refusal is reported as a skip with RCCL's own message.
@@ -39,21 +39,20 @@ _WORKER = textwrap.dedent("""
     import os, sys
     sys.path[:0] = [{pkg!r}, {root!r}]
     import numpy as np
-    import torch.distributed as tdist
     import anomod
     from anomod import dist
-    tdist.init_process_group("gloo")
     info = dist.rank_from_env()
+    grp = dist.HostGroup(info.rank, info.world)
     sp = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=9, p_orphan_ppm=3000), 30000)
     part = dist.shard_spans(sp, info)
     with anomod.Context(info.rank % anomod.device_count()) as c:
-        dist.attach_rccl(c, info)
+        dist.attach_rccl(c, info, grp)
         t = c.edge_aggregate(part)
     np.savez(os.path.join({out!r}, f"rank{{info.rank}}.npz"), count=t.count, errors=t.errors,
              sum_us=t.sum_us, min_us=t.min_us, max_us=t.max_us, hist=t.hist,
              p50_us=t.p50_us, p99_us=t.p99_us, n_part=part.n_spans)
-    tdist.barrier()
-    tdist.destroy_process_group()
+    grp.barrier()
+    grp.close()
 """)
 
 

@@ -204,6 +204,31 @@ def test_pagerank_persistent_equals_per_launch(ctx, monkeypatch, sub):
     g.free()
 
 
+def test_pagerank_persistent_timeout_falls_back(ctx, monkeypatch):
+    """A persistent solve whose grid barrier times out (forced: ANOMOD_PPR_SPIN=0,
+    no block waits) reruns in-process on the per-launch path and still returns
+    the per-launch bits; the path is recorded.  Without the knob the default
+    path is the persistent one again."""
+    g = anomod.DeviceGraph(ctx, synthetic=(100000, 7, 3))
+    p = np.random.default_rng(5).random(g.N)
+    cases = ((37, 0.0, "graph"), (1000, 1e-10, "readback"))
+    monkeypatch.setenv("ANOMOD_PPR_MODE", "1")
+    ref = [g.pagerank(p, iters=it, tol=tol) for it, tol, _ in cases]
+    monkeypatch.delenv("ANOMOD_PPR_MODE")
+    monkeypatch.setenv("ANOMOD_PPR_SPIN", "0")
+    fb0 = g.last_solve()[1]
+    for k, ((it, tol, path), (xr, dr)) in enumerate(zip(cases, ref)):
+        x, d = g.pagerank(p, iters=it, tol=tol)
+        assert g.last_solve() == ("fallback:" + path, fb0 + k + 1)
+        assert d == dr
+        np.testing.assert_array_equal(x, xr)
+    monkeypatch.delenv("ANOMOD_PPR_SPIN")
+    x, d = g.pagerank(p, iters=37)
+    assert g.last_solve()[0] == "persistent"
+    np.testing.assert_array_equal(x, ref[0][0])
+    g.free()
+
+
 @pytest.mark.parametrize("K", [1, 3, 8, 16])
 def test_pagerank_batch_equals_single_solves(ctx, K):
     g = anomod.DeviceGraph(ctx, synthetic=(30000, 8, 5))
