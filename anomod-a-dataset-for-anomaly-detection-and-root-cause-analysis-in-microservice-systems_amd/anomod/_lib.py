@@ -168,6 +168,7 @@ _SIGS = {
     "anomod_trace_structure_spans": (_i32, [_vp, _vp, _P(TraceStructC)]),
     "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),
     "anomod_value_summary": (_i32, [_vp, _P(C.c_double), _u64, C.c_int, _P(ValueSummaryC)]),
+    "anomod_sort_u64": (_i32, [_vp, _P(_u64), _u64, C.c_int, C.c_int, _P(_u64), _P(C.c_int)]),
     "anomod_response_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_uint8), _P(C.c_double),
                                        _u64, _P(ResponseSummaryC)]),
     "anomod_segment_summary": (_i32, [_vp, _P(_u32), _P(_u32), _P(C.c_int32), _P(C.c_int64),

@@ -175,6 +175,17 @@ class Context:
         self._check(self._lib.anomod_ctx_comm_info(self.handle, C.byref(n), C.byref(r)))
         return n.value, r.value
 
+    def sort_u64(self, keys, begin_bit: int = 0, end_bit: int = 64) -> tuple[np.ndarray, int]:
+        """Stable device radix sort of u64 keys by bits [begin_bit, end_bit)
+        (csrc/radix.hip) -> (sorted keys, digit passes run)."""
+        k = np.ascontiguousarray(keys, np.uint64)
+        out = np.empty_like(k)
+        passes = C.c_int()
+        self._check(self._lib.anomod_sort_u64(self.handle, L.ptr(k, C.c_uint64), k.size,
+                                              begin_bit, end_bit, L.ptr(out, C.c_uint64),
+                                              C.byref(passes)))
+        return out, passes.value
+
     def attach_host_comm(self, nranks: int, rank: int, allreduce, allgather):
         """Host collective transport instead of RCCL: ``allreduce(buf, dtype,
         op)`` reduces a numpy array in place over all ranks, ``allgather(buf,

@@ -90,7 +90,7 @@ def load_experiment(source, *, metrics=None, name: str | None = None,
     ``source`` is one of
       * a :class:`SynthSpec` — synthetic SN/TT spans (``n_traces`` traces,
         default 600 = 50 per SN service as collect_trace.sh:18/:49 scrapes)
-        plus a synthetic metric matrix;
+        over the services they name, plus a synthetic metric matrix;
       * a Jaeger dump (``all_traces.json``) or its directory
         (SN_data/trace_data/<exp>_traces_<ts>/);
       * a SkyWalking payload JSON (TT_data/trace_data/<exp>/*.json) or its
@@ -104,6 +104,10 @@ def load_experiment(source, *, metrics=None, name: str | None = None,
         fault = source.fault_service
         if isinstance(fault, int):
             fault = spans.services[fault]
+        # the services the traces name, as a collector payload lists them
+        # (services_discovered, trace_collector.py:572): the same experiment
+        # read back from its files has the same service list
+        spans = spans.observed_services()
         X = _synthetic_metrics(spans.services, metric_steps, series_per_service,
                                source.seed ^ 0x5EED, fault) if metric_steps else None
         return Experiment(name or f"synthetic_{source.topology}", spans, X, fault,

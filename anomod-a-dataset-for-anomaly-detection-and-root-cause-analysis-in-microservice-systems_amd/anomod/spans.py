@@ -92,6 +92,20 @@ class SpanSet:
         h[nz] = self.trace_hash[first[nz]]
         return self.select_traces((h % np.uint64(nshards)) == np.uint64(rank))
 
+    def observed_services(self) -> "SpanSet":
+        """The same spans over only the services they name (names stay sorted,
+        ids renumbered) — what a collector payload records as
+        metadata.services_discovered = sorted(union of observed services),
+        trace_collector.py:572."""
+        used = np.unique(self.svc)
+        if used.shape[0] == len(self.services):
+            return self
+        remap = np.zeros(len(self.services), np.uint16)
+        remap[used] = np.arange(used.shape[0], dtype=np.uint16)
+        return SpanSet([self.services[i] for i in used.tolist()], self.trace_ptr, self.trace_hash,
+                       self.span_id, self.parent_span_id, remap[self.svc], self.flags,
+                       self.dur_us, self.trace_ids)
+
     def take(self, order: np.ndarray, trace_ptr: np.ndarray) -> "SpanSet":
         """The spans in `order`, split into traces by `trace_ptr`."""
         return SpanSet(self.services, trace_ptr, self.trace_hash[order], self.span_id[order],

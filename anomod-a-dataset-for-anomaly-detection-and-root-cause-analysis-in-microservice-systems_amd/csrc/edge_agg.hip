@@ -39,10 +39,10 @@
 #include <cstring>
 #include <limits>
 
-#include <hipcub/hipcub.hpp>
 
 #include "chunk.h"
 #include "common.h"
+#include "radix.h"
 
 namespace anomod {
 namespace {
@@ -1126,11 +1126,7 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
   // One workspace: keys | sorted keys | sort temp | q | out | count | ctr +
   // long-trace counters | long-trace list
   const uint64_t big_cap = big_capacity(spans);
-  size_t sort_tmp = 0;
-  if (n)
-    ANOMOD_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(
-                        nullptr, sort_tmp, (const unsigned long long*)nullptr,
-                        (unsigned long long*)nullptr, n, 0, 32 + kbits, ctx->stream));
+  const size_t sort_tmp = n ? radix_temp_bytes(n) : 0;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t b_keys = al(n * 8), b_tmp = al(sort_tmp), b_q = al(nq * 4), b_out = al(E * nq * 8ull),
                b_cnt = al(E * 8ull);
@@ -1178,8 +1174,9 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
     if (e == hipSuccess && rc == ANOMOD_OK && big_cap)
       e = launch_big<kHtKeys, kStHbm>(ctx, spans, S, E, tab);
     if (e == hipSuccess && rc == ANOMOD_OK)
-      e = hipcub::DeviceRadixSort::SortKeys(tmp, sort_tmp, keys, sorted, n, 0, 32 + kbits,
-                                             ctx->stream);
+      e = radix_sort_u64(reinterpret_cast<const uint64_t*>(keys),
+                         reinterpret_cast<uint64_t*>(sorted), n, 0, 32 + kbits, tmp, sort_tmp,
+                         ctx->stream);
   }
   if (e == hipSuccess && rc == ANOMOD_OK) {
     hipLaunchKernelGGL(exact_pick_kernel, dim3((E + 255) / 256), dim3(256), 0, ctx->stream,

@@ -8,42 +8,34 @@
 // (x[n//2], x[int(n*0.95)], x[int(n*0.99)]) plus min / max / sum / count.
 //
 // Value summary: select (v > 0, generate_summary :167-169; or every non-NaN
-// value, generate_reports :324) -> LSD radix sort of the f64 keys -> one
-// deterministic tree sum over the sorted keys -> five gathers.  Order
-// statistics are exact (the sorted values themselves); the sum is a fixed
-// tree over the sorted order, reproducible run to run, and within
-// n * 2^-53 relative of Python's left-to-right sum.  HBM: the radix sort's
-// passes dominate (8 B/value read + written per 8-bit digit pass, plus the
-// selection's 8 + 8 B/value).
+// value, generate_reports :324) into order-preserving u64 keys -> the
+// hand-written LSD radix sort of radix.hip -> one fixed-order sum over the
+// sorted keys -> five gathers.  Order statistics are exact (the sorted values
+// themselves); the sum is reproducible run to run and within n * 2^-53
+// relative of Python's left-to-right sum.  HBM: the radix sort's passes
+// dominate (8 B/key counted + 16 B/key scattered per varying 8-bit digit,
+// plus the selection's 8 + 8 + 8 B/value).
 // Response summary: the status-code / content-type counts and the error
 // count (:163-177) in one pass with LDS-privatised integer counters, plus the
 // value summary of the positive latencies.
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <cmath>
 
 #include "common.h"
+#include "radix.h"
 
 namespace anomod {
 namespace {
 
-struct SelectPositive {
-  __device__ bool operator()(double v) const { return v > 0.0; }
-};
-struct SelectNumber {
-  __device__ bool operator()(double v) const { return v == v; }
-};
-
-// sorted[0], sorted[c-1] and the three nearest-rank picks
-__global__ void pick_kernel(const double* __restrict__ sorted, uint64_t c, uint64_t i50,
+// sorted[0], sorted[c-1] and the three nearest-rank picks (keys -> values)
+__global__ void pick_kernel(const uint64_t* __restrict__ sorted, uint64_t c, uint64_t i50,
                             uint64_t i95, uint64_t i99, double* __restrict__ out) {
   if (threadIdx.x == 0) {
-    out[0] = sorted[0];
-    out[1] = sorted[c - 1];
-    out[2] = sorted[i50];
-    out[3] = sorted[i95];
-    out[4] = sorted[i99];
+    out[0] = key_f64(sorted[0]);
+    out[1] = key_f64(sorted[c - 1]);
+    out[2] = key_f64(sorted[i50]);
+    out[3] = key_f64(sorted[i95]);
+    out[4] = key_f64(sorted[i99]);
   }
 }
 
@@ -99,61 +91,36 @@ CatFn pick_category_kernel(uint32_t na, uint32_t nb) {
 uint64_t py_rank(uint64_t c, double q) { return (uint64_t)((double)c * q); }
 
 // The value summary of n device values already at `vals` (device scratch
-// `work` of 2n doubles + temp allocated here).  Runs on ctx->stream.
+// allocated here).  Runs on ctx->stream.
 int value_summary_device(anomod_ctx* ctx, const double* vals, uint64_t n, int positive_only,
                          anomod_value_summary_out* out) {
   *out = anomod_value_summary_out{};
   if (n == 0) return ANOMOD_OK;
-  double *sel = nullptr, *sorted = nullptr, *res = nullptr;
-  uint64_t* d_count = nullptr;
-  void* temp = nullptr;
-  size_t tb_sel = 0, tb_sort = 0, tb_sum = 0;
-  hipError_t e = hipSuccess;
-  if (positive_only)
-    e = hipcub::DeviceSelect::If(nullptr, tb_sel, vals, sel, d_count, (int64_t)n,
-                                 SelectPositive{}, ctx->stream);
-  else
-    e = hipcub::DeviceSelect::If(nullptr, tb_sel, vals, sel, d_count, (int64_t)n,
-                                 SelectNumber{}, ctx->stream);
-  if (e == hipSuccess)
-    e = hipcub::DeviceRadixSort::SortKeys(nullptr, tb_sort, sel, sorted, (int64_t)n, 0, 64,
-                                          ctx->stream);
-  if (e == hipSuccess)
-    e = hipcub::DeviceReduce::Sum(nullptr, tb_sum, sorted, res, (int64_t)n, ctx->stream);
-  if (e != hipSuccess) {
-    set_error(ctx, "hipcub temp-size query failed: %s", hipGetErrorString(e));
-    return ANOMOD_EHIP;
-  }
-  const size_t tb = std::max(tb_sel, std::max(tb_sort, tb_sum));
-  const size_t bytes = 2 * n * 8 + 8 * 8 + tb;
+  const size_t tb = std::max(radix_temp_bytes(n),
+                             std::max(select_temp_bytes(n), sum_temp_bytes(n)));
+  const size_t keys_b = (n * 8 + 255) & ~size_t(255);
+  const size_t bytes = 2 * keys_b + 256 + tb;
   char* base = nullptr;
   if (hipMalloc(&base, bytes) != hipSuccess) {
     set_error(ctx, "hipMalloc(%zu) for the value summary failed", bytes);
     return ANOMOD_ENOMEM;
   }
-  sel = reinterpret_cast<double*>(base);
-  sorted = sel + n;
-  res = sorted + n;                                     // [0..4] picks, [5] sum
-  d_count = reinterpret_cast<uint64_t*>(res + 6);
-  temp = reinterpret_cast<void*>(res + 8);
-  uint64_t c = 0;
+  auto* sel = reinterpret_cast<uint64_t*>(base);
+  auto* sorted = reinterpret_cast<uint64_t*>(base + keys_b);
+  auto* res = reinterpret_cast<double*>(base + 2 * keys_b);  // [0..4] picks, [5] sum
+  auto* d_count = reinterpret_cast<unsigned long long*>(res + 6);
+  void* temp = base + 2 * keys_b + 256;
+  unsigned long long c = 0;
   double h[6] = {0, 0, 0, 0, 0, 0};
+  hipError_t e = hipSuccess;
   int rc = stage_begin(ctx, kStageSummary);
   if (rc == ANOMOD_OK) {
-    size_t t = tb;
-    e = positive_only ? hipcub::DeviceSelect::If(temp, t, vals, sel, d_count, (int64_t)n,
-                                                 SelectPositive{}, ctx->stream)
-                      : hipcub::DeviceSelect::If(temp, t, vals, sel, d_count, (int64_t)n,
-                                                 SelectNumber{}, ctx->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(&c, d_count, 8, hipMemcpyDeviceToHost, ctx->stream);
+    e = select_f64_keys(vals, n, positive_only, sel, d_count, temp, tb, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&c, d_count, 8, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess && c > 0) {
-      t = tb;
-      e = hipcub::DeviceRadixSort::SortKeys(temp, t, sel, sorted, (int64_t)c, 0, 64, ctx->stream);
-      t = tb;
-      if (e == hipSuccess)
-        e = hipcub::DeviceReduce::Sum(temp, t, sorted, res + 5, (int64_t)c, ctx->stream);
+      e = radix_sort_u64(sel, sorted, c, 0, 64, temp, tb, ctx->stream);
+      if (e == hipSuccess) e = sum_keys_f64(sorted, c, res + 5, temp, tb, ctx->stream);
       if (e == hipSuccess) {
         hipLaunchKernelGGL(pick_kernel, dim3(1), dim3(64), 0, ctx->stream, sorted, c, c / 2,
                            py_rank(c, 0.95), py_rank(c, 0.99), res);
@@ -211,6 +178,36 @@ int anomod_value_summary(anomod_ctx* ctx, const double* values, uint64_t n, int 
   if (rc == ANOMOD_OK) rc = value_summary_device(ctx, d, n, positive_only, out);
   (void)hipFree(d);
   return rc;
+}
+
+int anomod_sort_u64(anomod_ctx* ctx, const uint64_t* keys, uint64_t n, int begin_bit,
+                    int end_bit, uint64_t* sorted, int* passes) {
+  ANOMOD_REQUIRE(nullptr, ctx, "anomod_sort_u64: NULL context");
+  ANOMOD_REQUIRE(ctx, n == 0 || (keys && sorted), "anomod_sort_u64: NULL buffer");
+  ANOMOD_REQUIRE(ctx, 0 <= begin_bit && begin_bit <= end_bit && end_bit <= 64,
+                 "bit range [%d, %d) outside [0, 64]", begin_bit, end_bit);
+  ANOMOD_REQUIRE(ctx, n <= 0xFFFFFFFFull - 4096, "anomod_sort_u64: at most 2^32 - 4096 keys");
+  if (passes) *passes = 0;
+  if (n == 0) return ANOMOD_OK;
+  if (int rc = bind(ctx)) return rc;
+  const size_t kb = (n * 8 + 255) & ~size_t(255), tb = radix_temp_bytes(n);
+  char* d = nullptr;
+  if (hipMalloc(&d, kb + tb) != hipSuccess) {
+    set_error(ctx, "hipMalloc(%zu) for the sort failed", kb + tb);
+    return ANOMOD_ENOMEM;
+  }
+  auto* k = reinterpret_cast<uint64_t*>(d);
+  hipError_t e = hipMemcpyAsync(k, keys, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = radix_sort_u64(k, k, n, begin_bit, end_bit, d + kb, tb, ctx->stream,
+                                          passes);
+  if (e == hipSuccess) e = hipMemcpyAsync(sorted, k, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error(ctx, "anomod_sort_u64 failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
+  return ANOMOD_OK;
 }
 
 int anomod_response_summary(anomod_ctx* ctx, const uint32_t* status_id, const uint32_t* ctype_id,

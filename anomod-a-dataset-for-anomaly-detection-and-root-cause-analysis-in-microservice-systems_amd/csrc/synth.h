@@ -25,6 +25,7 @@ struct TopoView {
   const uint16_t* span_svc = nullptr;    // [total]
   const uint16_t* span_op = nullptr;     // [total]
   const uint32_t* dur_q = nullptr;       // [n_ops * kDurQuantiles] microseconds
+  uint32_t dur_quant = 1;                // durations are whole multiples of this (us)
 };
 
 struct SynthParams {
@@ -113,7 +114,11 @@ __host__ __device__ inline SynthSpan synth_span(const TopoView& tp, const SynthP
   uint64_t d = (uint64_t)base + (c[3] % (base / 16u + 1u));
   const bool faulty = (uint32_t)s.svc == sp.fault_svc;
   if (faulty) d *= sp.fault_mult;
-  s.dur_us = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+  if (d > 0xFFFFFFFFull) d = 0xFFFFFFFFull;
+  // TrainTicket: SkyWalking records whole milliseconds (duration = end_ms -
+  // start_ms, trace_collector.py:87), so the topology's durations are floored
+  // to a multiple of 1000 us, as the decoder reads them back (ms x 1000)
+  s.dur_us = (uint32_t)(d - d % tp.dur_quant);
   const uint32_t thr = faulty ? sp.thr_fault_err : sp.thr_err;
   s.flags = (c[1] < thr) ? (uint16_t)ANOMOD_FLAG_ERROR : (uint16_t)0;
   return s;

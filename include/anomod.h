@@ -351,6 +351,14 @@ typedef struct {
 } anomod_value_summary_out;
 int anomod_value_summary(anomod_ctx* ctx, const double* values, uint64_t n, int positive_only,
                          anomod_value_summary_out* out);
+/* The device sort under the exact-order-statistic paths (the exact per-edge
+ * quantiles and the value summary above): a stable LSD radix sort of n u64
+ * keys by bits [begin_bit, end_bit) (every key < 2^end_bit), hand-written
+ * for CDNA4 (csrc/radix.hip).  Host buffers in and out (may alias);
+ * *passes (may be NULL) = 8-bit digit passes run (digits equal in every key
+ * are skipped).                                                            */
+int anomod_sort_u64(anomod_ctx* ctx, const uint64_t* keys, uint64_t n, int begin_bit,
+                    int end_bit, uint64_t* sorted, int* passes);
 /* generate_summary's distributions in the same pass: status_id / ctype_id
  * index the caller's first-appearance lists of status codes and content
  * types (content_type.split(';')[0], 'unknown' when absent: :163-173),

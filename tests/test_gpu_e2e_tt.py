@@ -74,3 +74,27 @@ def test_tt_files_to_ranking(ctx, tmp_path):
     assert fe.window_scores.shape == (480 // 60, exp.metrics.S)
     ranking = anomod.rank(fe, ctx=ctx)
     assert anomod.hit_at(ranking, FAULT, 3) == 1.0
+
+
+def test_tt_files_rank_as_memory(ctx, tmp_path):
+    """Config 2 from files == config 2 from memory on the GPU: the staged
+    experiment (whole-ms durations, services_discovered) gives the in-memory
+    edge table bit for bit and the same ranking vector, with the same
+    baseline on both sides."""
+    from test_tt_file_roundtrip import stage
+
+    from test_gpu_edge import assert_table_equal
+
+    base_m, bd, bm = stage(tmp_path, i=0, fault=None)
+    exp_m, fd, fm = stage(tmp_path, i=3, fault="ts-order-service")
+    base_f = anomod.load_experiment(bd, metrics=bm)
+    exp_f = anomod.load_experiment(fd, metrics=fm)
+    fb_m, fb_f = anomod.features(base_m, ctx), anomod.features(base_f, ctx)
+    fe_m = anomod.features(exp_m, ctx, baseline=fb_m)
+    fe_f = anomod.features(exp_f, ctx, baseline=fb_f)
+    assert fe_f.edges.services == fe_m.edges.services
+    ref = {k: getattr(fe_m.edges, k) for k in ("count", "errors", "sum_us", "min_us", "max_us",
+                                               "hist")}
+    assert_table_equal(fe_f.edges, ref)
+    np.testing.assert_array_equal(fe_f.service_scores, fe_m.service_scores)
+    assert anomod.rank(fe_f, ctx=ctx) == anomod.rank(fe_m, ctx=ctx)
