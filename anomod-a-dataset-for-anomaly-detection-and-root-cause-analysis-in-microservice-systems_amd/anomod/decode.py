@@ -387,18 +387,36 @@ def _metrics_from_handle(h) -> MetricMatrix:
     return MetricMatrix(X, ts, series)
 
 
-def map_file(path):
-    """A file's bytes for the native decoders without a copy into Python: a
-    private, pre-faulted (MAP_POPULATE) read-only-in-practice mapping, as a
-    ctypes char array (the mapping lives as long as the array).  Empty files
-    give b''."""
-    with open(path, "rb") as fh:
-        n = os.fstat(fh.fileno()).st_size
-        if n == 0:
+class MappedFile:
+    """A file's bytes for the native decoders without a copy: a read-only
+    shared mapping (PROT_READ, so the pages stay the page cache's own — a
+    private writable mapping would copy every page at fault time).  Slicing
+    gives bytes; ``as_arg()`` is the address for a ``const char*`` parameter
+    (valid while this object lives)."""
+
+    def __init__(self, path):
+        with open(path, "rb") as fh:
+            self.size = os.fstat(fh.fileno()).st_size
+            self._mm = (mmap.mmap(fh.fileno(), self.size, prot=mmap.PROT_READ)
+                        if self.size else None)
+        self._view = (np.frombuffer(self._mm, np.uint8) if self._mm is not None
+                      else np.zeros(0, np.uint8))
+
+    def __len__(self) -> int:
+        return self.size
+
+    def __getitem__(self, sl) -> bytes:
+        return self._mm[sl] if self._mm is not None else b""[sl]
+
+    def as_arg(self):
+        if self._mm is None:
             return b""
-        mm = mmap.mmap(fh.fileno(), n, flags=mmap.MAP_PRIVATE | getattr(mmap, "MAP_POPULATE", 0),
-                       prot=mmap.PROT_READ | mmap.PROT_WRITE)
-    return (C.c_char * n).from_buffer(mm)
+        return C.cast(C.c_void_p(self._view.ctypes.data), C.c_char_p)
+
+
+def map_file(path) -> MappedFile:
+    """A file mapped read-only for the native decoders (see MappedFile)."""
+    return MappedFile(path)
 
 
 def decode_metric_long_csv_native(path_or_bytes) -> MetricMatrix:
@@ -438,7 +456,7 @@ def decode_prometheus_csv_dir_native(directory) -> MetricMatrix:
 # decoders above, without a Python object per span
 # --------------------------------------------------------------------------
 
-def decode_native(data: bytes, kind: str, services: list[str] | None = None) -> SpanSet:
+def decode_native(data: "bytes | MappedFile", kind: str, services: list[str] | None = None) -> SpanSet:
     """A Jaeger dump (kind 'jaeger') or a SkyWalking collector payload
     (kind 'skywalking') -> SpanSet, parsed by the native decoder."""
     lib = L.lib()
@@ -447,7 +465,8 @@ def decode_native(data: bytes, kind: str, services: list[str] | None = None) -> 
     if services is not None:
         names = (C.c_char_p * max(1, len(services)))(*[s.encode() for s in services])
     h = C.c_void_p()
-    L.check(fn(data, len(data), names, 0 if services is None else len(services), C.byref(h)))
+    arg = data.as_arg() if isinstance(data, MappedFile) else data
+    L.check(fn(arg, len(data), names, 0 if services is None else len(services), C.byref(h)))
     try:
         ns, nt, nsv = C.c_uint64(), C.c_uint64(), C.c_uint32()
         L.check(lib.anomod_decoded_info(h, C.byref(ns), C.byref(nt), C.byref(nsv)))

@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -789,24 +790,30 @@ bool decode_parallel(const char* json, size_t len, int kind, anomod_decoded* out
   cut.push_back(elems.size());
   std::vector<anomod_decoded> part(threads);
   names.assign(threads, Names());
-  std::vector<char> ok(threads, 1);
+  std::vector<char> ok(threads, 1), oom(threads, 0);
   std::vector<std::thread> pool;
   for (int t = 0; t < threads; ++t) {
     pool.emplace_back([&, t] {
-      Dom d;
-      std::unordered_map<std::string, std::string> proc;
-      std::unordered_map<std::string, uint64_t> first;
-      for (size_t k = cut[t]; k < cut[t + 1]; ++k) {
-        if (!d.parse(json + elems[k].b, elems[k].e - elems[k].b)) {
-          ok[t] = 0;
-          return;
+      try {  // an exception must not leave a worker thread (std::terminate)
+        Dom d;
+        std::unordered_map<std::string, std::string> proc;
+        std::unordered_map<std::string, uint64_t> first;
+        for (size_t k = cut[t]; k < cut[t + 1]; ++k) {
+          if (!d.parse(json + elems[k].b, elems[k].e - elems[k].b)) {
+            ok[t] = 0;
+            return;
+          }
+          if (kind == 0) jaeger_trace(d, 0, &part[t], names[t], proc);
+          else skywalking_trace(d, 0, &part[t], names[t], first);
         }
-        if (kind == 0) jaeger_trace(d, 0, &part[t], names[t], proc);
-        else skywalking_trace(d, 0, &part[t], names[t], first);
+      } catch (const std::bad_alloc&) {
+        oom[t] = 1;
       }
     });
   }
   for (auto& th : pool) th.join();
+  for (int t = 0; t < threads; ++t)
+    if (oom[t]) throw std::bad_alloc();  // reported by decode_common as ANOMOD_ENOMEM
   for (int t = 0; t < threads; ++t)
     if (!ok[t]) return false;
   size_t ns = 0, nt = 0;
@@ -836,14 +843,29 @@ bool decode_parallel(const char* json, size_t len, int kind, anomod_decoded* out
 
 thread_local std::string g_decode_err;
 
+int decode_common_impl(const char* json, uint64_t len, const char* const* services,
+                       uint32_t n_services, int kind, anomod_decoded** out);
+
 int decode_common(const char* json, uint64_t len, const char* const* services, uint32_t n_services,
                   int kind, anomod_decoded** out) {
+  try {
+    return decode_common_impl(json, len, services, n_services, kind, out);
+  } catch (const std::bad_alloc&) {
+    if (out) *out = nullptr;
+    anomod::set_error(nullptr, "anomod_decode: out of host memory");
+    return ANOMOD_ENOMEM;
+  }
+}
+
+int decode_common_impl(const char* json, uint64_t len, const char* const* services,
+                       uint32_t n_services, int kind, anomod_decoded** out) {
   if (!out || (!json && len)) {
     anomod::set_error(nullptr, "anomod_decode: NULL argument");
     return ANOMOD_EINVAL;
   }
   *out = nullptr;
-  auto* res = new anomod_decoded();
+  std::unique_ptr<anomod_decoded> owned(new anomod_decoded());  // freed if anything throws
+  anomod_decoded* res = owned.get();
   std::vector<Names> names;
   const int threads = decode_threads();
   if (threads <= 1 || len < (64u << 10) ||
@@ -852,13 +874,11 @@ int decode_common(const char* json, uint64_t len, const char* const* services, u
     names.assign(1, Names());
     Dom d;
     if (!d.parse(json, (size_t)len)) {
-      delete res;
       anomod::set_error(nullptr, "anomod_decode: %s", d.err.c_str());
       return ANOMOD_EINVAL;
     }
     std::string err;
     if (!decode_sequential(d, kind, res, names[0], err)) {
-      delete res;
       anomod::set_error(nullptr, "anomod_decode: %s", err.c_str());
       return ANOMOD_EINVAL;
     }
@@ -872,17 +892,15 @@ int decode_common(const char* json, uint64_t len, const char* const* services, u
   resolve_names(parts, services ? &fixed : nullptr, res);
   for (uint16_t v : res->svc) {
     if (v == 0xFFFF) {
-      delete res;
       anomod::set_error(nullptr, "anomod_decode: a span's service is not in the service list");
       return ANOMOD_EINVAL;
     }
   }
   if (res->services.size() > 0xFFFF) {
-    delete res;
     anomod::set_error(nullptr, "anomod_decode: more than 65535 services");
     return ANOMOD_EINVAL;
   }
-  *out = res;
+  *out = owned.release();
   return ANOMOD_OK;
 }
 

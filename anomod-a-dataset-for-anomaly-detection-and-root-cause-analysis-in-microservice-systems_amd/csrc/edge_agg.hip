@@ -890,9 +890,14 @@ __global__ __launch_bounds__(256) void exact_pick_kernel(const unsigned long lon
   const uint64_t b = lower((unsigned long long)(e + 1u) << 32);
   const uint64_t c = b - a;
   if (count) count[e] = c;
+  // the reference's int(c * q) with q = q_pct / 100 as a double (the same
+  // double as the literal 0.95, ...: IEEE division rounds correctly), the
+  // product truncated as Python's int() does (monitor_http_responses.py:
+  // 188-189; x[len // 2] at :186 is the same index for q = 50)
   for (uint32_t k = 0; k < nq; ++k)
     out[(uint64_t)e * nq + k] =
-        c ? (double)(uint32_t)sk[a + c * q_pct[k] / 100u] : (double)NAN;
+        c ? (double)(uint32_t)sk[a + (uint64_t)((double)c * ((double)q_pct[k] / 100.0))]
+          : (double)NAN;
 }
 
 using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,

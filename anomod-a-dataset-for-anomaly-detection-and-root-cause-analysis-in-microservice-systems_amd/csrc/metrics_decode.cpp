@@ -512,14 +512,21 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
     for (size_t k = 0; k < np; ++k)
       th.emplace_back([&, k] {
         quoted[k] = memchr(cut[k], '"', (size_t)(cut[k + 1] - cut[k])) != nullptr;
-        if (!quoted[k]) rc[k] = decode_long_rows(H, cut[k], cut[k + 1], part[k], 0);
+        try {  // an exception must not leave a worker thread (std::terminate)
+          if (!quoted[k]) rc[k] = decode_long_rows(H, cut[k], cut[k + 1], part[k], 0);
+        } catch (const std::bad_alloc&) {
+          rc[k] = ANOMOD_ENOMEM;
+        }
       });
     for (auto& x : th) x.join();
     bool any_quote = false;
     for (size_t k = 0; k < np; ++k) any_quote |= quoted[k] != 0;
     if (any_quote) return decode_long_rows(H, body, end, b, 0);
-    for (size_t k = 0; k < np; ++k)
+    for (size_t k = 0; k < np; ++k) {
+      if (rc[k] == ANOMOD_ENOMEM)
+        anomod::set_error(nullptr, "out of host memory decoding a metric CSV");
       if (rc[k] != ANOMOD_OK) return rc[k];  // (row numbers in the message are per piece)
+    }
     // the pieces' series into the builder (file order), their samples
     // referenced in place, not copied
     for (size_t k = 0; k < np; ++k) {

@@ -261,8 +261,9 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
                                     uint32_t n_services, anomod_edge_table* out);
 /* Exact per-edge order statistics (SURVEY.md §8a a11 cross-check mode): the
  * same per-span edges as the aggregation, one radix sort of (edge, latency)
- * keys, then per edge x[(c * q_pct[k]) // 100] of its sorted latencies (the
- * reference's sorted(x)[int(c*q)], monitor_http_responses.py:180-190).
+ * keys, then per edge x[int(c * q)] of its sorted latencies with q the double
+ * q_pct[k] / 100.0 and the product truncated — the reference's
+ * sorted(x)[int(n*q)] for any q_pct (monitor_http_responses.py:180-190).
  * out: [E][nq] doubles (NaN for an empty edge); count: [E] (may be NULL).
  * Needs a grouped set; q_pct[k] in [0, 99], nq <= 16.                       */
 int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,

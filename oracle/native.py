@@ -100,8 +100,9 @@ def span_edges(spans, S: int | None = None) -> np.ndarray:
 
 
 def exact_quantiles(spans, q_pct=(50, 99), S: int | None = None) -> np.ndarray:
-    """Per edge: sorted(latencies)[(c*q)//100] (monitor_http_responses.py:
-    180-190 nearest rank, floor index), NaN for an empty edge; [E, len(q)]."""
+    """Per edge: sorted(latencies)[int(c * (q / 100))] (monitor_http_responses.py:
+    180-190 nearest rank, the f64 product truncated as Python's int() does),
+    NaN for an empty edge; [E, len(q)]."""
     S = len(spans.services) if S is None else S
     E = (S + 2) * S
     e = span_edges(spans, S)
@@ -112,7 +113,8 @@ def exact_quantiles(spans, q_pct=(50, 99), S: int | None = None) -> np.ndarray:
     out = np.full((E, len(q_pct)), np.nan)
     for k, q in enumerate(q_pct):
         nz = cnt > 0
-        out[nz, k] = ds[start[nz] + cnt[nz] * q // 100]
+        rank = (cnt[nz].astype(np.float64) * (q / 100)).astype(np.int64)
+        out[nz, k] = ds[start[nz] + rank]
     return out
 
 

@@ -207,3 +207,21 @@ def test_exact_edge_quantiles_follow_reference_percentiles(golden):
         ref = case["latency_statistics"]  # written by the reference's generate_summary
         assert (q[1, 0], q[1, 1], q[1, 2]) == (ref["median"], ref["p95"], ref["p99"])
     assert checked >= 5
+
+
+def test_exact_rank_is_pythons_int_of_the_product():
+    """The exact-mode index is the reference's int(n * q) (Python f64
+    product, truncated; monitor_http_responses.py:188-189) for any q_pct, not
+    (n * q_pct) // 100 — they differ e.g. at n = 100, q = 0.57."""
+    import anomod
+    from oracle import native
+
+    sp = anomod.SpanSet(["a"], np.array([0, 100], np.uint64), np.ones(100, np.uint64),
+                        np.arange(1, 101, dtype=np.uint64), np.zeros(100, np.uint64),
+                        np.zeros(100, np.uint16), np.zeros(100, np.uint16),
+                        np.arange(100, dtype=np.uint32)[::-1].copy())
+    got = native.exact_quantiles(sp, tuple(range(100)), S=1)
+    row = 1 * 1 + 0  # ROOT -> a
+    for q in range(100):
+        assert got[row, q] == sorted(range(100))[int(100 * (q / 100))]
+    assert got[row, 57] == 56 and (100 * 57) // 100 == 57
