@@ -494,7 +494,13 @@ def load_trace_file(path, services: list[str] | None = None) -> SpanSet:
     """A trace file of the dataset -> SpanSet: Jaeger dumps ({"data": ...})
     and collector payloads ({"metadata": ..., "traces": ...}) go through the
     native decoder; anything else (raw GraphQL span lists) through the
-    Python decoders."""
+    Python decoders.  The set's unique_ids is checked exactly."""
+    spans = _load_trace_file(path, services)
+    spans.check_unique_ids()
+    return spans
+
+
+def _load_trace_file(path, services: list[str] | None = None) -> SpanSet:
     data = map_file(path)
     key = _first_key(data[:4096])
     if key == "data":

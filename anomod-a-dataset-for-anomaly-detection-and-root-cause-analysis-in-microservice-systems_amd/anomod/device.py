@@ -64,7 +64,8 @@ def synth_generate_host(spec: SynthSpec, n_traces: int, shard: int = 0) -> SpanS
     ptr = np.empty(n_traces + 1, np.uint64)
     L.check(lib.anomod_synth_generate_host(C.byref(cs), shard, n_traces,
                                            C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)))
-    return SpanSet(spec.services(), ptr, **arr)
+    # span ids are injective in the span index (csrc/synth.h synth_span_id)
+    return SpanSet(spec.services(), ptr, **arr, unique_ids=True)
 
 
 def _soa_out(arr: dict) -> L.SpanSoA:
@@ -96,6 +97,16 @@ class DeviceSpans:
         self.n_spans, self.n_traces = ns.value, nt.value
         self.grouped = bool(g.value)  # False: arrival order, traces known by trace_hash only
 
+    @property
+    def unique_ids(self) -> bool:
+        u = C.c_int()
+        L.check(L.lib().anomod_spans_unique_ids(self.handle, C.byref(u)))
+        return bool(u.value)
+
+    @unique_ids.setter
+    def unique_ids(self, v: bool):
+        L.check(L.lib().anomod_spans_set_unique_ids(self.handle, 1 if v else 0))
+
     def download(self) -> SpanSet:
         n = self.n_spans
         arr = dict(trace_hash=np.empty(n, np.uint64), span_id=np.empty(n, np.uint64),
@@ -105,7 +116,7 @@ class DeviceSpans:
         L.check(L.lib().anomod_spans_download(self.ctx.handle, self.handle,
                                               C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)),
                 self.ctx.handle)
-        return SpanSet(self.services, ptr, **arr)
+        return SpanSet(self.services, ptr, **arr, unique_ids=self.unique_ids)
 
     def free(self):
         if self.handle:
@@ -225,7 +236,9 @@ class Context:
         self._check(self._lib.anomod_spans_upload(self.handle, C.byref(soa), spans.n_spans,
                                                   L.ptr(spans.trace_ptr, C.c_uint64),
                                                   spans.n_traces, C.byref(h)))
-        return DeviceSpans(self, h, spans.services)
+        d = DeviceSpans(self, h, spans.services)
+        d.unique_ids = spans.unique_ids
+        return d
 
     def upload_ungrouped(self, spans: SpanSet) -> DeviceSpans:
         """Upload spans in arrival order: the trace of a span is its trace_hash
@@ -234,7 +247,9 @@ class Context:
         soa = spans.soa()
         self._check(self._lib.anomod_spans_upload_ungrouped(self.handle, C.byref(soa),
                                                             spans.n_spans, C.byref(h)))
-        return DeviceSpans(self, h, spans.services)
+        d = DeviceSpans(self, h, spans.services)
+        d.unique_ids = spans.unique_ids
+        return d
 
     def group(self, spans: DeviceSpans) -> DeviceSpans:
         """Group an ungrouped device span set by trace (segmented radix sort

@@ -179,15 +179,25 @@ def _series_service(key, services: list[str], memo: dict | None = None) -> int |
 
 def _latency_shift(cur: EdgeTable, base: EdgeTable, min_count: int = 10) -> np.ndarray:
     """Per service: largest log2 growth of an incoming edge's GPU p99 over
-    the same edge in a baseline run (edges with >= min_count spans)."""
-    S = cur.n_services
+    the same edge — matched by service NAMES (the two runs may have seen
+    different service sets: services_discovered lists only the services a
+    run's traces name, trace_collector.py:572) — in a baseline run (edges
+    with >= min_count spans on both sides)."""
+    S, Sb = cur.n_services, base.n_services
     out = np.zeros(S)
-    if base.services != cur.services:
-        return out
-    ok = ((cur.count >= min_count) & (base.count >= min_count) & np.isfinite(cur.p99_us)
-          & np.isfinite(base.p99_us) & (base.p99_us > 0))
+    pos = {s: i for i, s in enumerate(base.services)}
+    m = np.array([pos.get(s, -1) for s in cur.services] + [Sb, Sb + 1], np.int64)  # + ROOT, ORPHAN
+    p_cur = np.repeat(np.arange(S + 2), S)
+    c_cur = np.tile(np.arange(S), S + 2)
+    pb, cb = m[p_cur], m[c_cur]
+    have = (pb >= 0) & (cb >= 0)
+    rows = np.where(have, pb * Sb + np.where(cb >= 0, cb, 0), 0)
+    bc = np.where(have, base.count[rows], 0)
+    bp = np.where(have, base.p99_us[rows], np.nan)
+    ok = ((cur.count >= min_count) & (bc >= min_count) & np.isfinite(cur.p99_us)
+          & np.isfinite(bp) & (bp > 0))
     ratio = np.zeros(cur.count.shape[0])
-    ratio[ok] = np.maximum(0.0, np.log2(cur.p99_us[ok] / base.p99_us[ok]))
+    ratio[ok] = np.maximum(0.0, np.log2(cur.p99_us[ok] / bp[ok]))
     return ratio.reshape(S + 2, S).max(axis=0)
 
 

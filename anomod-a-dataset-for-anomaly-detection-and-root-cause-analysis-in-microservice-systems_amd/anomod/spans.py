@@ -26,6 +26,9 @@ class SpanSet:
     flags: np.ndarray          # u16 [n_spans]
     dur_us: np.ndarray         # u32 [n_spans]
     trace_ids: list[str] | None = None
+    # span ids unique within every trace (the producer's declaration, or
+    # check_unique_ids()): lets the GPU parent lookups scan from both ends
+    unique_ids: bool = False
     _keep: list = field(default_factory=list, repr=False, compare=False)
 
     def __post_init__(self):
@@ -62,6 +65,18 @@ class SpanSet:
             L.ptr(self.parent_span_id, C.c_uint64), L.ptr(self.svc, C.c_uint16),
             L.ptr(self.flags, C.c_uint16), L.ptr(self.dur_us, C.c_uint32))
 
+    def check_unique_ids(self) -> bool:
+        """Exact: no trace holds a span id twice (sets and returns
+        unique_ids)."""
+        if self.n_spans:
+            t = self.trace_of_span()
+            order = np.lexsort((self.span_id, t))
+            ts, ids = t[order], self.span_id[order]
+            self.unique_ids = not bool(np.any((ts[1:] == ts[:-1]) & (ids[1:] == ids[:-1])))
+        else:
+            self.unique_ids = True
+        return self.unique_ids
+
     def trace_of_span(self) -> np.ndarray:
         """Trace index of every span (host helper)."""
         lens = np.diff(self.trace_ptr).astype(np.int64)
@@ -79,7 +94,8 @@ class SpanSet:
             ids = [t for t, m in zip(self.trace_ids, mask) if m]
         return SpanSet(list(self.services), new_ptr, self.trace_hash[span_mask],
                        self.span_id[span_mask], self.parent_span_id[span_mask],
-                       self.svc[span_mask], self.flags[span_mask], self.dur_us[span_mask], ids)
+                       self.svc[span_mask], self.flags[span_mask], self.dur_us[span_mask], ids,
+                       self.unique_ids)
 
     def shard(self, nshards: int, rank: int) -> "SpanSet":
         """Traces whose trace_hash % nshards == rank."""
@@ -104,7 +120,7 @@ class SpanSet:
         remap[used] = np.arange(used.shape[0], dtype=np.uint16)
         return SpanSet([self.services[i] for i in used.tolist()], self.trace_ptr, self.trace_hash,
                        self.span_id, self.parent_span_id, remap[self.svc], self.flags,
-                       self.dur_us, self.trace_ids)
+                       self.dur_us, self.trace_ids, self.unique_ids)
 
     def take(self, order: np.ndarray, trace_ptr: np.ndarray) -> "SpanSet":
         """The spans in `order`, split into traces by `trace_ptr`."""
@@ -128,7 +144,8 @@ class SpanSet:
         if all(s.trace_ids is not None for s in sets):
             ids = [t for s in sets for t in s.trace_ids]
         return SpanSet(list(services), ptr, cat("trace_hash"), cat("span_id"),
-                       cat("parent_span_id"), cat("svc"), cat("flags"), cat("dur_us"), ids)
+                       cat("parent_span_id"), cat("svc"), cat("flags"), cat("dur_us"), ids,
+                       all(s.unique_ids for s in sets))
 
 
 def edge_rows(n_services: int) -> int:

@@ -67,6 +67,17 @@ struct anomod_spans {
   // UINT64_MAX = unknown.  Lets a call skip the long-trace pass when no
   // trace outgrows a wave chunk.
   uint64_t max_trace_len = ~0ull;
+  // The SN-width (E <= 512) edge kernel privatises its histogram in the pair
+  // form (8 Ki slots) — right for sets that touch a few thousand (edge, bin)
+  // keys per workgroup.  A set whose aggregation overflowed that table
+  // (spans counted in HBM after a full probe chain) takes the compact form
+  // (16 Ki packed slots) from then on; set by anomod_edge_aggregate_spans.
+  mutable bool hist_compact = false;
+  // Span ids are unique within every trace (declared by the producer: the
+  // synthetic generator by construction, anomod_spans_set_unique_ids for
+  // decoded / uploaded sets).  Lets the parent lookups scan from both ends
+  // (any match is the first match).  false = unknown: forward scan only.
+  bool unique_ids = false;
   bool grouped = true;       // false: spans in arrival order, trace_ptr = NULL
                              // (anomod_spans_upload_ungrouped; group first)
   uint64_t* trace_hash = nullptr;

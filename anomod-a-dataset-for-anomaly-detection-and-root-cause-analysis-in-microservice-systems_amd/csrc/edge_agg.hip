@@ -129,6 +129,7 @@ struct Table {
   unsigned long long* big;       // long traces: [0] listed, [1] ticket of edge_big_kernel
   unsigned long long* big_list;  // long traces: trace indices
   uint64_t t_base;           // trace index of this launch's first trace
+  unsigned long long* ovf;   // spans whose pair-form probe chain was full (counted in HBM)
 };
 
 struct Cols {
@@ -162,7 +163,8 @@ __device__ __forceinline__ uint32_t ht_hash(uint32_t key) { return key * 0x9E377
 
 __device__ __attribute__((noinline)) void ht_insert_pair(uint32_t* hk, uint32_t* hc, uint32_t key,
                                                          uint32_t s,
-                                                         unsigned long long* __restrict__ ghist) {
+                                                         unsigned long long* __restrict__ ghist,
+                                                         unsigned long long* __restrict__ ovf) {
   for (int probe = 0; probe < kPairMaxProbe; ++probe) {
     uint32_t cur = __hip_atomic_load(&hk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == 0u) {
@@ -176,6 +178,7 @@ __device__ __attribute__((noinline)) void ht_insert_pair(uint32_t* hk, uint32_t*
     s = (s + 1u) & (kPairSlots - 1u);
   }
   atomicAdd(&ghist[key - 1u], 1ull);
+  atomicAdd(ovf, 1ull);  // the host switches this span set to the compact form
 }
 
 __device__ __forceinline__ void ht_wrap(uint32_t old, uint32_t key, uint32_t kb,
@@ -331,7 +334,7 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
     const bool hit = (j < 3u) | (bk.w == key);
     atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
     stat_add<ST>(smem, edge, d, fl, tab, pk);
-    if (!hit) ht_insert_pair(hk, hc, key, s0, tab.hist);
+    if (!hit) ht_insert_pair(hk, hc, key, s0, tab.hist, tab.ovf);
   } else {  // kHtCompact
     auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
     const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
@@ -412,7 +415,7 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   return -1;
 }
 
-template <int HT, int ST>
+template <int HT, int ST, bool UNI>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
                                               const Chunk& c, const Regs& R, uint32_t S,
                                               const Table& tab) {
@@ -445,7 +448,8 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
         trace_bounds(Sm, r, lane, c.n, a, b);
-        const int q = find_parent(lsid, a, b, R.pid[r]);
+        const int q = UNI ? find_parent_bidir(lsid, a, b, i, R.pid[r])
+                          : find_parent(lsid, a, b, R.pid[r]);
         if (q >= 0) p = lsvc[q];
       } else {  // ablation: a parent-like edge without the lookup (keeps key diversity)
         p = ((R.sf[r] & 0xFFFFu) + 1u + (uint32_t)(R.pid[r] & 1u)) % S;
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
   tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
-template <int HT, int ST>
+template <int HT, int ST, bool UNI>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
@@ -775,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       if (cur.k == 0) {  // a trace longer than kStage: listed for edge_big_kernel
         if (lane == 0) tab.big_list[atomicAdd(&tab.big[0], 1ull)] = tab.t_base + t_cur;
       } else {
-        process_chunk<HT, ST>(smem, wsm, lane, cur, R, S, tab);
+        process_chunk<HT, ST, UNI>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
@@ -903,34 +907,54 @@ __global__ __launch_bounds__(256) void exact_pick_kernel(const unsigned long lon
 using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                           const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
 
-KernelFn pick_kernel(uint32_t E, const char** name) {
+// The histogram form an SN-width set asks for: its hint, or ANOMOD_HIST_FORM
+// = compact / pair (tests force either).
+bool want_compact(const anomod_spans* s) {
+  const char* f = getenv("ANOMOD_HIST_FORM");
+  if (f && !strcmp(f, "compact")) return true;
+  if (f && !strcmp(f, "pair")) return false;
+  return s->hist_compact;
+}
+
+// Whether the bidirectional parent scan may be used: the set's declared
+// id uniqueness (ANOMOD_UNIQUE_SCAN=0 forces the forward scan: tests, A/B).
+bool use_unique(const anomod_spans* s) {
+  const char* f = getenv("ANOMOD_UNIQUE_SCAN");
+  if (f && !strcmp(f, "0")) return false;
+  return s->unique_ids;
+}
+
+struct Pick {
+  KernelFn fn;
+  int ht, st;
+  const char* name;
+};
+
+Pick pick_kernel(uint32_t E, bool compact, bool uni) {
   const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
   const bool lds_hist = keys < (1ull << 31);  // >= 1 count bit above the key
-  if (lds_hist && E <= kLdsEdges) {
-    *name = "edge_agg_kernel<lds_hist,lds_stats>";
-    return edge_agg_kernel<kHtPair, kStDirect>;
-  }
-  if (lds_hist && E <= kWideEdges) {
-    *name = "edge_agg_kernel<lds_compact_hist,wide_stats>";
-    return edge_agg_kernel<kHtCompact, kStWide>;
-  }
-  if (lds_hist) {
-    *name = "edge_agg_kernel<lds_compact_hist,slot_stats>";
-    return edge_agg_kernel<kHtCompact, kStSlot>;
-  }
-  *name = "edge_agg_kernel<hbm_hist,hbm_stats>";
-  return edge_agg_kernel<kHtHbm, kStHbm>;
+#define ANOMOD_PICK(H, S_, NAME)                                                               \
+  return Pick{uni ? edge_agg_kernel<H, S_, true> : edge_agg_kernel<H, S_, false>, H, S_, NAME}
+  if (lds_hist && E <= kLdsEdges && compact)  // a set that overflowed the pair table
+    ANOMOD_PICK(kHtCompact, kStDirect, "edge_agg_kernel<lds_compact_hist,lds_stats>");
+  if (lds_hist && E <= kLdsEdges) ANOMOD_PICK(kHtPair, kStDirect, "edge_agg_kernel<lds_hist,lds_stats>");
+  if (lds_hist && E <= kWideEdges)
+    ANOMOD_PICK(kHtCompact, kStWide, "edge_agg_kernel<lds_compact_hist,wide_stats>");
+  if (lds_hist) ANOMOD_PICK(kHtCompact, kStSlot, "edge_agg_kernel<lds_compact_hist,slot_stats>");
+  ANOMOD_PICK(kHtHbm, kStHbm, "edge_agg_kernel<hbm_hist,hbm_stats>");
+#undef ANOMOD_PICK
 }
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
 // all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
-// ctr (u64) | big counters (u64 x 2; both zeroed with them) | count | p50 |
+// ctr (u64) | big counters (u64 x 2) | pair-table overflows (u64; all
+// zeroed with them) | count | p50 |
 // p99 | mn | long-trace list.  [off_err, end_small) is copied to the host in
 // one D2H.
 struct Layout {
   uint64_t E;
-  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_count, off_p50, off_p99,
-      off_mn, end_small, bytes;
+  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_ovf, off_count, off_p50,
+      off_p99, off_mn, end_small, bytes;
   Layout(uint64_t e, uint64_t big_cap) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
@@ -938,7 +962,8 @@ struct Layout {
     off_mx = off_sum + E * 8;
     off_ctr = (off_mx + E * 4 + 7) & ~size_t(7);
     off_big = off_ctr + 8;
-    off_count = off_big + 16;
+    off_ovf = off_big + 16;
+    off_count = off_ovf + 8;
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
@@ -972,13 +997,14 @@ hipError_t launch_big_for(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S
   // the LDS tables' u32 counters hold < 2^32 records per workgroup: a set
   // whose listed traces could exceed a launch's bound records to HBM
   if (spans->n_spans >= max_launch_spans()) return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
-  const char* name = nullptr;
-  const KernelFn fn = pick_kernel(E, &name);
-  if (fn == edge_agg_kernel<kHtPair, kStDirect>)
+  const Pick pk = pick_kernel(E, want_compact(spans), false);
+  if (pk.ht == kHtPair && pk.st == kStDirect)
     return launch_big<kHtPair, kStDirect>(ctx, spans, S, E, tab);
-  if (fn == edge_agg_kernel<kHtCompact, kStWide>)
+  if (pk.ht == kHtCompact && pk.st == kStDirect)
+    return launch_big<kHtCompact, kStDirect>(ctx, spans, S, E, tab);
+  if (pk.ht == kHtCompact && pk.st == kStWide)
     return launch_big<kHtCompact, kStWide>(ctx, spans, S, E, tab);
-  if (fn == edge_agg_kernel<kHtCompact, kStSlot>)
+  if (pk.ht == kHtCompact && pk.st == kStSlot)
     return launch_big<kHtCompact, kStSlot>(ctx, spans, S, E, tab);
   return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
 }
@@ -1025,6 +1051,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
   tab.big = reinterpret_cast<unsigned long long*>(base + L.off_big);
   tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
+  tab.ovf = reinterpret_cast<unsigned long long*>(base + L.off_ovf);
   tab.kb = 1;
   while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
   auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
@@ -1041,8 +1068,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
 
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
-    const char* kname = nullptr;
-    KernelFn fn = pick_kernel(E, &kname);
+    const KernelFn fn = pick_kernel(E, want_compact(spans), use_unique(spans)).fn;
     // As many workgroups as are resident at once (LDS / registers decide).
     int per_cu = 0;
     ANOMOD_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1107,6 +1133,13 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   fan(out->max_us, L.off_mx, E * 4ull);
   fan(out->p50_us, L.off_p50, E * 8ull);
   fan(out->p99_us, L.off_p99, E * 8ull);
+  // More than 1/64 of the spans counted in HBM past a full pair table: the
+  // set touches more (edge, bin) keys than 8 Ki slots hold (e.g. random call
+  // trees over every service pair); its next aggregations use the compact
+  // form (same results, exact either way).
+  unsigned long long ovf = 0;
+  memcpy(&ovf, hs + (L.off_ovf - L.off_err), 8);
+  if (ovf * 64ull > spans->n_spans) spans->hist_compact = true;
   return ANOMOD_OK;
 }
 
@@ -1158,7 +1191,8 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
     tab.ctr = d_ctr;
     tab.big = d_ctr + 1;
     tab.big_list = d_ctr + 32;
-    KernelFn fn = edge_agg_kernel<kHtKeys, kStHbm>;
+    KernelFn fn = use_unique(spans) ? edge_agg_kernel<kHtKeys, kStHbm, true>
+                                    : edge_agg_kernel<kHtKeys, kStHbm, false>;
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn),
                                                      kThreads, 0);

@@ -848,6 +848,7 @@ anomod_spans view_of(const anomod_spans* in, const GroupResult& g) {
   v.n_traces = g.n_traces;
   v.max_svc = in->max_svc;
   v.grouped = true;
+  v.unique_ids = in->unique_ids;  // grouping permutes spans, ids stay per trace
   v.trace_hash = g.cols.h;
   v.span_id = g.cols.sid;
   v.parent_span_id = g.cols.pid;
@@ -911,6 +912,7 @@ int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* in, anomod_spans** o
   anomod_spans* s = nullptr;
   if (int rc = alloc_spans(ctx, in->n_spans, g.n_traces, true, &s)) return rc;
   s->max_svc = in->max_svc;
+  s->unique_ids = in->unique_ids;
   const uint64_t n = in->n_spans;
   hipError_t e = hipSuccess;
   auto cp = [&](void* d, const void* src, size_t bytes) {
@@ -951,8 +953,11 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   if (rc == ANOMOD_OK) rc = group_run(ctx, spans, &g);
   if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
   if (rc != ANOMOD_OK) return comm_agree(ctx, rc);  // peers learn of it before their reduce
-  const anomod_spans view = view_of(spans, g);
-  return anomod_edge_aggregate_spans(ctx, &view, n_services, out);
+  anomod_spans view = view_of(spans, g);
+  view.hist_compact = spans->hist_compact;
+  const int rc2 = anomod_edge_aggregate_spans(ctx, &view, n_services, out);
+  spans->hist_compact = view.hist_compact;  // the set's histogram-form hint
+  return rc2;
 }
 
 int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* in, uint64_t seed,
@@ -971,6 +976,7 @@ int anomod_spans_shuffle(anomod_ctx* ctx, const anomod_spans* in, uint64_t seed,
     return rc;
   s->max_svc = in->max_svc;
   s->max_trace_len = in->max_trace_len;  // traces keep their spans either way
+  s->unique_ids = in->unique_ids;
   s->grouped = keep;
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
   const SoaOut sout{s->trace_hash, s->span_id, s->parent_span_id, s->svc_flags, s->dur_us};

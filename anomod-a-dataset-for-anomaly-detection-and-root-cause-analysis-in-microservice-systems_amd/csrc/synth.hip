@@ -606,10 +606,23 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
     return rc;
   }
   s->max_svc = (uint32_t)h->services.size() - 1u;
+  s->unique_ids = true;  // synth_span_id is injective in the span index
   s->max_trace_len = 0;
   for (size_t k = 0; k + 1 < h->tmpl_off.size(); ++k)
     s->max_trace_len = std::max<uint64_t>(s->max_trace_len, h->tmpl_off[k + 1] - h->tmpl_off[k]);
   *out = s;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_set_unique_ids(anomod_spans* spans, int unique) {
+  ANOMOD_REQUIRE(nullptr, spans, "anomod_spans_set_unique_ids: NULL span set");
+  spans->unique_ids = unique != 0;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_unique_ids(const anomod_spans* spans, int* unique) {
+  ANOMOD_REQUIRE(nullptr, spans && unique, "anomod_spans_unique_ids: NULL argument");
+  *unique = spans->unique_ids ? 1 : 0;
   return ANOMOD_OK;
 }
 

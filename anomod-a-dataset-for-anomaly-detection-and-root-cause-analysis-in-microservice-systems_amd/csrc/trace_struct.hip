@@ -35,6 +35,9 @@
 // outgrowing L); per-trace counters in LDS.  A trace longer than 256 spans is
 // resolved by the whole wave against HBM (O(L^2 / 64) compares plus
 // relaxation rounds over a scratch edge list; rare).
+#include <cstdlib>
+#include <cstring>
+
 #include "chunk.h"
 #include "common.h"
 
@@ -130,6 +133,7 @@ __device__ __forceinline__ int first_of(const uint64_t* lsid, uint32_t a, uint32
   return -1;
 }
 
+template <bool UNI>
 __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t t0,
                          const uint64_t (&sid)[kPer], const uint64_t (&pid)[kPer],
                          const uint32_t (&svc)[kPer], const TsOut& o) {
@@ -176,10 +180,19 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
       uint32_t b;
       trace_bounds(Sm, r, lane, c.n, a[r], b);
       int l, pf;  // pf: own parent (child lists)
-      scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
-      np[r] = (l == (int)i) ? pf : first_of(lsid, a[r], b, lpid[l]);  // node parent
+      if constexpr (UNI) {
+        // ids unique in the trace: the span is its node's only span (f = l =
+        // i), and the parent reference has at most one match, found from
+        // either end (chunk.h find_parent_bidir); no own-id scan
+        f[r] = l = (int)i;
+        pf = pid[r] != 0ull ? find_parent_bidir(lsid, a[r], b, i, pid[r]) : -1;
+        np[r] = pf;
+      } else {
+        scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
+        np[r] = (l == (int)i) ? pf : first_of(lsid, a[r], b, lpid[l]);  // node parent
+      }
       if (pf >= 0) atomicAdd(&lcnt[pf], 1u);
-      dup |= f[r] != (int)i;
+      if constexpr (!UNI) dup |= f[r] != (int)i;
       pfl = (uint32_t)(pf + 1) | (b - a[r]) << 16;
     }
     lpfl[i] = pfl;
@@ -539,6 +552,7 @@ __global__ __launch_bounds__(kBigThreads) void ts_big_kernel(
   }
 }
 
+template <bool UNI>
 __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4))) void trace_struct_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint64_t* __restrict__ trace_ptr, uint64_t n_traces,
@@ -594,7 +608,7 @@ __global__ __launch_bounds__(kTsThreads) __attribute__((amdgpu_waves_per_eu(4)))
         o.big_list[2 * j + 1] = atomicAdd(&o.big[1], (unsigned long long)cur.n);
       }
     } else {
-      ts_chunk(wsm, lane, cur, t_cur, sid, pid, svc, o);
+      ts_chunk<UNI>(wsm, lane, cur, t_cur, sid, pid, svc, o);
     }
     if (!has_next) break;
     cur = nxt;
@@ -699,12 +713,17 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
     return rc;
   }
   if (nt > 0) {
+    // ids unique within every trace (the set's declaration; ANOMOD_UNIQUE_SCAN=0
+    // forces the general scan): no own-id scans, no duplicate path
+    const char* us = getenv("ANOMOD_UNIQUE_SCAN");
+    const bool uni = spans->unique_ids && !(us && !strcmp(us, "0"));
+    auto kfn = uni ? trace_struct_kernel<true> : trace_struct_kernel<false>;
     int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(trace_struct_kernel), kTsThreads, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn),
+                                                     kTsThreads, 0);
     if (e != hipSuccess) return fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
-    hipLaunchKernelGGL(trace_struct_kernel, dim3((unsigned)grid), dim3(kTsThreads), 0, ctx->stream,
+    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kTsThreads), 0, ctx->stream,
                        spans->span_id, spans->parent_span_id, spans->svc_flags, spans->trace_ptr,
                        nt, o);
     e = hipGetLastError();

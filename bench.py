@@ -33,8 +33,8 @@ import numpy as np  # noqa: E402
 import anomod  # noqa: E402
 from anomod import _lib as L  # noqa: E402
 
-LEGS = ("trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped", "tt_width",
-        "long_traces", "pagerank", "ewma", "tt_config2", "tt_config2_files")
+LEGS = ("general_scan", "trace_structure", "exact_quantiles", "in_trace_shuffled", "ungrouped",
+        "tt_width", "long_traces", "pagerank", "ewma", "tt_config2", "tt_config2_files")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 METRIC = "spans/sec aggregated (node) + % HBM peak; RCA PageRank iters/sec at 1/2/4/8 GPUs"
 
@@ -392,6 +392,16 @@ def main() -> int:
             "bytes_per_launch": bytes_launch,
         },
     }
+    if "general_scan" in legs:
+        # --- the same spans without the generator's unique-id declaration
+        # (ANOMOD_UNIQUE_SCAN=0): the first-match forward parent scan every
+        # set takes when nothing is known about duplicated ids
+        os.environ["ANOMOD_UNIQUE_SCAN"] = "0"
+        try:
+            result["sn_general_scan"] = edge_leg(ctx, spans, 3, "edge kernel, first-match forward "
+                                                 "scan (ids not declared unique)")
+        finally:
+            del os.environ["ANOMOD_UNIQUE_SCAN"]
     if "trace_structure" in legs:
         # --- trace structure on the same resident spans:
         # reads 20 B/span + 8 B/trace, writes 13 B/span + 12 B/trace
@@ -421,7 +431,7 @@ def main() -> int:
             r = np.abs(h - x) / np.maximum(x, 1.0)
             rel[name] = {"max_rel_err": float(r.max()), "mean_rel_err": float(r.mean())}
         result["exact_quantiles"] = {
-            "what": "exact x[(c*q)//100] per edge vs the 896-bin histogram midpoints",
+            "what": "exact x[int(c*q)] per edge vs the 896-bin histogram midpoints",
             "edges": int(ok.sum()), "seconds": q_s, **rel}
     if "in_trace_shuffled" in legs:
         # --- the same spans with every trace's spans in a random order (the

@@ -127,6 +127,15 @@ uint32_t anomod_hist_bin(uint32_t v);
 int anomod_hist_bin_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi);
 
 /* ---- span sets -----------------------------------------------------------*/
+/* Span ids unique within every trace: the producer's declaration (the
+ * synthetic generator sets it by construction; the native decoders report it
+ * per decoded document, anomod_decoded_unique_ids).  With it, parent
+ * lookups may stop at the nearest match from either end of the trace (any
+ * match is the first match).  Declaring it for a set that holds a duplicated
+ * id inside a trace gives unspecified parents for those spans.  Default 0
+ * (unknown: the first-match scan).  Grouping and shuffling keep it.         */
+int anomod_spans_set_unique_ids(anomod_spans* spans, int unique);
+int anomod_spans_unique_ids(const anomod_spans* spans, int* unique);
 /* Copy a host span set to HBM.  Replaces the in-memory hand-off between
  * json.load and the per-span loop of jaeger_to_csv.py:12-32 /
  * trace_collector.py:519-531.                                              */

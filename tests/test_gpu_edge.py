@@ -261,3 +261,67 @@ def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
         ex = got[ok, k].astype(np.uint32)
         b = [spec.hist_bounds(spec.hist_bin(int(v))) for v in ex]
         np.testing.assert_array_equal(tab[qq][ok], [0.5 * (lo + hi) for lo, hi in b])
+
+
+@pytest.mark.parametrize("form", ["pair", "compact"])
+def test_sn_width_histogram_forms(ctx, monkeypatch, form):
+    """Both LDS histogram forms of the SN-width kernel (E <= 512) give the
+    oracle's table bit for bit (ANOMOD_HIST_FORM forces one)."""
+    monkeypatch.setenv("ANOMOD_HIST_FORM", form)
+    rng = np.random.default_rng(61)
+    sp = _random_spanset(rng, 14, 30000, 40, dup=0.01)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+    dev = ctx.generate(anomod.SynthSpec("LONG", seed=8, p_orphan_ppm=500), 2000)
+    ref = native.edge_aggregate(dev.download())
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    dev.free()
+
+
+def test_pair_table_overflow_switches_form(ctx):
+    """A device set touching far more (edge, bin) keys per workgroup than the
+    pair table's 8 Ki slots (random call trees over 20 services, latencies
+    over the whole u32 range) overflows it on the first aggregation; later
+    aggregations of the same set take the compact form.  Every result equals
+    the oracle's."""
+    rng = np.random.default_rng(62)
+    sp = _random_spanset(rng, 20, 700_000, 40)
+    ref = native.edge_aggregate(sp)
+    dev = ctx.upload(sp)
+    for _ in range(3):
+        assert_table_equal(ctx.edge_aggregate(dev), ref)
+    dev.free()
+
+
+@pytest.mark.parametrize("S,max_len", [(12, 24), (46, 80), (5, 256)])
+def test_unique_id_bidirectional_scan(ctx, monkeypatch, S, max_len):
+    """Sets whose span ids are unique within every trace (checked exactly on
+    the host) take the bidirectional parent scan; the table equals the
+    oracle's and the forward-scan build's (ANOMOD_UNIQUE_SCAN=0), parents
+    before and after their children (in-trace shuffle), orphans included."""
+    rng = np.random.default_rng(S * 7 + max_len)
+    sp = _random_spanset(rng, S, 20000, max_len, orphan=0.03)
+    assert sp.check_unique_ids()
+    ref = native.edge_aggregate(sp)
+    dev = ctx.upload(sp)
+    assert dev.unique_ids
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    shuf = ctx.shuffle(dev, seed=5, window_traces=0)  # parents anywhere in the trace
+    assert shuf.unique_ids
+    host = shuf.download()
+    ref2 = native.edge_aggregate(host)
+    assert_table_equal(ctx.edge_aggregate(shuf), ref2)
+    monkeypatch.setenv("ANOMOD_UNIQUE_SCAN", "0")
+    assert_table_equal(ctx.edge_aggregate(shuf), ref2)
+    shuf.free()
+    dev.free()
+
+
+def test_duplicate_ids_are_not_declared_unique(ctx):
+    rng = np.random.default_rng(70)
+    sp = _random_spanset(rng, 12, 5000, 30, dup=0.05)
+    assert not sp.check_unique_ids()
+    dev = ctx.upload(sp)
+    assert not dev.unique_ids
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(sp))
+    gen = ctx.generate(anomod.SynthSpec("SN", seed=3), 1000)
+    assert gen.unique_ids and gen.download().check_unique_ids()
