@@ -103,6 +103,14 @@ class DeviceSpans:
         L.check(L.lib().anomod_spans_unique_ids(self.handle, C.byref(u)))
         return bool(u.value)
 
+    @property
+    def hist_compact(self) -> bool:
+        """True once an aggregation overflowed the pair-form LDS histogram
+        (later ones use the compact form)."""
+        c = C.c_int()
+        L.check(L.lib().anomod_spans_hist_compact(self.handle, C.byref(c)))
+        return bool(c.value)
+
     @unique_ids.setter
     def unique_ids(self, v: bool):
         L.check(L.lib().anomod_spans_set_unique_ids(self.handle, 1 if v else 0))

@@ -603,15 +603,203 @@ __device__ __forceinline__ uint32_t big_slot(uint64_t id) {
   return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> (64 - 12)) & (kBigSlots - 1u);
 }
 
+// One trace longer than kBigWin spans: blocks of kBigThreads * kBigPer
+// spans, each looked up against the trace's id windows in order (the first
+// window holding a parent reference gives its first match).
+template <int HT, int ST>
+__device__ void big_one(unsigned char* smem, const uint64_t* __restrict__ span_id,
+                        const uint64_t* __restrict__ parent, const uint32_t* __restrict__ svcfl,
+                        const uint32_t* __restrict__ dur, uint64_t lo, uint64_t L, uint32_t S,
+                        const Table& tab) {
+  auto* bkey = reinterpret_cast<unsigned long long*>(smem + kOffBigKey);
+  auto* bval = reinterpret_cast<uint32_t*>(smem + kOffBigPos);
+  const int tid = threadIdx.x;
+  for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kBigThreads * kBigPer) {
+    uint64_t pid[kBigPer];
+    uint32_t sf[kBigPer], dr[kBigPer], psv[kBigPer];  // psv: parent's service (~0: none yet)
+    bool need = false;
+#pragma unroll
+    for (int r = 0; r < kBigPer; ++r) {
+      const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
+      pid[r] = i < L ? parent[lo + i] : 0ull;
+      sf[r] = i < L ? svcfl[lo + i] : 0u;
+      dr[r] = i < L ? dur[lo + i] : 0u;
+      psv[r] = 0xFFFFFFFFu;
+      need |= pid[r] != 0ull;
+    }
+    for (uint64_t w0 = 0; w0 < L; w0 += kBigWin) {
+      if (!__syncthreads_or(need)) break;  // also orders the previous clear
+      constexpr int kIns = kBigWin / kBigThreads;
+      uint64_t id[kIns];
+      uint32_t sv[kIns];
+#pragma unroll
+      for (int u = 0; u < kIns; ++u) {
+        const uint32_t k = (uint32_t)(u * kBigThreads + tid);
+        id[u] = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
+        sv[u] = w0 + k < L ? svcfl[lo + w0 + k] & 0xFFFFu : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kIns; ++u) {
+        if (id[u] == 0ull) continue;
+        const uint32_t k = (uint32_t)(u * kBigThreads + tid);
+        for (uint32_t sl = big_slot(id[u]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+          const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id[u]);
+          if (prev == 0ull || prev == id[u]) {
+            atomicMin(&bval[sl], (k << 16) | sv[u]);  // the first position wins, with its service
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      need = false;
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
+        for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
+          const unsigned long long key = bkey[sl];
+          if (key == pid[r]) {
+            psv[r] = bval[sl] & 0xFFFFu;
+            break;
+          }
+          if (key == 0ull) break;
+        }
+        need |= psv[r] == 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
+        bkey[k] = 0ull;
+        bval[k] = 0xFFFFFFFFu;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kBigPer; ++r) {
+      const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
+      if (i >= L) continue;
+      const uint32_t p = pid[r] == 0ull ? S : psv[r] == 0xFFFFFFFFu ? S + 1u : psv[r];
+      const uint32_t edge = p * S + (sf[r] & 0xFFFFu);
+      if constexpr (HT == kHtKeys) {
+        tab.keys[lo + i] = ((unsigned long long)edge << 32) | dr[r];
+      } else {
+        record<HT, ST>(smem, edge, dr[r], sf[r] >> 16, tab);
+      }
+    }
+  }
+  __syncthreads();  // the last window's clear before the next user of the table
+}
+
+// Up to kGroup listed traces of <= kBigWin spans packed into ONE table window
+// (r03): trace i owns table slots [2 off_i, 2 off_i + 2 L_i) (load 1/2;
+// range reduction by multiply-shift, linear probing inside the region), so
+// ids of different traces never meet, and a workgroup pays the
+// load / insert / lookup round trips once per batch instead of once per
+// trace.  <= 2 spans per thread (sum L_i <= kBigWin = 2 x kBigThreads).
+constexpr int kGroup = 4;  // traces per ticket (one atomic, their entries and bounds loaded together)
+static_assert(kBigWin == 2 * kBigThreads, "a packed batch is two spans per thread");
+
+__device__ __forceinline__ uint32_t big_region_slot(uint64_t id, uint32_t size) {
+  return __umulhi((uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 32), size);
+}
+
+// bm: the group entries (bits) packed into this window, consecutive
+template <int HT, int ST>
+__device__ void big_batch(unsigned char* smem, const uint64_t* __restrict__ span_id,
+                          const uint64_t* __restrict__ parent, const uint32_t* __restrict__ svcfl,
+                          const uint32_t* __restrict__ dur, const uint64_t (&lo)[kGroup],
+                          const uint64_t (&L)[kGroup], uint32_t bm, uint32_t S, const Table& tab) {
+  auto* bkey = reinterpret_cast<unsigned long long*>(smem + kOffBigKey);
+  auto* bval = reinterpret_cast<uint32_t*>(smem + kOffBigPos);
+  const int tid = threadIdx.x;
+  uint32_t off[kGroup + 1];  // non-members have length 0
+  off[0] = 0;
+#pragma unroll
+  for (int i = 0; i < kGroup; ++i) off[i + 1] = off[i] + (((bm >> i) & 1u) ? (uint32_t)L[i] : 0u);
+  const uint32_t tot = off[kGroup];
+  uint64_t id[2], pid[2], g[2];
+  uint32_t sf[2], dr[2], rb[2], rs[2], pos[2], psv[2];
+  bool v[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t q = (uint32_t)(u * kBigThreads + tid);
+    v[u] = q < tot;
+    // the member holding batch position q: the last entry whose start <= q
+    // (entries before the batch start at 0 with length 0, entries after it
+    // at tot)
+    uint32_t a0 = 0, a1 = off[1];
+    uint64_t tl = lo[0];
+#pragma unroll
+    for (int i = 1; i < kGroup; ++i)
+      if (q >= off[i] && ((bm >> i) & 1u)) {
+        a0 = off[i];
+        a1 = off[i + 1];
+        tl = lo[i];
+      }
+    pos[u] = q - a0;
+    rb[u] = 2u * a0;  // the trace's table region
+    rs[u] = 2u * (a1 - a0);
+    g[u] = tl + pos[u];
+    id[u] = v[u] ? span_id[g[u]] : 0ull;
+    pid[u] = v[u] ? parent[g[u]] : 0ull;
+    sf[u] = v[u] ? svcfl[g[u]] : 0u;
+    dr[u] = v[u] ? dur[g[u]] : 0u;
+    psv[u] = 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!v[u] || id[u] == 0ull) continue;
+    uint32_t r = big_region_slot(id[u], rs[u]);
+    while (true) {
+      const uint32_t sl = rb[u] + r;
+      const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id[u]);
+      if (prev == 0ull || prev == id[u]) {
+        atomicMin(&bval[sl], (pos[u] << 16) | (sf[u] & 0xFFFFu));  // the first position wins
+        break;
+      }
+      r = r + 1u == rs[u] ? 0u : r + 1u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!v[u] || pid[u] == 0ull) continue;
+    uint32_t r = big_region_slot(pid[u], rs[u]);
+    for (uint32_t probe = 0; probe < rs[u]; ++probe) {
+      const unsigned long long key = bkey[rb[u] + r];
+      if (key == pid[u]) {
+        psv[u] = bval[rb[u] + r] & 0xFFFFu;
+        break;
+      }
+      if (key == 0ull) break;
+      r = r + 1u == rs[u] ? 0u : r + 1u;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!v[u]) continue;
+    const uint32_t p = pid[u] == 0ull ? S : psv[u] == 0xFFFFFFFFu ? S + 1u : psv[u];
+    const uint32_t edge = p * S + (sf[u] & 0xFFFFu);
+    if constexpr (HT == kHtKeys) {
+      tab.keys[g[u]] = ((unsigned long long)edge << 32) | dr[u];
+    } else {
+      record<HT, ST>(smem, edge, dr[u], sf[u] >> 16, tab);
+    }
+  }
+  __syncthreads();  // every lookup done before the clear
+  for (uint32_t k = tid; k < 2u * tot; k += kBigThreads) {
+    bkey[k] = 0ull;
+    bval[k] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+}
+
 template <int HT, int ST>
 __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
     const uint64_t* __restrict__ trace_ptr, uint32_t S, uint32_t E, Table tab) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[kBigLdsBytes];
-  __shared__ unsigned long long s_tr[3];  // ticket, first span, length of this iteration's trace
+  __shared__ unsigned long long s_g[kGroup][2];  // the current group: first span, length (0: none)
   auto* bkey = reinterpret_cast<unsigned long long*>(smem + kOffBigKey);  // 0 = empty (id 0 is never a parent ref)
-  auto* bval = reinterpret_cast<uint32_t*>(smem + kOffBigPos);  // (first position in window) << 16 | svc
+  auto* bval = reinterpret_cast<uint32_t*>(smem + kOffBigPos);  // (first position) << 16 | svc
   const int tid = threadIdx.x;
   const uint64_t nbig = tab.big[0];
   if (nbig == 0) return;
@@ -620,102 +808,71 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
     bkey[k] = 0ull;
     bval[k] = 0xFFFFFFFFu;
   }
-  // Thread 0 keeps the NEXT trace in flight (ticket, list entry, bounds),
-  // each load issued a phase after the one it depends on, so a trace's
-  // dependent latency overlaps the previous trace's work.
-  unsigned long long nj = 0, nt = 0, nlo = 0, nhi = 0;
-  if (tid == 0) {
-    nj = atomicAdd(&tab.big[1], 1ull);
-    nt = nj < nbig ? tab.big_list[nj] : 0ull;
-    nlo = nj < nbig ? trace_ptr[nt] : 0ull;
-    nhi = nj < nbig ? trace_ptr[nt + 1] : 0ull;
-  }
+  // Wave 0 keeps the NEXT group of kGroup traces in flight (one ticket, the
+  // list entries and bounds loaded by lanes 0..kGroup-1 together) while the
+  // workgroup works on the current one.
+  unsigned long long nlo = 0, nL = 0;
+  auto fetch = [&]() {
+    unsigned long long j = 0;
+    if (tid == 0) j = atomicAdd(&tab.big[1], (unsigned long long)kGroup);
+    j = __shfl(j, 0);
+    nlo = nL = 0;
+    if (tid < kGroup && j + tid < nbig) {
+      const uint64_t t = tab.big_list[j + tid];
+      nlo = trace_ptr[t];
+      nL = trace_ptr[t + 1] - nlo;
+    }
+  };
+  if (tid < kWave) fetch();
   while (true) {
-    __syncthreads();  // table clear / s_tr reuse
-    if (tid == 0) {
-      s_tr[0] = nj;
-      s_tr[1] = nlo;
-      s_tr[2] = nhi - nlo;
-      nj = atomicAdd(&tab.big[1], 1ull);
+    __syncthreads();  // the previous group is done with s_g
+    if (tid < kGroup) {
+      s_g[tid][0] = nlo;
+      s_g[tid][1] = nL;
     }
     __syncthreads();
-    const uint64_t j = s_tr[0];
-    if (j >= nbig) break;
-    const uint64_t lo = s_tr[1], L = s_tr[2];
-    for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kBigThreads * kBigPer) {
-      uint64_t pid[kBigPer];
-      uint32_t sf[kBigPer], dr[kBigPer], psv[kBigPer];  // psv: parent's service (~0: none yet)
-      bool need = false;
+    uint64_t glo[kGroup], gL[kGroup];
+    bool any = false;
 #pragma unroll
-      for (int r = 0; r < kBigPer; ++r) {
-        const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
-        pid[r] = i < L ? parent[lo + i] : 0ull;
-        sf[r] = i < L ? svcfl[lo + i] : 0u;
-        dr[r] = i < L ? dur[lo + i] : 0u;
-        psv[r] = 0xFFFFFFFFu;
-        need |= pid[r] != 0ull;
+    for (int k = 0; k < kGroup; ++k) {
+      glo[k] = s_g[k][0];
+      gL[k] = s_g[k][1];
+      any |= gL[k] != 0;
+    }
+    if (!any) break;  // tickets exhausted (listed traces are never empty)
+    if (tid < kWave) fetch();  // next group, overlapping this one's work
+    // greedy in order: a trace longer than a window alone, else as many
+    // consecutive ones as one window holds (group entries addressed by
+    // compile-time indices only: the arrays stay in registers)
+    uint32_t left = 0;
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) left |= (gL[q] != 0 ? 1u : 0u) << q;
+    while (left) {
+      const int k = __ffs(left) - 1;
+      uint64_t lk = 0, Lk = 0;
+#pragma unroll
+      for (int q = 0; q < kGroup; ++q)
+        if (q == k) {
+          lk = glo[q];
+          Lk = gL[q];
+        }
+      if (Lk > kBigWin) {
+        big_one<HT, ST>(smem, span_id, parent, svcfl, dur, lk, Lk, S, tab);
+        left &= ~(1u << k);
+        continue;
       }
-      if (tid == 0 && b0 == 0 && nj < nbig) nt = tab.big_list[nj];  // next trace, phase 2
-      for (uint64_t w0 = 0; w0 < L; w0 += kBigWin) {
-        if (!__syncthreads_or(need)) break;  // also orders the previous clear
-        constexpr int kIns = kBigWin / kBigThreads;
-        uint64_t id[kIns];
-        uint32_t sv[kIns];
+      uint32_t bm = 0;
+      uint64_t tot = 0;
 #pragma unroll
-        for (int u = 0; u < kIns; ++u) {
-          const uint32_t k = (uint32_t)(u * kBigThreads + tid);
-          id[u] = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
-          sv[u] = w0 + k < L ? svcfl[lo + w0 + k] & 0xFFFFu : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kIns; ++u) {
-          if (id[u] == 0ull) continue;
-          const uint32_t k = (uint32_t)(u * kBigThreads + tid);
-          for (uint32_t sl = big_slot(id[u]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
-            const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id[u]);
-            if (prev == 0ull || prev == id[u]) {
-              atomicMin(&bval[sl], (k << 16) | sv[u]);  // the first position wins, with its service
-              break;
-            }
-          }
-        }
-        __syncthreads();
-        need = false;
-#pragma unroll
-        for (int r = 0; r < kBigPer; ++r) {
-          if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
-          for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kBigSlots - 1u)) {
-            const unsigned long long key = bkey[sl];
-            if (key == pid[r]) {
-              psv[r] = bval[sl] & 0xFFFFu;
-              break;
-            }
-            if (key == 0ull) break;
-          }
-          need |= psv[r] == 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        for (uint32_t k = tid; k < kBigSlots; k += kBigThreads) {
-          bkey[k] = 0ull;
-          bval[k] = 0xFFFFFFFFu;
+      for (int q = 0; q < kGroup; ++q) {
+        const bool chain = q == k || (q > 0 && ((bm >> (q - 1)) & 1u));
+        if (q >= k && chain && ((left >> q) & 1u) && gL[q] <= kBigWin && tot + gL[q] <= kBigWin) {
+          bm |= 1u << q;
+          tot += gL[q];
         }
       }
-      if (tid == 0 && b0 == 0 && nj < nbig) {  // next trace, phase 3
-        nlo = trace_ptr[nt];
-        nhi = trace_ptr[nt + 1];
-      }
-#pragma unroll
-      for (int r = 0; r < kBigPer; ++r) {
-        const uint64_t i = b0 + (uint64_t)r * kBigThreads + tid;
-        if (i >= L) continue;
-        const uint32_t p = pid[r] == 0ull ? S : psv[r] == 0xFFFFFFFFu ? S + 1u : psv[r];
-        const uint32_t edge = p * S + (sf[r] & 0xFFFFu);
-        if constexpr (HT == kHtKeys) {
-          tab.keys[lo + i] = ((unsigned long long)edge << 32) | dr[r];
-        } else {
-          record<HT, ST>(smem, edge, dr[r], sf[r] >> 16, tab);
-        }
-      }
+      big_batch<HT, ST>(smem, span_id, parent, svcfl, dur, glo, gL, bm, S, tab);
+      left &= ~bm;
     }
   }
   __syncthreads();
@@ -938,6 +1095,11 @@ Pick pick_kernel(uint32_t E, bool compact, bool uni) {
   if (lds_hist && E <= kLdsEdges && compact)  // a set that overflowed the pair table
     ANOMOD_PICK(kHtCompact, kStDirect, "edge_agg_kernel<lds_compact_hist,lds_stats>");
   if (lds_hist && E <= kLdsEdges) ANOMOD_PICK(kHtPair, kStDirect, "edge_agg_kernel<lds_hist,lds_stats>");
+  // TrainTicket width: the pair form while the set's keys fit it (whole-ms
+  // SkyWalking latencies give a few thousand (edge, bin) keys per
+  // workgroup), the compact form once it overflowed
+  if (lds_hist && E <= kWideEdges && !compact)
+    ANOMOD_PICK(kHtPair, kStWide, "edge_agg_kernel<lds_hist,wide_stats>");
   if (lds_hist && E <= kWideEdges)
     ANOMOD_PICK(kHtCompact, kStWide, "edge_agg_kernel<lds_compact_hist,wide_stats>");
   if (lds_hist) ANOMOD_PICK(kHtCompact, kStSlot, "edge_agg_kernel<lds_compact_hist,slot_stats>");
@@ -1002,6 +1164,8 @@ hipError_t launch_big_for(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S
     return launch_big<kHtPair, kStDirect>(ctx, spans, S, E, tab);
   if (pk.ht == kHtCompact && pk.st == kStDirect)
     return launch_big<kHtCompact, kStDirect>(ctx, spans, S, E, tab);
+  if (pk.ht == kHtPair && pk.st == kStWide)
+    return launch_big<kHtPair, kStWide>(ctx, spans, S, E, tab);
   if (pk.ht == kHtCompact && pk.st == kStWide)
     return launch_big<kHtCompact, kStWide>(ctx, spans, S, E, tab);
   if (pk.ht == kHtCompact && pk.st == kStSlot)

@@ -620,6 +620,12 @@ int anomod_spans_set_unique_ids(anomod_spans* spans, int unique) {
   return ANOMOD_OK;
 }
 
+int anomod_spans_hist_compact(const anomod_spans* spans, int* compact) {
+  ANOMOD_REQUIRE(nullptr, spans && compact, "anomod_spans_hist_compact: NULL argument");
+  *compact = spans->hist_compact ? 1 : 0;
+  return ANOMOD_OK;
+}
+
 int anomod_spans_unique_ids(const anomod_spans* spans, int* unique) {
   ANOMOD_REQUIRE(nullptr, spans && unique, "anomod_spans_unique_ids: NULL argument");
   *unique = spans->unique_ids ? 1 : 0;

@@ -136,6 +136,10 @@ int anomod_hist_bin_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi);
  * (unknown: the first-match scan).  Grouping and shuffling keep it.         */
 int anomod_spans_set_unique_ids(anomod_spans* spans, int unique);
 int anomod_spans_unique_ids(const anomod_spans* spans, int* unique);
+/* 1 once an aggregation of this set overflowed the workgroups' 8 Ki-slot
+ * (pair-form) LDS histogram: its later aggregations use the 16 Ki packed-slot
+ * (compact) form (same results; a performance hint the library keeps).     */
+int anomod_spans_hist_compact(const anomod_spans* spans, int* compact);
 /* Copy a host span set to HBM.  Replaces the in-memory hand-off between
  * json.load and the per-span loop of jaeger_to_csv.py:12-32 /
  * trace_collector.py:519-531.                                              */

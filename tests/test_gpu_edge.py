@@ -264,12 +264,14 @@ def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
 
 
 @pytest.mark.parametrize("form", ["pair", "compact"])
-def test_sn_width_histogram_forms(ctx, monkeypatch, form):
-    """Both LDS histogram forms of the SN-width kernel (E <= 512) give the
-    oracle's table bit for bit (ANOMOD_HIST_FORM forces one)."""
+@pytest.mark.parametrize("S", [14, 46])
+def test_histogram_forms(ctx, monkeypatch, form, S):
+    """Both LDS histogram forms of the SN-width (E <= 512, direct stats) and
+    TrainTicket-width (E <= 2304, wide stats) kernels give the oracle's table
+    bit for bit (ANOMOD_HIST_FORM forces one)."""
     monkeypatch.setenv("ANOMOD_HIST_FORM", form)
-    rng = np.random.default_rng(61)
-    sp = _random_spanset(rng, 14, 30000, 40, dup=0.01)
+    rng = np.random.default_rng(61 + S)
+    sp = _random_spanset(rng, S, 30000, 40, dup=0.01)
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
     dev = ctx.generate(anomod.SynthSpec("LONG", seed=8, p_orphan_ppm=500), 2000)
     ref = native.edge_aggregate(dev.download())
@@ -287,8 +289,10 @@ def test_pair_table_overflow_switches_form(ctx):
     sp = _random_spanset(rng, 20, 700_000, 40)
     ref = native.edge_aggregate(sp)
     dev = ctx.upload(sp)
+    assert not dev.hist_compact
     for _ in range(3):
         assert_table_equal(ctx.edge_aggregate(dev), ref)
+        assert dev.hist_compact
     dev.free()
 
 
