@@ -177,6 +177,14 @@ class Context:
         self._check(self._lib.anomod_ctx_stage_ms(self.handle, stage, C.byref(v)))
         return v.value
 
+    def group_info(self) -> dict:
+        """How the last grouping ran: path ("bucket" / "lsd"), scatter levels
+        or radix passes, and the key bits they sorted on."""
+        p, lv, b = C.c_int(), C.c_int(), C.c_int()
+        self._check(self._lib.anomod_ctx_group_info(self.handle, C.byref(p), C.byref(lv),
+                                                    C.byref(b)))
+        return {"path": "bucket" if p.value == 1 else "lsd", "levels": lv.value, "bits": b.value}
+
     # -- multi-GPU
     @staticmethod
     def unique_id() -> bytes:

@@ -1,0 +1,837 @@
+// Trace grouping, bucket path: two stable MSD scatter levels over the top T
+// bits of k = mix64(trace_hash), then one workgroup per bucket of ~512 spans
+// that puts the bucket in (k, arrival) order inside LDS and writes the grouped
+// SoA columns and its trace starts.  Same output as the LSD path of group.hip
+// (traces by k ascending, spans of a trace in arrival order — the order the
+// reference's first-match parent rule sees, trace_collector.py:424-443), with
+// fewer bytes moved: 2 record scatters + 1 coalesced record pass instead of
+// ceil(log2(n)/8) scatters + bucket fix-up + trace_ptr scan.
+//
+// Per span (n = 1.15e9: T = 20, DA = DB = 10):
+//   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 2 (next digit out)
+//   level B: 2 (count: digits) + 32 + 32
+//   buckets: 32 (records in) + 32 (SoA columns out) + 8/trace (trace_ptr, two moves)
+// = 172 B/span + tile counts (~2 B/span) against 286 B/span for the LSD path.
+//
+// A bucket larger than the small kernel's 2048 spans (a long trace, or the
+// tail of the size distribution) goes to a list that a 1024-thread kernel of
+// 8192-span capacity works through; a bucket beyond that (a single trace of
+// thousands of spans near others) makes the caller regroup with the LSD path.
+#include <algorithm>
+#include <cstdlib>
+
+#include "chunk.h"
+#include "group.h"
+
+namespace anomod {
+namespace {
+
+using chunk::wave_sync;
+// Experiment-only builds (never set in the shipped library):
+//  1 = level B counts its digits from the level-A records (no 2-B digit array);
+//  2 = level A stores nothing, then the LSD path groups (timing of level A's
+//      loads and ranking only);
+//  4 = scatter levels stage whole 32-B records (one stage / write phase; digit
+//      levels of at most 9 bits, else the LSD path groups).
+#ifndef ANOMOD_BK_ABL
+#define ANOMOD_BK_ABL 0
+#endif
+constexpr int kWv = 64;
+constexpr int kBThreads = 1024;                // scatter workgroup
+constexpr int kBWaves = kBThreads / kWv;       // 16
+constexpr int kBPer = 4;                       // records per thread
+constexpr int kBTile = kBThreads * kBPer;      // 4096 records per tile
+#if ANOMOD_BK_ABL & 4
+constexpr int kDMax = 9;                       // digit bits per scatter level
+#else
+constexpr int kDMax = 11;                      // digit bits per scatter level
+#endif
+constexpr int kNDMax = 1 << kDMax;
+constexpr int kScanRows = 256;                 // tiles per block of the tile scan
+constexpr int kSubBits = 8;                    // per-bucket split before the key compare
+constexpr int kSub = 1 << kSubBits;
+constexpr int kSmallW = 512, kSmallPer = 4;    // per-bucket kernel: 2048 spans
+constexpr int kBigW = 1024, kBigPer = 8;       // oversized buckets: 8192 spans
+constexpr int kDChunk = 4096;                  // entries per partial sum of the trace-count scan
+
+// Exclusive scan of one value per thread across a workgroup of NW waves;
+// *tot = the sum.  Every thread must call it (two barriers).
+template <int NW>
+__device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t* tot) {
+  const int lane = threadIdx.x & (kWv - 1), w = threadIdx.x / kWv;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < kWv; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWv - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+#pragma unroll
+  for (int ww = 0; ww < NW; ++ww) {
+    const uint32_t s = wsum[ww];
+    pre += ww < w ? s : 0u;
+    all += s;
+  }
+  __syncthreads();
+  *tot = all;
+  return pre + inc - x;
+}
+
+// ---- level A: per-tile digit counts of the top DA bits -----------------------
+__global__ __launch_bounds__(256) void bk_count_a_kernel(const uint64_t* __restrict__ h, uint64_t n,
+                                                         int da, uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t lh[kNDMax];
+  const int nd = 1 << da, tid = threadIdx.x, sh = 64 - da;
+  for (int i = tid; i < nd; i += 256) lh[i] = 0u;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kBTile;
+#pragma unroll 4
+  for (int j = 0; j < kBTile / 256; ++j) {
+    const uint64_t p = t0 + (uint64_t)(j * 256 + tid);
+    if (p < n) atomicAdd(&lh[(uint32_t)(mix64(h[p]) >> sh)], 1u);
+  }
+  __syncthreads();
+  for (int i = tid; i < nd; i += 256) tcnt[(uint64_t)blockIdx.x * nd + i] = lh[i];
+}
+
+// ---- level A: exclusive scan of the tile counts over tiles, per digit -------
+// column sums of kScanRows tiles; grid (blocks, ceil(nd / 256))
+__global__ __launch_bounds__(256) void bk_scan_up_kernel(const uint32_t* __restrict__ tcnt,
+                                                         uint64_t tiles, int nd,
+                                                         uint32_t* __restrict__ bsum) {
+  const int d = blockIdx.y * 256 + threadIdx.x;
+  if (d >= nd) return;
+  const uint64_t a = (uint64_t)blockIdx.x * kScanRows;
+  const uint64_t b = a + kScanRows < tiles ? a + kScanRows : tiles;
+  uint32_t s = 0;
+#pragma unroll 8
+  for (uint64_t t = a; t < b; ++t) s += tcnt[t * nd + d];
+  bsum[(uint64_t)blockIdx.x * nd + d] = s;
+}
+
+// One block: the block sums scanned down every digit, the digit starts (=
+// level-A bucket starts, bsA[nd] = n) added in, and the level-B tile starts of
+// every level-A bucket (btile[nd] = level-B tiles in all).
+__global__ __launch_bounds__(1024) void bk_scan_top_kernel(uint32_t* __restrict__ bsum,
+                                                           uint64_t nbk, int nd, uint64_t n,
+                                                           uint32_t* __restrict__ bsA,
+                                                           uint32_t* __restrict__ btile) {
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x;
+  const int dpt = nd > 1024 ? nd / 1024 : 1;  // consecutive digits per thread (nd <= 2048)
+  uint32_t tot[2] = {0u, 0u}, til[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int d = tid * dpt + i;
+    if (d >= nd) continue;
+    uint32_t run = 0;
+    for (uint64_t b = 0; b < nbk; ++b) {
+      const uint32_t x = bsum[b * nd + d];
+      bsum[b * nd + d] = run;
+      run += x;
+    }
+    tot[i] = run;
+    til[i] = (run + kBTile - 1) / kBTile;
+  }
+  uint32_t all, allt;
+  const uint32_t pre = block_excl_scan<16>(tot[0] + tot[1], wsum, &all);
+  const uint32_t pret = block_excl_scan<16>(til[0] + til[1], wsum, &allt);
+  for (int i = 0; i < dpt; ++i) {
+    const int d = tid * dpt + i;
+    if (d >= nd) continue;
+    const uint32_t start = pre + (i ? tot[0] : 0u);
+    bsA[d] = start;
+    btile[d] = pret + (i ? til[0] : 0u);
+    for (uint64_t b = 0; b < nbk; ++b) bsum[b * nd + d] += start;
+  }
+  if (tid == 0) {
+    bsA[nd] = (uint32_t)n;
+    btile[nd] = allt;
+  }
+}
+
+__global__ __launch_bounds__(256) void bk_scan_down_kernel(uint32_t* __restrict__ tcnt,
+                                                           uint64_t tiles, int nd,
+                                                           const uint32_t* __restrict__ bsum) {
+  const int d = blockIdx.y * 256 + threadIdx.x;
+  if (d >= nd) return;
+  const uint64_t a = (uint64_t)blockIdx.x * kScanRows;
+  const uint64_t b = a + kScanRows < tiles ? a + kScanRows : tiles;
+  uint32_t run = bsum[(uint64_t)blockIdx.x * nd + d];
+#pragma unroll 8
+  for (uint64_t t = a; t < b; ++t) {
+    const uint32_t x = tcnt[t * nd + d];
+    tcnt[t * nd + d] = run;
+    run += x;
+  }
+}
+
+// ---- level B: tiles inside level-A buckets -----------------------------------
+__global__ __launch_bounds__(256) void bk_tilemap_kernel(const uint32_t* __restrict__ btile,
+                                                         uint32_t* __restrict__ tmap) {
+  const uint32_t b = blockIdx.x;
+  for (uint32_t t = btile[b] + threadIdx.x; t < btile[b + 1]; t += 256) tmap[t] = b;
+}
+
+__device__ inline bool seg_tile(uint64_t t, const uint32_t* __restrict__ bsA,
+                                const uint32_t* __restrict__ btile,
+                                const uint32_t* __restrict__ tmap, int na, uint64_t* base,
+                                uint64_t* nvalid) {
+  if (t >= btile[na]) return false;
+  const uint32_t b = tmap[t];
+  const uint64_t a = (uint64_t)bsA[b] + (t - btile[b]) * (uint64_t)kBTile;
+  const uint64_t e = a + kBTile < (uint64_t)bsA[b + 1] ? a + kBTile : (uint64_t)bsA[b + 1];
+  *base = a;
+  *nvalid = e - a;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bk_count_b_kernel(const uint16_t* __restrict__ dn,
+                                                         const uint32_t* __restrict__ bsA,
+                                                         const uint32_t* __restrict__ btile,
+                                                         const uint32_t* __restrict__ tmap,
+                                                         int na, int db,
+                                                         uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t lh[kNDMax];
+  uint64_t base, nvalid;
+  if (!seg_tile(blockIdx.x, bsA, btile, tmap, na, &base, &nvalid)) return;
+  const int nd = 1 << db, tid = threadIdx.x;
+  for (int i = tid; i < nd; i += 256) lh[i] = 0u;
+  __syncthreads();
+#if ANOMOD_BK_ABL & 1
+  const GRec* rec = reinterpret_cast<const GRec*>(dn);
+  const int sh = 64 - db - (int)__builtin_ctz((unsigned)na);
+  for (uint64_t p = tid; p < nvalid; p += 256)
+    atomicAdd(&lh[(uint32_t)(mix64(rec[base + p].h) >> sh) & (uint32_t)(nd - 1)], 1u);
+#else
+  for (uint64_t p = tid; p < nvalid; p += 256) atomicAdd(&lh[dn[base + p]], 1u);
+#endif
+  __syncthreads();
+  for (int i = tid; i < nd; i += 256) tcnt[(uint64_t)blockIdx.x * nd + i] = lh[i];
+}
+
+// One block per level-A bucket: its tiles' counts scanned per digit, the
+// digit starts inside the bucket added in (= the final bucket starts).
+__global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict__ tcnt,
+                                                           const uint32_t* __restrict__ bsA,
+                                                           const uint32_t* __restrict__ btile,
+                                                           int na, int db,
+                                                           uint32_t* __restrict__ bstart) {
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x, nd = 1 << db;
+  const int dpt = nd > 1024 ? nd / 1024 : 1;
+  const uint32_t b = blockIdx.x, t0 = btile[b], t1 = btile[b + 1], base = bsA[b];
+  uint32_t tot[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int d = tid * dpt + i;
+    if (d >= nd) continue;
+    uint32_t s = 0;
+    for (uint32_t t = t0; t < t1; ++t) s += tcnt[(uint64_t)t * nd + d];
+    tot[i] = s;
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<16>(tot[0] + tot[1], wsum, &all);
+  for (int i = 0; i < dpt; ++i) {
+    const int d = tid * dpt + i;
+    if (d >= nd) continue;
+    const uint32_t start = base + pre + (i ? tot[0] : 0u);
+    bstart[(uint64_t)b * nd + d] = start;
+    uint32_t run = start;
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t x = tcnt[(uint64_t)t * nd + d];
+      tcnt[(uint64_t)t * nd + d] = run;
+      run += x;
+    }
+  }
+  if (b == (uint32_t)na - 1 && tid == 0) bstart[(uint64_t)na * nd] = bsA[na];
+}
+
+// ---- one stable scatter level ------------------------------------------------
+// Tile = 4096 records (1024 threads x 4; wave w owns positions [256w, 256w +
+// 256)), ranked with wave ballots (dbits ballots give each lane its
+// same-digit peers; a per-wave LDS counter per digit carries the count down
+// the wave's rows), staged in LDS in digit order one 16-B half at a time and
+// written as digit runs from the tile's global run starts.  Level A reads the
+// SoA columns and writes every record's level-B digit beside it.
+template <bool SOA_IN, bool SEG, bool DNEXT>
+__global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
+    SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
+    int dbits, const uint32_t* __restrict__ toff, uint16_t* __restrict__ dnext, int nshift,
+    uint32_t nmask, const uint32_t* __restrict__ bsA, const uint32_t* __restrict__ btile,
+    const uint32_t* __restrict__ tmap, int na) {
+  constexpr bool kFull = (ANOMOD_BK_ABL & 4) != 0;
+  constexpr bool kNoStore = (ANOMOD_BK_ABL & 2) != 0 && SOA_IN;
+  __shared__ uint4 stage[kBTile * (kFull ? 2 : 1)];  // 64 KiB: one half of every record
+  __shared__ uint16_t wcnt[kBWaves][kNDMax];   // per-wave digit counts, then wave offsets
+  __shared__ uint16_t sdig[kBTile];
+  __shared__ uint32_t tstart[kNDMax];          // tile-local start of each digit
+  __shared__ uint32_t gbase[kNDMax];           // global start of each digit's run
+  __shared__ uint32_t wsum[kBWaves];
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const int nd = 1 << dbits;
+  const uint64_t tile = blockIdx.x;
+  uint64_t base, nvalid;
+  if constexpr (SEG) {
+    if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
+  } else {
+    base = tile * kBTile;
+    nvalid = n - base < (uint64_t)kBTile ? n - base : (uint64_t)kBTile;
+  }
+  uint4 ra[kBPer], rb[kBPer];
+  uint32_t d[kBPer];
+  bool v[kBPer];
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kBPer * kWv) + k * kWv + lane);
+    const uint64_t i = base + loc;
+    v[k] = loc < nvalid;
+    ra[k] = make_uint4(0, 0, 0, 0);
+    rb[k] = make_uint4(0, 0, 0, 0);
+    if (v[k]) {
+      if constexpr (SOA_IN) {
+        const uint64_t h = sin.h[i], sid = sin.sid[i], pid = sin.pid[i];
+        ra[k] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)sid, (uint32_t)(sid >> 32));
+        rb[k] = make_uint4((uint32_t)pid, (uint32_t)(pid >> 32), sin.sf[i], sin.dur[i]);
+      } else {
+        const uint4* q = reinterpret_cast<const uint4*>(ain + i);
+        ra[k] = q[0];
+        rb[k] = q[1];
+      }
+    }
+    d[k] = (uint32_t)(mix64(((uint64_t)ra[k].y << 32) | ra[k].x) >> shift) & (uint32_t)(nd - 1);
+  }
+  for (int ww = 0; ww < kBWaves; ++ww)
+    for (int dd = tid; dd < nd; dd += kBThreads) wcnt[ww][dd] = 0;
+  for (int dd = tid; dd < nd; dd += kBThreads) gbase[dd] = toff[tile * nd + dd];
+  __syncthreads();
+
+  // wave multisplit, rows in order
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t off[kBPer];
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k) {
+    uint64_t peers = __ballot(v[k]);
+    for (int b = 0; b < dbits; ++b) {
+      const bool bit = (d[k] >> b) & 1u;
+      const uint64_t bb = __ballot(v[k] && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    off[k] = 0;
+    if (v[k]) {
+      const uint64_t lower = peers & lt_mask;
+      const uint32_t b0 = wcnt[w][d[k]];
+      off[k] = b0 + (uint32_t)__popcll(lower);
+      if (lower == 0ull) wcnt[w][d[k]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
+    }
+    wave_sync();
+  }
+  __syncthreads();
+
+  // per digit: wave offsets and the tile total, then the tile's digit starts
+  const int dpt = nd > kBThreads ? nd / kBThreads : 1;
+  uint32_t tot[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd >= nd) continue;
+    uint32_t run = 0;
+    for (int ww = 0; ww < kBWaves; ++ww) {
+      const uint32_t c = wcnt[ww][dd];
+      wcnt[ww][dd] = (uint16_t)run;
+      run += c;
+    }
+    tot[i] = run;
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kBWaves>(tot[0] + tot[1], wsum, &all);
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd < nd) tstart[dd] = pre + (i ? tot[0] : 0u);
+  }
+  __syncthreads();
+
+  uint32_t lp[kBPer];
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k) {
+    lp[k] = 0;
+    if (v[k]) {
+      lp[k] = tstart[d[k]] + wcnt[w][d[k]] + off[k];
+      if constexpr (kFull) {
+        stage[2 * lp[k]] = ra[k];
+        stage[2 * lp[k] + 1] = rb[k];
+      } else {
+        stage[lp[k]] = ra[k];
+      }
+      sdig[lp[k]] = (uint16_t)d[k];
+    }
+  }
+  __syncthreads();
+  if constexpr (kNoStore) return;
+  uint64_t g[kBPer];
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k) {
+    const uint32_t p = (uint32_t)(tid + k * kBThreads);
+    g[k] = 0;
+    if (p < nvalid) {
+      const uint32_t dd = sdig[p];
+      g[k] = (uint64_t)gbase[dd] + (p - tstart[dd]);
+      const uint4 x = stage[kFull ? 2 * p : p];
+      reinterpret_cast<uint4*>(aout + g[k])[0] = x;
+      if constexpr (kFull) reinterpret_cast<uint4*>(aout + g[k])[1] = stage[2 * p + 1];
+      if constexpr (DNEXT)
+        dnext[g[k]] = (uint16_t)((mix64(((uint64_t)x.y << 32) | x.x) >> nshift) & nmask);
+    }
+  }
+  if constexpr (kFull) return;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k)
+    if (v[k]) stage[lp[k]] = rb[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kBPer; ++k) {
+    const uint32_t p = (uint32_t)(tid + k * kBThreads);
+    if (p < nvalid) reinterpret_cast<uint4*>(aout + g[k])[1] = stage[p];
+  }
+}
+
+// ---- one bucket in (k, arrival) order ---------------------------------------
+template <int W, int PER>
+struct BucketLds {
+  static constexpr int kCap = W * PER, kNW = W / kWv;
+  struct Pre {
+    uint64_t skey[kCap];          // keys in sub-digit order
+    uint64_t kmin[kSub], kmax[kSub];
+    uint32_t tstart[kSub + 1];
+    uint16_t sorig[kCap];         // arrival position of every staged key
+    uint16_t wcnt[kNW][kSub];
+    uint8_t sflag[kCap];          // trace start at final position f
+  };
+  union {
+    uint4 stage[kCap];            // one 16-B half of every record, final order
+    Pre pre;
+  } u;
+  uint16_t sfinal[kCap];          // final position of every arrival position
+  uint32_t wsum[kNW];
+};
+
+// Bucket c = [bstart[c], bstart[c + 1]) of `in` (records in arrival order
+// inside the bucket; every k shares its top T bits).  Split once more by the
+// next 8 bits of k (stable); a sub-bucket holding one key is already in
+// arrival order, a mixed one ranks each key by compares:
+// rank = #{smaller k} + #{equal k earlier}.  Writes the grouped columns of the
+// bucket, its trace starts at tsp[4 * bstart[c] + ordinal] (the bucket's own
+// record region, read before) and the trace count dcnt[c].
+template <int W, int PER>
+__device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __restrict__ in,
+                                SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
+                                uint32_t* __restrict__ dcnt, bool small,
+                                uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
+                                uint32_t over_cap, unsigned long long* __restrict__ too_big) {
+  constexpr int kCap = W * PER, kNW = W / kWv;
+  static_assert(W >= kSub, "one thread per sub-digit");
+  auto& P = L.u.pre;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
+  if (m > (uint32_t)kCap) {
+    if (tid == 0) {
+      if (small) {
+        const unsigned long long i = atomicAdd(over_n, 1ull);
+        if (i < over_cap) over[i] = c;
+        else atomicAdd(too_big, 1ull);
+      } else {
+        atomicAdd(too_big, 1ull);
+      }
+    }
+    return;
+  }
+  if (m == 0) {
+    if (tid == 0) dcnt[c] = 0;
+    return;
+  }
+  // keys only; the records are read again (from L2) when staged in final order
+  uint64_t k[PER];
+  uint32_t e[PER], off[PER];
+  bool v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    v[j] = p < m;
+    k[j] = v[j] ? mix64(in[a0 + p].h) : 0ull;
+    e[j] = (uint32_t)(k[j] >> kshift) & (kSub - 1);
+  }
+  for (int i = tid; i < kNW * kSub; i += W) (&P.wcnt[0][0])[i] = 0;
+  for (int i = tid; i < kSub; i += W) {
+    P.kmin[i] = ~0ull;
+    P.kmax[i] = 0ull;
+  }
+  __syncthreads();
+
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    uint64_t peers = __ballot(v[j]);
+#pragma unroll
+    for (int b = 0; b < kSubBits; ++b) {
+      const bool bit = (e[j] >> b) & 1u;
+      const uint64_t bb = __ballot(v[j] && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    off[j] = 0;
+    if (v[j]) {
+      const uint64_t lower = peers & lt_mask;
+      const uint32_t b0 = P.wcnt[w][e[j]];
+      off[j] = b0 + (uint32_t)__popcll(lower);
+      if (lower == 0ull) P.wcnt[w][e[j]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
+      atomicMin(reinterpret_cast<unsigned long long*>(&P.kmin[e[j]]), (unsigned long long)k[j]);
+      atomicMax(reinterpret_cast<unsigned long long*>(&P.kmax[e[j]]), (unsigned long long)k[j]);
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  uint32_t tot = 0;
+  if (tid < kSub) {
+    uint32_t run = 0;
+    for (int ww = 0; ww < kNW; ++ww) {
+      const uint32_t cc = P.wcnt[ww][tid];
+      P.wcnt[ww][tid] = (uint16_t)run;
+      run += cc;
+    }
+    tot = run;
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kNW>(tot, L.wsum, &all);
+  if (tid < kSub) P.tstart[tid] = pre;
+  if (tid == 0) P.tstart[kSub] = m;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (v[j]) {
+      const uint32_t sp = P.tstart[e[j]] + P.wcnt[w][e[j]] + off[j];
+      P.skey[sp] = k[j];
+      P.sorig[sp] = (uint16_t)(w * (PER * kWv) + j * kWv + lane);
+    }
+  }
+  __syncthreads();
+
+  // final position inside the bucket
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t sp = (uint32_t)(tid + j * W);
+    if (sp < m) {
+      const uint64_t kp = P.skey[sp];
+      const uint32_t ee = (uint32_t)(kp >> kshift) & (kSub - 1);
+      const uint32_t a = P.tstart[ee], b = P.tstart[ee + 1];
+      uint32_t rank, first;
+      if (P.kmin[ee] == P.kmax[ee]) {
+        rank = sp - a;
+        first = sp == a;
+      } else {
+        rank = 0;
+        first = 1;
+        for (uint32_t q = a; q < b; ++q) {
+          const uint64_t kq = P.skey[q];
+          const bool eq_before = kq == kp && q < sp;
+          rank += (kq < kp || eq_before) ? 1u : 0u;
+          first &= eq_before ? 0u : 1u;
+        }
+      }
+      const uint32_t f = a + rank;
+      P.sflag[f] = (uint8_t)first;
+      L.sfinal[P.sorig[sp]] = (uint16_t)f;
+    }
+  }
+  __syncthreads();
+
+  // trace starts: ordinals in final order (written last: tsp is this bucket's
+  // own record region, read until then)
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t f = (uint32_t)(tid * PER + j);
+    cnt += f < m ? P.sflag[f] : 0u;
+  }
+  uint32_t nt;
+  const uint32_t ord0 = block_excl_scan<kNW>(cnt, L.wsum, &nt);
+  uint32_t fl = 0;  // bit j: tid * PER + j is a trace start
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t f = (uint32_t)(tid * PER + j);
+    fl |= (f < m && P.sflag[f]) ? (1u << j) : 0u;
+  }
+  __syncthreads();
+
+  // the records in final order, one half at a time, written coalesced
+  const uint4* src = reinterpret_cast<const uint4*>(in + a0);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if (v[j]) L.u.stage[L.sfinal[p]] = src[2 * p];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t i = (uint32_t)(tid + j * W);
+    if (i < m) {
+      const uint4 x = L.u.stage[i];
+      out.h[a0 + i] = ((uint64_t)x.y << 32) | x.x;
+      out.sid[a0 + i] = ((uint64_t)x.w << 32) | x.z;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if (v[j]) L.u.stage[L.sfinal[p]] = src[2 * p + 1];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t i = (uint32_t)(tid + j * W);
+    if (i < m) {
+      const uint4 x = L.u.stage[i];
+      out.pid[a0 + i] = ((uint64_t)x.y << 32) | x.x;
+      out.sf[a0 + i] = x.z;
+      out.dur[a0 + i] = x.w;
+    }
+  }
+  uint64_t* tsp = reinterpret_cast<uint64_t*>(const_cast<GRec*>(in)) + 4ull * a0;
+  uint32_t ord = ord0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if ((fl >> j) & 1u) tsp[ord++] = (uint64_t)a0 + (uint32_t)(tid * PER + j);
+  if (tid == 0) dcnt[c] = nt;
+}
+
+__global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
+    const GRec* __restrict__ in, SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
+    uint32_t* __restrict__ dcnt, uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
+    uint32_t over_cap, unsigned long long* __restrict__ too_big) {
+  __shared__ BucketLds<kSmallW, kSmallPer> L;
+  bucket_sort_one<kSmallW, kSmallPer>(L, blockIdx.x, in, out, bstart, kshift, dcnt, true, over,
+                                      over_n, over_cap, too_big);
+}
+
+__global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
+    const GRec* __restrict__ in, SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
+    uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ over,
+    const unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ BucketLds<kBigW, kBigPer> L;
+  const uint64_t cnt = *over_n < over_cap ? *over_n : over_cap;
+  for (uint64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    bucket_sort_one<kBigW, kBigPer>(L, over[i], in, out, bstart, kshift, dcnt, false, nullptr,
+                                    nullptr, 0, too_big);
+    __syncthreads();
+  }
+}
+
+// ---- trace_ptr from the buckets' trace starts --------------------------------
+__global__ __launch_bounds__(256) void bk_dsum_kernel(const uint32_t* __restrict__ dcnt, uint64_t nb,
+                                                      uint32_t* __restrict__ part) {
+  __shared__ uint32_t wsum[4];
+  const uint64_t a = (uint64_t)blockIdx.x * kDChunk;
+  uint32_t s = 0;
+  for (int j = 0; j < kDChunk / 256; ++j) {
+    const uint64_t p = a + (uint64_t)(j * 256 + threadIdx.x);
+    s += p < nb ? dcnt[p] : 0u;
+  }
+  uint32_t all;
+  (void)block_excl_scan<4>(s, wsum, &all);
+  if (threadIdx.x == 0) part[blockIdx.x] = all;
+}
+
+// one block: exclusive scan of the partial sums (<= 1024 of them), the trace
+// count to *total, trace_ptr closed
+__global__ __launch_bounds__(1024) void bk_dscan_top_kernel(uint32_t* __restrict__ part, uint64_t np,
+                                                            unsigned long long* __restrict__ total,
+                                                            uint64_t* __restrict__ tptr, uint64_t n) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t x = threadIdx.x < np ? part[threadIdx.x] : 0u;
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<16>(x, wsum, &all);
+  if (threadIdx.x < np) part[threadIdx.x] = pre;
+  if (threadIdx.x == 0) {
+    *total = all;
+    tptr[all] = n;
+  }
+}
+
+// dcnt -> its exclusive scan in place, dcnt[nb] = the total
+__global__ __launch_bounds__(256) void bk_ddown_kernel(uint32_t* __restrict__ dcnt, uint64_t nb,
+                                                       const uint32_t* __restrict__ part) {
+  __shared__ uint32_t wsum[4];
+  constexpr int kPerT = kDChunk / 256;
+  const uint64_t a = (uint64_t)blockIdx.x * kDChunk + (uint64_t)threadIdx.x * kPerT;
+  uint32_t x[kPerT], s = 0;
+#pragma unroll
+  for (int j = 0; j < kPerT; ++j) {
+    x[j] = a + j < nb ? dcnt[a + j] : 0u;
+    s += x[j];
+  }
+  uint32_t all;
+  uint32_t run = part[blockIdx.x] + block_excl_scan<4>(s, wsum, &all);
+#pragma unroll
+  for (int j = 0; j < kPerT; ++j) {
+    if (a + j < nb) dcnt[a + j] = run;
+    run += x[j];
+  }
+}
+
+// one wave per bucket: its trace starts to trace_ptr[tbase[c] ...]
+__global__ __launch_bounds__(256) void bk_tptr_kernel(const uint64_t* __restrict__ tsp,
+                                                      const uint32_t* __restrict__ bstart,
+                                                      const uint32_t* __restrict__ tbase,
+                                                      uint64_t nb,
+                                                      const unsigned long long* __restrict__ total,
+                                                      uint64_t* __restrict__ tptr) {
+  const uint64_t c = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kWv;
+  const uint32_t lane = threadIdx.x & (kWv - 1);
+  if (c >= nb) return;
+  const uint32_t t0 = tbase[c];
+  const uint32_t t1 = c + 1 < nb ? tbase[c + 1] : (uint32_t)*total;
+  const uint64_t src = 4ull * bstart[c];
+  for (uint32_t o = lane; o < t1 - t0; o += kWv) tptr[t0 + o] = tsp[src + o];
+}
+
+inline int env_int(const char* name, int dflt) {
+  const char* s = std::getenv(name);
+  return s && *s ? std::atoi(s) : dflt;
+}
+
+}  // namespace
+
+BucketGeom bucket_geom(uint64_t n) {
+  BucketGeom g;
+  // mean bucket size in (avg/2, avg]; the small kernel holds 2048 spans (at
+  // a mean of 1400 SN spans that is +3.6 sigma: ~1e-4 of the buckets take
+  // the large kernel)
+  int avg = env_int("ANOMOD_BUCKET_AVG", 1400);
+  avg = std::min(std::max(avg, 64), 2048);
+  g.T = 1;
+  while (g.T < 2 * kDMax && (n >> g.T) > (uint64_t)avg) ++g.T;
+  if (g.T <= kDMax) {
+    g.DA = g.T;
+    g.DB = 0;
+  } else {
+    g.DA = (g.T + 1) / 2;
+    g.DB = g.T - g.DA;
+  }
+  g.tilesA = n ? (n + kBTile - 1) / kBTile : 1;
+  g.tilesB = g.DB ? g.tilesA + (1ull << g.DA) : 0;
+  return g;
+}
+
+int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback) {
+  *fallback = false;
+  GroupWs* ws = ctx->group_ws;
+  const uint64_t n = in->n_spans;
+  const BucketGeom g = bucket_geom(n);
+  const int na = 1 << g.DA;
+  const uint64_t nbk = 1ull << g.T;
+  if (nbk > ws->bucket_cap || g.tilesB > ws->tile_cap ||  // sized for the default geometry
+      g.DA > kDMax || g.DB > kDMax) {
+    *fallback = true;
+    return ANOMOD_OK;
+  }
+  const uint64_t cap = ws->cap;
+  auto soa_of = [cap](GRec* buf) {
+    char* ob = reinterpret_cast<char*>(buf);
+    return SoaOut{reinterpret_cast<uint64_t*>(ob), reinterpret_cast<uint64_t*>(ob + 8 * cap),
+                  reinterpret_cast<uint64_t*>(ob + 16 * cap),
+                  reinterpret_cast<uint32_t*>(ob + 24 * cap),
+                  reinterpret_cast<uint32_t*>(ob + 28 * cap)};
+  };
+  const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
+  GRec* bufA = ws->aos[0];
+  GRec* bufB = ws->aos[1];
+  uint16_t* dn = reinterpret_cast<uint16_t*>(ws->dig);
+  hipStream_t st = ctx->stream;
+  ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc, 0, kMiscWords * 8, st));
+
+  // level A
+  const uint64_t nbA = (g.tilesA + kScanRows - 1) / kScanRows;
+  const unsigned dgA = (unsigned)((na + 255) / 256);
+  hipLaunchKernelGGL(bk_count_a_kernel, dim3((unsigned)g.tilesA), dim3(256), 0, st,
+                     in->trace_hash, n, g.DA, ws->tcnt);
+  hipLaunchKernelGGL(bk_scan_up_kernel, dim3((unsigned)nbA, dgA), dim3(256), 0, st, ws->tcnt,
+                     g.tilesA, na, ws->bsum);
+  hipLaunchKernelGGL(bk_scan_top_kernel, dim3(1), dim3(1024), 0, st, ws->bsum, nbA, na, n,
+                     ws->bsA, ws->btile);
+  hipLaunchKernelGGL(bk_scan_down_kernel, dim3((unsigned)nbA, dgA), dim3(256), 0, st, ws->tcnt,
+                     g.tilesA, na, ws->bsum);
+  const GRec* cin;
+  SoaOut cols;
+  const uint32_t* bstart;
+  if (g.DB > 0) {
+    constexpr bool kDnext = (ANOMOD_BK_ABL & 1) == 0;
+    hipLaunchKernelGGL((bk_scatter_kernel<true, false, kDnext>), dim3((unsigned)g.tilesA),
+                       dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
+                       dn, 64 - g.DA - g.DB, (uint32_t)((1u << g.DB) - 1u), nullptr, nullptr,
+                       nullptr, 0);
+    if (ANOMOD_BK_ABL & 2) {  // timing of level A only
+      *fallback = true;
+      return ANOMOD_OK;
+    }
+    hipLaunchKernelGGL(bk_tilemap_kernel, dim3((unsigned)na), dim3(256), 0, st, ws->btile,
+                       ws->tmap);
+    hipLaunchKernelGGL(bk_count_b_kernel, dim3((unsigned)g.tilesB), dim3(256), 0, st,
+                       kDnext ? dn : reinterpret_cast<const uint16_t*>(bufA), ws->bsA,
+                       ws->btile, ws->tmap, na, g.DB, ws->tcnt);
+    hipLaunchKernelGGL(bk_scan_seg_kernel, dim3((unsigned)na), dim3(1024), 0, st, ws->tcnt,
+                       ws->bsA, ws->btile, na, g.DB, ws->bstart);
+    hipLaunchKernelGGL((bk_scatter_kernel<false, true, false>), dim3((unsigned)g.tilesB),
+                       dim3(kBThreads), 0, st, sin, bufA, bufB, n, 64 - g.DA - g.DB, g.DB,
+                       ws->tcnt, nullptr, 0, 0u, ws->bsA, ws->btile, ws->tmap, na);
+    cin = bufB;
+    cols = soa_of(bufA);
+    bstart = ws->bstart;
+  } else {
+    hipLaunchKernelGGL((bk_scatter_kernel<true, false, false>), dim3((unsigned)g.tilesA),
+                       dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
+                       nullptr, 0, 0u, nullptr, nullptr, nullptr, 0);
+    cin = bufA;
+    cols = soa_of(bufB);
+    bstart = ws->bsA;
+  }
+  ANOMOD_HIP(ctx, hipGetLastError());
+
+  // buckets
+  const int kshift = 64 - g.T - kSubBits;
+  hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, cin, cols,
+                     bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                     ws->misc + kMiscTooBig);
+  hipLaunchKernelGGL(bk_bucket_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
+                     dim3(kBigW), 0, st, cin, cols, bstart, kshift, ws->dcnt, ws->over,
+                     ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
+  ANOMOD_HIP(ctx, hipGetLastError());
+
+  // trace_ptr
+  const uint64_t np = (nbk + kDChunk - 1) / kDChunk;  // <= 1024 (T <= 22)
+  hipLaunchKernelGGL(bk_dsum_kernel, dim3((unsigned)np), dim3(256), 0, st, ws->dcnt, nbk,
+                     ws->part);
+  hipLaunchKernelGGL(bk_dscan_top_kernel, dim3(1), dim3(1024), 0, st, ws->part, np,
+                     ws->misc + kMiscTraces, ws->tptr, n);
+  hipLaunchKernelGGL(bk_ddown_kernel, dim3((unsigned)np), dim3(256), 0, st, ws->dcnt, nbk,
+                     ws->part);
+  hipLaunchKernelGGL(bk_tptr_kernel, dim3((unsigned)((nbk * kWv + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint64_t*>(cin), bstart, ws->dcnt, nbk,
+                     ws->misc + kMiscTraces, ws->tptr);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
+                                 (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost, st));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(st));
+  if (ws->h_misc[kMiscTooBig]) {
+    *fallback = true;
+    return ANOMOD_OK;
+  }
+  res->cols = cols;
+  res->n_traces = ws->h_misc[kMiscTraces];
+  res->tptr = ws->tptr;
+  res->passes = g.DB ? 2 : 1;
+  res->bits = g.T;
+  res->bucket = true;
+  return ANOMOD_OK;
+}
+
+}  // namespace anomod

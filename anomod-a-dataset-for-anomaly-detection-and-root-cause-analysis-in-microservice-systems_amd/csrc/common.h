@@ -50,6 +50,7 @@ struct anomod_ctx {
   int* h_status = nullptr;     // pinned host twin
   // Trace-grouping workspace (segmented radix sort of ungrouped span sets).
   anomod::GroupWs* group_ws = nullptr;
+  int group_path = 0, group_levels = 0, group_bits = 0;  // anomod_ctx_group_info
   // Cached device workspace for the edge table.
   void* d_table = nullptr;
   size_t table_bytes = 0;

@@ -39,46 +39,16 @@
 #include <algorithm>
 #include <cmath>
 
+#include <cstdlib>
+
 #include "chunk.h"
-#include "common.h"
+#include "group.h"
 
 namespace anomod {
-
-struct __attribute__((aligned(16))) GRec {
-  uint64_t h, sid, pid;
-  uint32_t sf, dur;
-};
-static_assert(sizeof(GRec) == 32, "32-B records");
-
-struct GroupWs {
-  uint64_t cap = 0;                   // spans the buffers hold
-  GRec* aos[2] = {nullptr, nullptr};  // ping-pong records; the other one holds the SoA output
-  uint64_t* tptr = nullptr;           // [cap + 1]
-  uint64_t* state = nullptr;          // look-back words
-  uint64_t state_words = 0;
-  unsigned long long* misc = nullptr; // counters
-  unsigned long long* list = nullptr; // key changes inside buckets
-  unsigned long long* owned = nullptr;  // mixed buckets sorted into scratch (start << 11 | size)
-  uint32_t* tcnt = nullptr;           // [tiles][256] digit counts, then run starts
-  uint32_t* bsum = nullptr;           // [tiles / 256 + 1][256] block sums of tcnt
-  uint8_t* dig = nullptr;             // [cap + 16] every record's digit of the next pass
-  uint64_t list_cap = 0;
-  uint32_t epoch = 0;
-  unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
-  void* block = nullptr;  // one allocation the device buffers are carved from (ANOMOD_GRP_ONEALLOC)
-};
 
 namespace {
 
 using chunk::wave_sync;
-// The workspace's device buffers are carved (2-MiB aligned) from one
-// allocation; 0 = one hipMalloc per buffer.  The radix passes' time varies by
-// process (98.8-113.4 ms at 2^27 traces over 12 processes of this form,
-// 100.0-112.6 over 8 of the other: no measurable difference); a physically
-// contiguous allocation (hipDeviceMallocContiguous) ran 138-153 ms.
-#ifndef ANOMOD_GRP_ONEALLOC
-#define ANOMOD_GRP_ONEALLOC 1
-#endif
 // Experiment-only ablation (never set in the shipped build; timing only,
 // wrong output): 1 = every pass writes its staged tile to the tile's own rows.
 #ifndef ANOMOD_GRP_ABL
@@ -99,21 +69,6 @@ constexpr int kFixCap = 1024;                // records of a mixed bucket one wa
 constexpr int kFixWaves = 4;
 constexpr uint64_t kValMask = (1ull << 54) - 1;
 constexpr uint32_t kSpinLimit = 1u << 26;
-
-// misc layout (u64 words)
-constexpr int kMiscTicket = 0;                        // [2] tiles of the two scans
-constexpr int kMiscListCnt = kMiscTicket + 2;         // key changes inside buckets
-constexpr int kMiscOver = kMiscListCnt + 1;           // oversized mixed buckets
-constexpr int kMiscTraces = kMiscOver + 1;            // n_traces
-constexpr int kMiscErr = kMiscTraces + 1;             // look-back timeout
-constexpr int kMiscWords = kMiscErr + 1;
-constexpr int kMiscRead = kMiscListCnt;               // [kMiscRead, kMiscWords) read back
-
-__host__ __device__ inline uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 
 __device__ inline uint64_t pack_state(uint32_t epoch, uint32_t flag, uint64_t v) {
   return ((uint64_t)epoch << 56) | ((uint64_t)flag << 54) | (v & kValMask);
@@ -150,22 +105,6 @@ __device__ uint64_t look_back(uint64_t* state, uint64_t stride, uint64_t tile, u
   }
   return excl;
 }
-
-struct SoaIn {
-  const uint64_t* __restrict__ h;
-  const uint64_t* __restrict__ sid;
-  const uint64_t* __restrict__ pid;
-  const uint32_t* __restrict__ sf;
-  const uint32_t* __restrict__ dur;
-};
-
-struct SoaOut {
-  uint64_t* __restrict__ h;
-  uint64_t* __restrict__ sid;
-  uint64_t* __restrict__ pid;
-  uint32_t* __restrict__ sf;
-  uint32_t* __restrict__ dur;
-};
 
 // ---- per-tile digit counts and their exclusive scan over tiles -------------
 // Reduce-then-scan instead of a decoupled look-back: a chained look-back over
@@ -679,46 +618,49 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ws->cap = cap;
   ws->state_words = (cap + kTTile - 1) / kTTile;  // look-back words of the scans
   ws->list_cap = cap / 8 + 65536;
-#if ANOMOD_GRP_ONEALLOC
-  {
-    const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
-                            ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
-                            ws->list_cap * 8, tiles * kDig * 4,
-                            (tiles / kTScanRows + 1) * kDig * 4, cap + 16};
-    void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
-                     (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
-                     (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum, (void**)&ws->dig};
-    constexpr size_t kAlign = size_t(2) << 20;
-    size_t total = 0;
-    for (size_t z : sizes) total += (z + kAlign - 1) / kAlign * kAlign;
-    bool ok1 = hipMalloc(&ws->block, total) == hipSuccess;
+  // Bucket path: any geometry bucket_geom picks for n <= cap (digits of up
+  // to 11 bits per level, 2^T buckets with T at most that of a 64-span mean).
+  int tmax = 1;
+  while (tmax < 22 && (cap >> tmax) > 64u) ++tmax;
+  ws->bucket_cap = 1ull << tmax;
+  ws->tile_cap = tiles + 2048;
+  const size_t tcnt_words = std::max<size_t>(tiles * kDig, ws->tile_cap * 2048);
+  const size_t bsum_words = (tiles / kTScanRows + 2) * 2048;
+  const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
+                          ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
+                          ws->list_cap * 8, tcnt_words * 4, bsum_words * 4, 2 * cap + 32,
+                          (ws->bucket_cap + 1) * 4, 2049 * 4, 2049 * 4, ws->tile_cap * 4,
+                          (ws->bucket_cap + 1) * 4, ws->bucket_cap * 4,
+                          (ws->bucket_cap / 4096 + 2) * 4};
+  void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
+                   (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
+                   (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum, (void**)&ws->dig,
+                   (void**)&ws->bstart, (void**)&ws->bsA, (void**)&ws->btile, (void**)&ws->tmap,
+                   (void**)&ws->dcnt, (void**)&ws->over, (void**)&ws->part};
+  constexpr int kBufs = sizeof(sizes) / sizeof(sizes[0]);
+  static_assert(kBufs == sizeof(ptrs) / sizeof(ptrs[0]), "one pointer per size");
+  // Carved 2-MiB aligned from one allocation (the radix passes' time varies by
+  // process either way: 98.8-113.4 ms at 2^27 traces over 12 processes of
+  // this form, 100.0-112.6 over 8 with one hipMalloc per buffer).
+  constexpr size_t kAlign = size_t(2) << 20;
+  size_t total = 0;
+  for (size_t z : sizes) total += (z + kAlign - 1) / kAlign * kAlign;
+  bool ok = hipMalloc(&ws->block, total) == hipSuccess;
+  if (ok) {
     size_t off = 0;
-    for (int i = 0; ok1 && i < 10; ++i) {
+    for (int i = 0; i < kBufs; ++i) {
       *ptrs[i] = static_cast<char*>(ws->block) + off;
       off += (sizes[i] + kAlign - 1) / kAlign * kAlign;
     }
-    if (!ok1) ws->block = nullptr;
+  } else {
+    ws->block = nullptr;
   }
-  bool ok = ws->block != nullptr;
-#else
-  bool ok = hipMalloc(&ws->aos[0], cap * sizeof(GRec)) == hipSuccess;
-  ok = ok && hipMalloc(&ws->aos[1], cap * sizeof(GRec)) == hipSuccess;
-  ok = ok && hipMalloc(&ws->tptr, (cap + 1) * 8) == hipSuccess;
-  ok = ok && hipMalloc(&ws->state, ws->state_words * 8) == hipSuccess;
-  ok = ok && hipMalloc(&ws->misc, kMiscWords * 8) == hipSuccess;
-  ok = ok && hipMalloc(&ws->list, ws->list_cap * 8) == hipSuccess;
-  ok = ok && hipMalloc(&ws->owned, ws->list_cap * 8) == hipSuccess;
-  ok = ok && hipMalloc(&ws->tcnt, tiles * kDig * 4) == hipSuccess;
-  ok = ok && hipMalloc(&ws->bsum, (tiles / kTScanRows + 1) * kDig * 4) == hipSuccess;
-  ok = ok && hipMalloc(&ws->dig, cap + 16) == hipSuccess;
-#endif
   ok = ok && hipHostMalloc(reinterpret_cast<void**>(&ws->h_misc), kMiscWords * 8,
                            hipHostMallocDefault) == hipSuccess;
   if (!ok) {
     free_group_ws(ctx);
     set_error(ctx, "hipMalloc failed for the trace-grouping workspace of %llu spans "
-              "(~%llu GB)", (unsigned long long)n,
-              (unsigned long long)((cap * 76ull) >> 30));
+              "(~%llu GB)", (unsigned long long)n, (unsigned long long)(total >> 30));
     return ANOMOD_ENOMEM;
   }
   ANOMOD_HIP(ctx, hipMemsetAsync(ws->state, 0, ws->state_words * 8, ctx->stream));
@@ -735,13 +677,12 @@ uint32_t next_epoch(anomod_ctx* ctx) {
   return ++ws->epoch;
 }
 
-// The grouped view of the workspace after a run.
-struct GroupResult {
-  SoaOut cols;
-  uint64_t n_traces = 0;
-  uint64_t* tptr = nullptr;
-  int passes = 0;
-};
+// ANOMOD_GROUP_PATH=lsd: the LSD path even where the bucket path applies
+// (A/B timing, tests).
+bool force_lsd() {
+  const char* e = std::getenv("ANOMOD_GROUP_PATH");
+  return e && e[0] == 'l';
+}
 
 int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
   const uint64_t n = in->n_spans;
@@ -752,6 +693,16 @@ int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
   }
   if (int rc = ensure_group_ws(ctx, n)) return rc;
   GroupWs* ws = ctx->group_ws;
+  if (n > 0 && !force_lsd()) {
+    bool fallback = false;
+    if (int rc = bucket_group_run(ctx, in, res, &fallback)) return rc;
+    if (!fallback) {
+      ctx->group_path = 1;
+      ctx->group_levels = res->passes;
+      ctx->group_bits = res->bits;
+      return ANOMOD_OK;
+    }
+  }
   int P = 1;
   while (P < kMaxPasses && (1ull << (8 * P)) < n) ++P;  // 2^(8P) >= n
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
@@ -837,6 +788,10 @@ int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
     res->n_traces = n > 0 ? hm[kMiscTraces] : 0;
     res->tptr = ws->tptr;
     res->passes = P;
+    res->bits = 8 * P;
+    ctx->group_path = 0;
+    ctx->group_levels = P;
+    ctx->group_bits = 8 * P;
     return ANOMOD_OK;
   }
 }
@@ -864,14 +819,7 @@ void free_group_ws(anomod_ctx* ctx) {
   GroupWs* ws = ctx->group_ws;
   if (!ws) return;
   (void)hipStreamSynchronize(ctx->stream);
-  void* p[] = {ws->aos[0], ws->aos[1], ws->tptr, ws->state, ws->misc, ws->list, ws->owned,
-               ws->tcnt, ws->bsum, ws->dig};
-  if (ws->block) {
-    (void)hipFree(ws->block);
-  } else {
-    for (void* q : p)
-      if (q) (void)hipFree(q);
-  }
+  if (ws->block) (void)hipFree(ws->block);
   if (ws->h_misc) (void)hipHostFree(ws->h_misc);
   delete ws;
   ctx->group_ws = nullptr;
@@ -890,6 +838,14 @@ int anomod_spans_upload_ungrouped(anomod_ctx* ctx, const anomod_span_soa* soa, u
                  "an ungrouped span set needs trace_hash (it defines the traces)");
   if (int rc = anomod_spans_upload(ctx, soa, n_spans, nullptr, 0, out)) return rc;
   (*out)->grouped = false;
+  return ANOMOD_OK;
+}
+
+int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits) {
+  ANOMOD_REQUIRE(nullptr, ctx && path && levels && bits, "anomod_ctx_group_info: NULL argument");
+  *path = ctx->group_path;
+  *levels = ctx->group_levels;
+  *bits = ctx->group_bits;
   return ANOMOD_OK;
 }
 

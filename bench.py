@@ -231,12 +231,31 @@ def edge_leg(ctx, spans, reps: int, what: str) -> dict:
             "achieved_GBps": b / (k * 1e-3) / 1e9, "frac": b / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS}
 
 
-def group_passes(n: int) -> int:
-    """Radix passes anomod_spans_group starts with (csrc/group.hip: 2^(8P) >= n)."""
-    p = 1
-    while p < 8 and (1 << (8 * p)) < n:
-        p += 1
-    return p
+def group_bytes(info: dict, n: int, n_traces: int) -> int:
+    """HBM bytes the grouping moves, by the path that ran (ctx.group_info())."""
+    tiles = -(-n // 4096)
+    if info["path"] == "bucket":
+        # csrc/bucket.hip: level A counts read trace_hash (8 B) and the scatter
+        # moves 32 B in + 32 B out; with two levels it writes each record's
+        # level-B digit (2 B), which the level-B counts read (2 B), and level B
+        # moves 64 B; the bucket kernel reads the records once (32 B) and writes
+        # the SoA columns (32 B); trace starts: written, read, written to
+        # trace_ptr (24 B/trace).  Tile counts (4 B per tile and digit): written,
+        # scanned (read twice, written once), read by the scatter.
+        T, two = info["bits"], info["levels"] == 2
+        da = (T + 1) // 2 if two else T
+        db = T - da if two else 0
+        b = 8 * n + 64 * n + 5 * 4 * tiles * (1 << da)
+        if two:
+            b += 4 * n + 64 * n + 5 * 4 * tiles * (1 << db)
+        return b + 64 * n + 24 * n_traces
+    # csrc/group.hip (LSD): the first pass's tile counts read trace_hash, later
+    # passes' the 1-B digits the previous pass wrote (written + read: 2 B);
+    # each radix pass reads and writes 32 B (records, the last one the SoA
+    # columns); the bucket-list and trace_ptr scans read the grouped hashes;
+    # trace_ptr writes 8 B/trace
+    P = info["levels"]
+    return 8 * n + 2 * (P - 1) * n + 64 * P * n + 16 * n + 8 * n_traces
 
 
 def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
@@ -250,17 +269,12 @@ def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
         wall.append(time.perf_counter() - t0)
         g.append(ctx.stage_ms(L.STAGE_GROUP))
         e.append(ctx.stage_ms(L.STAGE_EDGE_AGG))
-    n, P = inter.n_spans, group_passes(inter.n_spans)
-    # bytes the grouping moves (csrc/group.hip): the first pass's tile counts
-    # read trace_hash, later passes' the 1-B digits the previous pass wrote
-    # (written + read: 2 B); each radix pass reads and writes 32 B (records,
-    # the last one the SoA columns); the bucket-list and trace_ptr scans read
-    # the grouped hashes; trace_ptr writes 8 B/trace
-    gbytes = 8 * n + 2 * (P - 1) * n + 64 * P * n + 16 * n + 8 * n_traces
+    n, info = inter.n_spans, ctx.group_info()
+    gbytes = group_bytes(info, n, n_traces)
     g_ms, e_ms = float(np.mean(g)), float(np.mean(e))
     return {"what": "SN spans of every 4096 consecutive traces interleaved (ES start_time "
                     "order); step = device grouping + edge aggregation",
-            "spans": n, "traces": n_traces, "radix_passes": P,
+            "spans": n, "traces": n_traces, "group_path": info,
             "spans_per_s": allsum(n / float(np.mean(wall))), "step_ms": float(np.mean(wall)) * 1e3,
             "group_ms": g_ms, "edge_ms": e_ms,
             "group_bytes": gbytes, "group_GBps": gbytes / (g_ms * 1e-3) / 1e9,

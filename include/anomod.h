@@ -163,6 +163,12 @@ int anomod_spans_upload_ungrouped(anomod_ctx* ctx, const anomod_span_soa* soa, u
                                   anomod_spans** out);
 int anomod_spans_grouped(const anomod_spans* spans, int* grouped);
 int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* ungrouped, anomod_spans** grouped);
+/* How the ctx's last grouping ran (csrc/group.hip, csrc/bucket.hip):
+ * *path = 1 bucket path (two stable MSD scatters over the top *bits bits of
+ * mix64(trace_hash), then one workgroup per bucket), 0 LSD path (8-bit radix
+ * passes + bucket fix-up); *levels = scatter levels / radix passes run;
+ * *bits = bucket bits (bucket path) or 8 * passes.  All 0 before any grouping. */
+int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits);
 /* Rearranged copies of a grouped set (synthetic arrival orders for tests
  * and benchmarks): window_traces = 0 shuffles the spans inside every trace
  * (the result stays grouped); window_traces = W interleaves the spans of

@@ -75,11 +75,20 @@ def main() -> int:
             seg = max(l, 16384 // l * l)
             per_unit["ewma_zt_kernel"] = -(-e["steps_per_chunk"] // seg)
         if "ungrouped" in bench:
-            # a radix pass reads and writes one 32-B record per span; every pass
-            # but the last also writes the next pass's 1-B digit
             u = bench["ungrouped"]
-            P = u["radix_passes"]
-            alg["group_scatter_kernel"] = (64 + (P - 1) / P) * u["spans"]
+            info = u.get("group_path", {"path": "lsd", "levels": u.get("radix_passes", 4)})
+            if info["path"] == "bucket":
+                # a scatter level reads and writes one 32-B record per span (the
+                # first also writes the next level's 2-B digit: averaged); the
+                # bucket kernel reads the records and writes the SoA columns
+                lv = info["levels"]
+                alg["bk_scatter_kernel"] = (64 + 2 * (lv - 1) / lv) * u["spans"]
+                alg["bk_bucket_kernel"] = 64 * u["spans"]
+            else:
+                # a radix pass reads and writes one 32-B record per span; every
+                # pass but the last also writes the next pass's 1-B digit
+                P = info["levels"]
+                alg["group_scatter_kernel"] = (64 + (P - 1) / P) * u["spans"]
     kernels = {}
     for k, a in alg.items():
         fetch = counter(prof / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)

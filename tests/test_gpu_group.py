@@ -182,3 +182,41 @@ def test_large_interleaved_conservation(ctx):
         np.testing.assert_array_equal(getattr(got, k), getattr(want, k), err_msg=k)
     g = ctx.group(inter)
     assert g.n_traces == 1 << 23 and g.n_spans == inter.n_spans
+
+
+@pytest.fixture
+def env_knob(monkeypatch):
+    """Set a libanomod environment knob for one test (read on every call)."""
+    return monkeypatch.setenv
+
+
+@pytest.mark.parametrize("path,avg", [("lsd", None), ("bucket", "64"), ("bucket", "1024")])
+def test_group_paths_agree(ctx, env_knob, path, avg):
+    """The LSD path (ANOMOD_GROUP_PATH=lsd) and the bucket path at the
+    smallest / largest mean bucket size (ANOMOD_BUCKET_AVG: one or two
+    scatter levels, most buckets in the small or the large per-bucket
+    kernel) give the oracle's grouping."""
+    if path == "lsd":
+        env_knob("ANOMOD_GROUP_PATH", "lsd")
+    else:
+        env_knob("ANOMOD_BUCKET_AVG", avg)
+    rng = np.random.default_rng(77)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 60000, 40, dup=0.02), rng)
+    big = _with_trace_hashes(_random_spanset(rng, 12, 4, 1500, dup=0.02), rng)
+    flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "time")
+    g = ctx.group(ctx.upload_ungrouped(flat))
+    _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+
+
+def test_group_bucket_overflow_falls_back(ctx):
+    """Traces of 1000-5000 spans overfill their buckets (small per-bucket
+    kernel: 1024 spans) and take the large kernel (8192 spans); a 12 000-span
+    trace fills a bucket beyond that, and the call regroups with the LSD
+    path.  Same grouping either way."""
+    rng = np.random.default_rng(78)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 20000, 16, dup=0.02), rng)
+    for lens in (rng.integers(1000, 5000, 6), np.r_[12000, rng.integers(1000, 5000, 3)]):
+        big = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02, lens=lens), rng)
+        flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "random")
+        g = ctx.group(ctx.upload_ungrouped(flat))
+        _assert_grouped_equal(g.download(), _oracle_grouped(flat))
