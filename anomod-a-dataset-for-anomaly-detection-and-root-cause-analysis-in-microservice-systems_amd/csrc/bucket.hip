@@ -18,6 +18,7 @@
 // 8192-span capacity works through; a bucket beyond that (a single trace of
 // thousands of spans near others) makes the caller regroup with the LSD path.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "chunk.h"
@@ -30,9 +31,9 @@ using chunk::wave_sync;
 // Experiment-only builds (never set in the shipped library):
 //  1 = level B counts its digits from the level-A records (no 2-B digit array);
 //  2 = level A stores nothing, then the LSD path groups (timing of level A's
-//      loads and ranking only);
-//  4 = scatter levels stage whole 32-B records (one stage / write phase; digit
-//      levels of at most 9 bits, else the LSD path groups).
+//      loads and ranking only).
+
+
 #ifndef ANOMOD_BK_ABL
 #define ANOMOD_BK_ABL 0
 #endif
@@ -41,14 +42,10 @@ constexpr int kBThreads = 1024;                // scatter workgroup
 constexpr int kBWaves = kBThreads / kWv;       // 16
 constexpr int kBPer = 4;                       // records per thread
 constexpr int kBTile = kBThreads * kBPer;      // 4096 records per tile
-#if ANOMOD_BK_ABL & 4
-constexpr int kDMax = 9;                       // digit bits per scatter level
-#else
 constexpr int kDMax = 11;                      // digit bits per scatter level
-#endif
 constexpr int kNDMax = 1 << kDMax;
 constexpr int kScanRows = 256;                 // tiles per block of the tile scan
-constexpr int kSubBits = 8;                    // per-bucket split before the key compare
+constexpr int kSubBits = 9;                    // per-bucket split before the key compare
 constexpr int kSub = 1 << kSubBits;
 constexpr int kSmallW = 512, kSmallPer = 4;    // per-bucket kernel: 2048 spans
 constexpr int kBigW = 1024, kBigPer = 8;       // oversized buckets: 8192 spans
@@ -205,7 +202,8 @@ __global__ __launch_bounds__(256) void bk_count_b_kernel(const uint16_t* __restr
   for (uint64_t p = tid; p < nvalid; p += 256)
     atomicAdd(&lh[(uint32_t)(mix64(rec[base + p].h) >> sh) & (uint32_t)(nd - 1)], 1u);
 #else
-  for (uint64_t p = tid; p < nvalid; p += 256) atomicAdd(&lh[dn[base + p]], 1u);
+  const int dsh = kDMax - db;  // dn holds the kDMax bits below level A's
+  for (uint64_t p = tid; p < nvalid; p += 256) atomicAdd(&lh[dn[base + p] >> dsh], 1u);
 #endif
   __syncthreads();
   for (int i = tid; i < nd; i += 256) tcnt[(uint64_t)blockIdx.x * nd + i] = lh[i];
@@ -251,22 +249,30 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
 // Tile = 4096 records (1024 threads x 4; wave w owns positions [256w, 256w +
 // 256)), ranked with wave ballots (dbits ballots give each lane its
 // same-digit peers; a per-wave LDS counter per digit carries the count down
-// the wave's rows), staged in LDS in digit order one 16-B half at a time and
-// written as digit runs from the tile's global run starts.  Level A reads the
-// SoA columns and writes every record's level-B digit beside it.
+// the wave's rows), staged whole in LDS in digit order — over the per-wave
+// counters, which are dead by then — and written as 16-B chunks, a wave
+// instruction covering 32 consecutive staged records (1 KiB, runs of ~4-8
+// records to one place each at 9-10 digit bits).  Level A reads the SoA
+// columns and writes every record's level-B digit beside it.
+// (Measured at 2^25 SN traces, 9-bit levels: half-record staging with one
+// 16-B store per lane and record half 9.2 / 6.0 ms for levels A / B; whole
+// records 6.0 / 5.4; no stores at all 1.0 ms — the scattered writes are the
+// cost.)
 template <bool SOA_IN, bool SEG, bool DNEXT>
 __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
     int dbits, const uint32_t* __restrict__ toff, uint16_t* __restrict__ dnext, int nshift,
     uint32_t nmask, const uint32_t* __restrict__ bsA, const uint32_t* __restrict__ btile,
     const uint32_t* __restrict__ tmap, int na) {
-  constexpr bool kFull = (ANOMOD_BK_ABL & 4) != 0;
   constexpr bool kNoStore = (ANOMOD_BK_ABL & 2) != 0 && SOA_IN;
-  __shared__ uint4 stage[kBTile * (kFull ? 2 : 1)];  // 64 KiB: one half of every record
-  __shared__ uint16_t wcnt[kBWaves][kNDMax];   // per-wave digit counts, then wave offsets
-  __shared__ uint16_t sdig[kBTile];
-  __shared__ uint32_t tstart[kNDMax];          // tile-local start of each digit
-  __shared__ uint32_t gbase[kNDMax];           // global start of each digit's run
+  static_assert(kBWaves * kNDMax * 2 <= kBTile * 32, "counters fit under the stage");
+  union Lds {
+    uint4 stage[2 * kBTile];              // 128 KiB: the tile's records in digit order
+    uint16_t wcnt[kBWaves][kNDMax];       // per-wave digit counts, then wave offsets
+  };
+  __shared__ Lds u;
+  __shared__ uint32_t tstart[kNDMax];     // tile-local start of each digit
+  __shared__ uint32_t gbase[kNDMax];      // global start of each digit's run
   __shared__ uint32_t wsum[kBWaves];
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   const int nd = 1 << dbits;
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     d[k] = (uint32_t)(mix64(((uint64_t)ra[k].y << 32) | ra[k].x) >> shift) & (uint32_t)(nd - 1);
   }
   for (int ww = 0; ww < kBWaves; ++ww)
-    for (int dd = tid; dd < nd; dd += kBThreads) wcnt[ww][dd] = 0;
+    for (int dd = tid; dd < nd; dd += kBThreads) u.wcnt[ww][dd] = 0;
   for (int dd = tid; dd < nd; dd += kBThreads) gbase[dd] = toff[tile * nd + dd];
   __syncthreads();
 
@@ -320,9 +326,9 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     off[k] = 0;
     if (v[k]) {
       const uint64_t lower = peers & lt_mask;
-      const uint32_t b0 = wcnt[w][d[k]];
+      const uint32_t b0 = u.wcnt[w][d[k]];
       off[k] = b0 + (uint32_t)__popcll(lower);
-      if (lower == 0ull) wcnt[w][d[k]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
+      if (lower == 0ull) u.wcnt[w][d[k]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
     }
     wave_sync();
   }
@@ -336,8 +342,8 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     if (dd >= nd) continue;
     uint32_t run = 0;
     for (int ww = 0; ww < kBWaves; ++ww) {
-      const uint32_t c = wcnt[ww][dd];
-      wcnt[ww][dd] = (uint16_t)run;
+      const uint32_t c = u.wcnt[ww][dd];
+      u.wcnt[ww][dd] = (uint16_t)run;
       run += c;
     }
     tot[i] = run;
@@ -349,49 +355,35 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     if (dd < nd) tstart[dd] = pre + (i ? tot[0] : 0u);
   }
   __syncthreads();
-
   uint32_t lp[kBPer];
 #pragma unroll
+  for (int k = 0; k < kBPer; ++k) lp[k] = v[k] ? tstart[d[k]] + u.wcnt[w][d[k]] + off[k] : 0u;
+  __syncthreads();  // the counters are dead: the stage goes over them
+#pragma unroll
   for (int k = 0; k < kBPer; ++k) {
-    lp[k] = 0;
     if (v[k]) {
-      lp[k] = tstart[d[k]] + wcnt[w][d[k]] + off[k];
-      if constexpr (kFull) {
-        stage[2 * lp[k]] = ra[k];
-        stage[2 * lp[k] + 1] = rb[k];
-      } else {
-        stage[lp[k]] = ra[k];
-      }
-      sdig[lp[k]] = (uint16_t)d[k];
+      u.stage[2 * lp[k]] = ra[k];
+      u.stage[2 * lp[k] + 1] = rb[k];
     }
   }
   __syncthreads();
   if constexpr (kNoStore) return;
-  uint64_t g[kBPer];
+  // 16-B chunks in staged order: chunk c is half (c & 1) of staged record c / 2
+  const uint64_t nch = 2 * nvalid;
 #pragma unroll
-  for (int k = 0; k < kBPer; ++k) {
-    const uint32_t p = (uint32_t)(tid + k * kBThreads);
-    g[k] = 0;
-    if (p < nvalid) {
-      const uint32_t dd = sdig[p];
-      g[k] = (uint64_t)gbase[dd] + (p - tstart[dd]);
-      const uint4 x = stage[kFull ? 2 * p : p];
-      reinterpret_cast<uint4*>(aout + g[k])[0] = x;
-      if constexpr (kFull) reinterpret_cast<uint4*>(aout + g[k])[1] = stage[2 * p + 1];
+  for (int j = 0; j < 2 * kBPer; ++j) {
+    const uint32_t c = (uint32_t)(tid + j * kBThreads);
+    if (c < nch) {
+      const uint32_t p = c >> 1;
+      const uint4 x = u.stage[c];
+      const uint4 x0 = (c & 1u) ? u.stage[c - 1] : x;  // the record's (h, sid) half
+      const uint64_t k = mix64(((uint64_t)x0.y << 32) | x0.x);
+      const uint32_t dd = (uint32_t)(k >> shift) & (uint32_t)(nd - 1);
+      const uint64_t g = (uint64_t)gbase[dd] + (p - tstart[dd]);
+      reinterpret_cast<uint4*>(aout)[2 * g + (c & 1u)] = x;
       if constexpr (DNEXT)
-        dnext[g[k]] = (uint16_t)((mix64(((uint64_t)x.y << 32) | x.x) >> nshift) & nmask);
+        if (!(c & 1u)) dnext[g] = (uint16_t)((k >> nshift) & nmask);
     }
-  }
-  if constexpr (kFull) return;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kBPer; ++k)
-    if (v[k]) stage[lp[k]] = rb[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kBPer; ++k) {
-    const uint32_t p = (uint32_t)(tid + k * kBThreads);
-    if (p < nvalid) reinterpret_cast<uint4*>(aout + g[k])[1] = stage[p];
   }
 }
 
@@ -401,19 +393,146 @@ struct BucketLds {
   static constexpr int kCap = W * PER, kNW = W / kWv;
   struct Pre {
     uint64_t skey[kCap];          // keys in sub-digit order
-    uint64_t kmin[kSub], kmax[kSub];
+    uint32_t mixed[kSub];         // sub-bucket holds more than one key
     uint32_t tstart[kSub + 1];
     uint16_t sorig[kCap];         // arrival position of every staged key
     uint16_t wcnt[kNW][kSub];
     uint8_t sflag[kCap];          // trace start at final position f
   };
   union {
-    uint4 stage[kCap];            // one 16-B half of every record, final order
     Pre pre;
   } u;
   uint16_t sfinal[kCap];          // final position of every arrival position
   uint32_t wsum[kNW];
 };
+
+// A bucket beyond the large kernel (a trace of thousands of spans, or two
+// such traces side by side): its distinct keys (at most kHugeKeys) counted in
+// an LDS hash table and ranked, then ONE wave walks the records in arrival
+// order and sends each to its trace's next row (peers of a row found by
+// ballots over the slot index; a per-slot running row in LDS) — stable, and
+// O(m) for any size.  More distinct keys than that sends the set to the LSD
+// path.  Uses the large kernel's LDS (>= 82 KiB) as raw bytes.
+constexpr uint32_t kHugeSlots = 4096;
+constexpr uint32_t kHugeKeys = 2048;
+constexpr uint64_t kEmptyKey = ~0ull;
+
+__device__ inline int huge_slot(const uint64_t* hkey, uint64_t k) {
+  uint32_t s = (uint32_t)k & (kHugeSlots - 1u);
+  for (uint32_t probe = 0; probe < kHugeSlots; ++probe) {
+    const uint64_t cur = hkey[s];
+    if (cur == k) return (int)s;
+    if (cur == kEmptyKey) return -1;
+    s = (s + 1u) & (kHugeSlots - 1u);
+  }
+  return -1;
+}
+
+template <int W>
+__device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_t m,
+                            const GRec* __restrict__ in, SoaOut out, uint32_t* __restrict__ dcnt,
+                            unsigned long long* __restrict__ too_big) {
+  constexpr int kNW = W / kWv;
+  uint64_t* hkey = reinterpret_cast<uint64_t*>(lds);               // [kHugeSlots]
+  uint32_t* hcnt = reinterpret_cast<uint32_t*>(lds + 32768);       // count, then next row
+  uint32_t* hrank = reinterpret_cast<uint32_t*>(lds + 49152);      // rank of the slot's key
+  uint32_t* rrow = reinterpret_cast<uint32_t*>(lds + 65536);       // [kHugeKeys] by rank
+  uint32_t* slots = reinterpret_cast<uint32_t*>(lds + 73728);      // [kHugeKeys] occupied
+  uint32_t* hm = reinterpret_cast<uint32_t*>(lds + 81920);         // distinct, failed, listed
+  uint32_t* wsum = hm + 4;                                          // [kNW]
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  for (uint32_t i = tid; i < kHugeSlots; i += W) {
+    hkey[i] = kEmptyKey;
+    hcnt[i] = 0u;
+  }
+  if (tid < 4) hm[tid] = 0u;
+  __syncthreads();
+  for (uint32_t p = tid; p < m; p += W) {
+    const uint64_t k = mix64(in[a0 + p].h);
+    bool done = k == kEmptyKey;  // the table's empty mark: LSD path
+    if (done) hm[1] = 1u;
+    uint32_t s = (uint32_t)k & (kHugeSlots - 1u);
+    for (uint32_t probe = 0; !done && probe < kHugeSlots; ++probe) {
+      uint64_t cur = hkey[s];
+      if (cur == kEmptyKey) {
+        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&hkey[s]),
+                                        (unsigned long long)kEmptyKey, (unsigned long long)k);
+        if (prev == kEmptyKey) atomicAdd(&hm[0], 1u);
+        cur = prev == kEmptyKey ? k : prev;
+      }
+      if (cur == k) {
+        atomicAdd(&hcnt[s], 1u);
+        done = true;
+      }
+      s = (s + 1u) & (kHugeSlots - 1u);
+    }
+    if (!done) hm[1] = 1u;
+  }
+  __syncthreads();
+  const uint32_t d = hm[0];
+  if (hm[1] || d > kHugeKeys) {
+    if (tid == 0) atomicAdd(too_big, 1ull);
+    return;
+  }
+  for (uint32_t i = tid; i < kHugeSlots; i += W)
+    if (hkey[i] != kEmptyKey) slots[atomicAdd(&hm[2], 1u)] = i;
+  __syncthreads();
+  for (uint32_t j = tid; j < d; j += W) {  // rank = keys below (d is small)
+    const uint32_t sj = slots[j];
+    const uint64_t kj = hkey[sj];
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < d; ++i) r += hkey[slots[i]] < kj ? 1u : 0u;
+    hrank[sj] = r;
+    rrow[r] = hcnt[sj];
+  }
+  __syncthreads();
+  const uint32_t x0 = 2u * tid < d ? rrow[2 * tid] : 0u;
+  const uint32_t x1 = 2u * tid + 1u < d ? rrow[2 * tid + 1] : 0u;
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kNW>(x0 + x1, wsum, &all);
+  if (2u * tid < d) rrow[2 * tid] = pre;
+  if (2u * tid + 1u < d) rrow[2 * tid + 1] = pre + x0;
+  __syncthreads();
+  for (uint32_t i = tid; i < kHugeSlots; i += W)
+    if (hkey[i] != kEmptyKey) hcnt[i] = rrow[hrank[i]];
+  __syncthreads();
+  if (w == 0) {
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (uint32_t p0 = 0; p0 < m; p0 += kWv) {
+      const uint32_t p = p0 + (uint32_t)lane;
+      const bool v = p < m;
+      uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+      if (v) {
+        const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+        r0 = q[0];
+        r1 = q[1];
+      }
+      const int sl = v ? huge_slot(hkey, mix64(((uint64_t)r0.y << 32) | r0.x)) : 0;
+      const uint32_t su = (uint32_t)(sl < 0 ? 0 : sl);
+      uint64_t peers = __ballot(v);
+      for (int b = 0; b < 12; ++b) {
+        const bool bit = (su >> b) & 1u;
+        const uint64_t bb = __ballot(v && bit);
+        peers &= bit ? bb : ~bb;
+      }
+      const uint32_t row = v ? hcnt[su] + (uint32_t)__popcll(peers & lt_mask) : 0u;
+      wave_sync();
+      if (v && (peers >> lane) == 1ull) hcnt[su] += (uint32_t)__popcll(peers);
+      wave_sync();
+      if (v) {
+        out.h[a0 + row] = ((uint64_t)r0.y << 32) | r0.x;
+        out.sid[a0 + row] = ((uint64_t)r0.w << 32) | r0.z;
+        out.pid[a0 + row] = ((uint64_t)r1.y << 32) | r1.x;
+        out.sf[a0 + row] = r1.z;
+        out.dur[a0 + row] = r1.w;
+      }
+    }
+  }
+  __syncthreads();  // every record read before the trace starts go over them
+  uint64_t* tsp = reinterpret_cast<uint64_t*>(const_cast<GRec*>(in)) + 4ull * a0;
+  for (uint32_t r = tid; r < d; r += W) tsp[r] = (uint64_t)a0 + rrow[r];
+  if (tid == 0) dcnt[c] = d;
+}
 
 // Bucket c = [bstart[c], bstart[c + 1]) of `in` (records in arrival order
 // inside the bucket; every k shares its top T bits).  Split once more by the
@@ -434,37 +553,49 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
   if (m > (uint32_t)kCap) {
-    if (tid == 0) {
-      if (small) {
+    if (small) {
+      if (tid == 0) {
         const unsigned long long i = atomicAdd(over_n, 1ull);
         if (i < over_cap) over[i] = c;
         else atomicAdd(too_big, 1ull);
-      } else {
-        atomicAdd(too_big, 1ull);
       }
+      return;
     }
+    if constexpr (sizeof(BucketLds<W, PER>) >= 81920 + 16 + 4 * (W / kWv))
+      bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, in, out, dcnt, too_big);
+    else if (tid == 0)
+      atomicAdd(too_big, 1ull);
     return;
   }
   if (m == 0) {
     if (tid == 0) dcnt[c] = 0;
     return;
   }
-  // keys only; the records are read again (from L2) when staged in final order
+  // REG (the small kernel): whole records held in registers; else keys only,
+  // the records read again (from L2) when staged in final order.  (2^25 SN
+  // traces: 6.14 ms re-reading, 5.32 holding; 64-bit LDS min / max atomics
+  // for the one-key test instead of the flag pass: +1.1 ms.)
+  constexpr bool REG = PER <= 4;
   uint64_t k[PER];
   uint32_t e[PER], off[PER];
   bool v[PER];
+  uint4 ra[REG ? PER : 1], rb[REG ? PER : 1];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
     v[j] = p < m;
-    k[j] = v[j] ? mix64(in[a0 + p].h) : 0ull;
+    if constexpr (REG) {
+      const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+      ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+      rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+      k[j] = mix64(((uint64_t)ra[j].y << 32) | ra[j].x);
+    } else {
+      k[j] = v[j] ? mix64(in[a0 + p].h) : 0ull;
+    }
     e[j] = (uint32_t)(k[j] >> kshift) & (kSub - 1);
   }
   for (int i = tid; i < kNW * kSub; i += W) (&P.wcnt[0][0])[i] = 0;
-  for (int i = tid; i < kSub; i += W) {
-    P.kmin[i] = ~0ull;
-    P.kmax[i] = 0ull;
-  }
+  for (int i = tid; i < kSub; i += W) P.mixed[i] = 0u;
   __syncthreads();
 
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -483,8 +614,6 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
       const uint32_t b0 = P.wcnt[w][e[j]];
       off[j] = b0 + (uint32_t)__popcll(lower);
       if (lower == 0ull) P.wcnt[w][e[j]] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
-      atomicMin(reinterpret_cast<unsigned long long*>(&P.kmin[e[j]]), (unsigned long long)k[j]);
-      atomicMax(reinterpret_cast<unsigned long long*>(&P.kmax[e[j]]), (unsigned long long)k[j]);
     }
     wave_sync();
   }
@@ -513,6 +642,17 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
     }
   }
   __syncthreads();
+  // one key per sub-bucket? (plain stores of 1: any writer will do)
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t sp = (uint32_t)(tid + j * W);
+    if (sp < m) {
+      const uint64_t kp = P.skey[sp];
+      const uint32_t ee = (uint32_t)(kp >> kshift) & (kSub - 1);
+      if (kp != P.skey[P.tstart[ee]]) P.mixed[ee] = 1u;
+    }
+  }
+  __syncthreads();
 
   // final position inside the bucket
 #pragma unroll
@@ -523,17 +663,24 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
       const uint32_t ee = (uint32_t)(kp >> kshift) & (kSub - 1);
       const uint32_t a = P.tstart[ee], b = P.tstart[ee + 1];
       uint32_t rank, first;
-      if (P.kmin[ee] == P.kmax[ee]) {
+      if (!P.mixed[ee]) {
         rank = sp - a;
         first = sp == a;
       } else {
         rank = 0;
         first = 1;
-        for (uint32_t q = a; q < b; ++q) {
-          const uint64_t kq = P.skey[q];
-          const bool eq_before = kq == kp && q < sp;
-          rank += (kq < kp || eq_before) ? 1u : 0u;
-          first &= eq_before ? 0u : 1u;
+        for (uint32_t q0 = a; q0 < b; q0 += 4) {  // 4 keys per step: one LDS round trip
+          uint64_t kq[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) kq[t] = P.skey[q0 + t < b ? q0 + t : a];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint32_t q = q0 + t;
+            const bool in = q < b;
+            const bool eq_before = in && kq[t] == kp && q < sp;
+            rank += (in && (kq[t] < kp || eq_before)) ? 1u : 0u;
+            first &= eq_before ? 0u : 1u;
+          }
         }
       }
       const uint32_t f = a + rank;
@@ -561,40 +708,30 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
   }
   __syncthreads();
 
-  // the records in final order, one half at a time, written coalesced
-  const uint4* src = reinterpret_cast<const uint4*>(in + a0);
+  // each record straight to its final row (the bucket's rows of every column
+  // are a few KiB: the stores merge in L2)
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-    if (v[j]) L.u.stage[L.sfinal[p]] = src[2 * p];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t i = (uint32_t)(tid + j * W);
-    if (i < m) {
-      const uint4 x = L.u.stage[i];
-      out.h[a0 + i] = ((uint64_t)x.y << 32) | x.x;
-      out.sid[a0 + i] = ((uint64_t)x.w << 32) | x.z;
+    if (v[j]) {
+      uint4 x0, x1;
+      if constexpr (REG) {
+        x0 = ra[j];
+        x1 = rb[j];
+      } else {
+        const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+        x0 = q[0];
+        x1 = q[1];
+      }
+      const uint32_t i = L.sfinal[p];
+      out.h[a0 + i] = ((uint64_t)x0.y << 32) | x0.x;
+      out.sid[a0 + i] = ((uint64_t)x0.w << 32) | x0.z;
+      out.pid[a0 + i] = ((uint64_t)x1.y << 32) | x1.x;
+      out.sf[a0 + i] = x1.z;
+      out.dur[a0 + i] = x1.w;
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-    if (v[j]) L.u.stage[L.sfinal[p]] = src[2 * p + 1];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t i = (uint32_t)(tid + j * W);
-    if (i < m) {
-      const uint4 x = L.u.stage[i];
-      out.pid[a0 + i] = ((uint64_t)x.y << 32) | x.x;
-      out.sf[a0 + i] = x.z;
-      out.dur[a0 + i] = x.w;
-    }
-  }
+  __syncthreads();  // every record read before tsp goes over them
   uint64_t* tsp = reinterpret_cast<uint64_t*>(const_cast<GRec*>(in)) + 4ull * a0;
   uint32_t ord = ord0;
 #pragma unroll
@@ -624,6 +761,22 @@ __global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
                                     nullptr, 0, too_big);
     __syncthreads();
   }
+}
+
+// Largest bucket -> *mx (the host skips the bucket kernels when one cannot hold it).
+__global__ __launch_bounds__(256) void bk_maxsize_kernel(const uint32_t* __restrict__ bstart,
+                                                         uint64_t nb,
+                                                         unsigned long long* __restrict__ mx) {
+  uint32_t m = 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < nb; c += (uint64_t)gridDim.x * 256) {
+    const uint32_t s = bstart[c + 1] - bstart[c];
+    m = s > m ? s : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = __shfl_xor(m, o);
+    m = y > m ? y : m;
+  }
+  if ((threadIdx.x & (kWv - 1)) == 0) atomicMax(mx, (unsigned long long)m);
 }
 
 // ---- trace_ptr from the buckets' trace starts --------------------------------
@@ -722,14 +875,30 @@ BucketGeom bucket_geom(uint64_t n) {
   return g;
 }
 
-int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback) {
+namespace {
+
+// Largest bucket of bstart[0 .. nbk] (one host wait).
+int max_bucket(anomod_ctx* ctx, const uint32_t* bstart, uint64_t nbk, uint64_t* mx) {
+  GroupWs* ws = ctx->group_ws;
+  hipStream_t st = ctx->stream;
+  ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc + kMiscTooBig, 0, 8, st));
+  hipLaunchKernelGGL(bk_maxsize_kernel, dim3((unsigned)std::min<uint64_t>((nbk + 255) / 256, 1024)),
+                     dim3(256), 0, st, bstart, nbk, ws->misc + kMiscTooBig);
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscTooBig, ws->misc + kMiscTooBig, 8,
+                                 hipMemcpyDeviceToHost, st));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(st));
+  *mx = ws->h_misc[kMiscTooBig];
+  return hipMemsetAsync(ws->misc + kMiscTooBig, 0, 8, st) == hipSuccess ? ANOMOD_OK : ANOMOD_EHIP;
+}
+
+int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, GroupResult* res,
+                    bool* fallback, bool* escalate) {
   *fallback = false;
+  *escalate = false;
   GroupWs* ws = ctx->group_ws;
   const uint64_t n = in->n_spans;
-  const BucketGeom g = bucket_geom(n);
   const int na = 1 << g.DA;
-  const uint64_t nbk = 1ull << g.T;
-  if (nbk > ws->bucket_cap || g.tilesB > ws->tile_cap ||  // sized for the default geometry
+  if ((1ull << g.T) > ws->bucket_cap || g.tilesB > ws->tile_cap ||  // sized for the geometry
       g.DA > kDMax || g.DB > kDMax) {
     *fallback = true;
     return ANOMOD_OK;
@@ -763,11 +932,15 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
   const GRec* cin;
   SoaOut cols;
   const uint32_t* bstart;
+  uint64_t mx = 0;
   if (g.DB > 0) {
+    // every record's next kDMax key bits beside it, so level B can count with
+    // any digit width up to kDMax (a wider level B is the retry for a set
+    // whose buckets outgrow the large kernel)
     constexpr bool kDnext = (ANOMOD_BK_ABL & 1) == 0;
     hipLaunchKernelGGL((bk_scatter_kernel<true, false, kDnext>), dim3((unsigned)g.tilesA),
                        dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
-                       dn, 64 - g.DA - g.DB, (uint32_t)((1u << g.DB) - 1u), nullptr, nullptr,
+                       dn, 64 - g.DA - kDMax, (uint32_t)((1u << kDMax) - 1u), nullptr, nullptr,
                        nullptr, 0);
     if (ANOMOD_BK_ABL & 2) {  // timing of level A only
       *fallback = true;
@@ -775,11 +948,23 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
     }
     hipLaunchKernelGGL(bk_tilemap_kernel, dim3((unsigned)na), dim3(256), 0, st, ws->btile,
                        ws->tmap);
-    hipLaunchKernelGGL(bk_count_b_kernel, dim3((unsigned)g.tilesB), dim3(256), 0, st,
-                       kDnext ? dn : reinterpret_cast<const uint16_t*>(bufA), ws->bsA,
-                       ws->btile, ws->tmap, na, g.DB, ws->tcnt);
-    hipLaunchKernelGGL(bk_scan_seg_kernel, dim3((unsigned)na), dim3(1024), 0, st, ws->tcnt,
-                       ws->bsA, ws->btile, na, g.DB, ws->bstart);
+    for (;;) {
+      hipLaunchKernelGGL(bk_count_b_kernel, dim3((unsigned)g.tilesB), dim3(256), 0, st,
+                         kDnext ? dn : reinterpret_cast<const uint16_t*>(bufA), ws->bsA,
+                         ws->btile, ws->tmap, na, g.DB, ws->tcnt);
+      hipLaunchKernelGGL(bk_scan_seg_kernel, dim3((unsigned)na), dim3(1024), 0, st, ws->tcnt,
+                         ws->bsA, ws->btile, na, g.DB, ws->bstart);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      if (int rc = max_bucket(ctx, ws->bstart, 1ull << g.T, &mx)) return rc;
+      if (env_int("ANOMOD_BUCKET_DEBUG", 0))
+        std::fprintf(stderr, "bucket path: DA=%d DB=%d max bucket %llu\n", g.DA, g.DB,
+                     (unsigned long long)mx);
+      if (mx <= (uint64_t)(kBigW * kBigPer) || g.DB == kDMax ||
+          (1ull << (g.DA + kDMax)) > ws->bucket_cap)
+        break;
+      g.DB = kDMax;  // long traces side by side: split finer
+      g.T = g.DA + g.DB;
+    }
     hipLaunchKernelGGL((bk_scatter_kernel<false, true, false>), dim3((unsigned)g.tilesB),
                        dim3(kBThreads), 0, st, sin, bufA, bufB, n, 64 - g.DA - g.DB, g.DB,
                        ws->tcnt, nullptr, 0, 0u, ws->bsA, ws->btile, ws->tmap, na);
@@ -787,6 +972,15 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
     cols = soa_of(bufA);
     bstart = ws->bstart;
   } else {
+    ANOMOD_HIP(ctx, hipGetLastError());
+    if (int rc = max_bucket(ctx, ws->bsA, 1ull << g.T, &mx)) return rc;
+    if (env_int("ANOMOD_BUCKET_DEBUG", 0))
+      std::fprintf(stderr, "bucket path: one level, T=%d, max bucket %llu\n", g.T,
+                   (unsigned long long)mx);
+    if (mx > (uint64_t)(kBigW * kBigPer)) {  // the caller retries with two levels
+      *escalate = true;
+      return ANOMOD_OK;
+    }
     hipLaunchKernelGGL((bk_scatter_kernel<true, false, false>), dim3((unsigned)g.tilesA),
                        dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
                        nullptr, 0, 0u, nullptr, nullptr, nullptr, 0);
@@ -795,8 +989,10 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
     bstart = ws->bsA;
   }
   ANOMOD_HIP(ctx, hipGetLastError());
+  const uint64_t nbk = 1ull << g.T;
 
-  // buckets
+  // buckets: <= 2048 spans in the small kernel, the rest listed for the
+  // large one (<= 8192 spans, or any size holding one trace)
   const int kshift = 64 - g.T - kSubBits;
   hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, cin, cols,
                      bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
@@ -821,6 +1017,10 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
   ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
                                  (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost, st));
   ANOMOD_HIP(ctx, hipStreamSynchronize(st));
+  if (env_int("ANOMOD_BUCKET_DEBUG", 0))
+    std::fprintf(stderr, "bucket path: T=%d DA=%d DB=%d max bucket %llu, %llu over 2048, %llu too big\n",
+                 g.T, g.DA, g.DB, (unsigned long long)mx, ws->h_misc[kMiscBigN],
+                 ws->h_misc[kMiscTooBig]);
   if (ws->h_misc[kMiscTooBig]) {
     *fallback = true;
     return ANOMOD_OK;
@@ -832,6 +1032,21 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
   res->bits = g.T;
   res->bucket = true;
   return ANOMOD_OK;
+}
+
+}  // namespace
+
+int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback) {
+  BucketGeom g = bucket_geom(in->n_spans);
+  bool escalate = false;
+  if (int rc = bucket_run_geom(ctx, in, g, res, fallback, &escalate)) return rc;
+  if (!escalate) return ANOMOD_OK;
+  // one level was not enough for the set's longest traces: two, the second
+  // with kDMax bits
+  g.DB = kDMax;
+  g.T = g.DA + g.DB;
+  g.tilesB = g.tilesA + (1ull << g.DA);
+  return bucket_run_geom(ctx, in, g, res, fallback, &escalate);
 }
 
 }  // namespace anomod

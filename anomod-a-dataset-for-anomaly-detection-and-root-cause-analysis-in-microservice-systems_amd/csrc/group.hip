@@ -619,10 +619,11 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ws->state_words = (cap + kTTile - 1) / kTTile;  // look-back words of the scans
   ws->list_cap = cap / 8 + 65536;
   // Bucket path: any geometry bucket_geom picks for n <= cap (digits of up
-  // to 11 bits per level, 2^T buckets with T at most that of a 64-span mean).
+  // to 11 bits per level, 2^T buckets with T at most that of a 64-span mean,
+  // or a level of 11 bits more).
   int tmax = 1;
   while (tmax < 22 && (cap >> tmax) > 64u) ++tmax;
-  ws->bucket_cap = 1ull << tmax;
+  ws->bucket_cap = 1ull << std::min(22, tmax + 11);  // + a retry with 11-bit level B
   ws->tile_cap = tiles + 2048;
   const size_t tcnt_words = std::max<size_t>(tiles * kDig, ws->tile_cap * 2048);
   const size_t bsum_words = (tiles / kTScanRows + 2) * 2048;

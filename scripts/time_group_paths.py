@@ -19,7 +19,8 @@ lg = int(sys.argv[1]) if len(sys.argv) > 1 else 25
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 avgs = sys.argv[3:] or ["1024"]
 with anomod.Context(0) as ctx:
-    dev = ctx.generate(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100), 1 << lg)
+    topo = os.environ.get("TG_TOPO", "SN")
+    dev = ctx.generate(anomod.SynthSpec(topo, seed=20251103, p_orphan_ppm=100), 1 << lg)
     want = ctx.edge_aggregate(dev, with_hist=False)
     inter = ctx.shuffle(dev, seed=5, window_traces=4096)
     n = dev.n_spans
@@ -39,5 +40,6 @@ with anomod.Context(0) as ctx:
             ok = all((getattr(t, k) == getattr(want, k)).all()
                      for k in ("count", "errors", "sum_us", "min_us", "max_us"))
             res.setdefault(key + "_equal", []).append(bool(ok))
+            res[key + "_info"] = ctx.group_info()
             print(json.dumps({key: res[key + "_group_ms"][-1], "equal": ok}), flush=True)
     print(json.dumps(res), flush=True)

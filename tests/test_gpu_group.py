@@ -208,15 +208,37 @@ def test_group_paths_agree(ctx, env_knob, path, avg):
     _assert_grouped_equal(g.download(), _oracle_grouped(flat))
 
 
-def test_group_bucket_overflow_falls_back(ctx):
+def test_group_bucket_overflow(ctx):
     """Traces of 1000-5000 spans overfill their buckets (small per-bucket
-    kernel: 1024 spans) and take the large kernel (8192 spans); a 12 000-span
-    trace fills a bucket beyond that, and the call regroups with the LSD
-    path.  Same grouping either way."""
+    kernel: 2048 spans) and take the large kernel (8192 spans); a bucket
+    beyond that makes the call retry with finer buckets, and one holding a
+    single 9 000- / 12 000- / 20 000-span trace is copied in arrival order.
+    Same grouping every way."""
     rng = np.random.default_rng(78)
     sp = _with_trace_hashes(_random_spanset(rng, 12, 20000, 16, dup=0.02), rng)
-    for lens in (rng.integers(1000, 5000, 6), np.r_[12000, rng.integers(1000, 5000, 3)]):
+    for lens in (rng.integers(1000, 5000, 6), np.r_[12000, rng.integers(1000, 5000, 3)],
+                 np.r_[20000, 9000]):
         big = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02, lens=lens), rng)
         flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "random")
         g = ctx.group(ctx.upload_ungrouped(flat))
         _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+        assert ctx.group_info()["path"] == "bucket"
+
+
+def test_group_huge_buckets(ctx):
+    """Traces whose keys share their top 40 bits stay in one bucket however
+    fine the split: three long ones (11 000 spans) are ranked by the huge-
+    bucket walk; 2100 four-span traces in one bucket (more distinct keys than
+    that walk holds) send the call to the LSD path.  Same grouping."""
+    rng = np.random.default_rng(79)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 5000, 16, dup=0.02), rng)
+    for lens, path in (([4000, 4000, 3000], "bucket"), ([4] * 2100, "lsd")):
+        base = rng.integers(0, 2**64, 1, dtype=np.uint64)[0] & np.uint64(0xFFFFFFFFFF000000)
+        low = rng.choice(2**24, len(lens), replace=False).astype(np.uint64)
+        keys = (base | low).astype(np.uint64)
+        big = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02, lens=lens), rng,
+                                 _unmix64(keys))
+        flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "random")
+        g = ctx.group(ctx.upload_ungrouped(flat))
+        _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+        assert ctx.group_info()["path"] == path
