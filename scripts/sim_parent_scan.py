@@ -5,7 +5,8 @@ scan's row-steps per chunk (a row waits for its slowest lane):
   fwd N      first-match forward scan from the trace start, N ids per step
   bidir F B  unique ids: F ids forward from the trace start + B ids backward
              from the span's own position per step
-usage: python scripts/sim_parent_scan.py [SN|TT|LONG] [n_traces]"""
+usage: python scripts/sim_parent_scan.py [SN|TT|LONG] [n_traces] [shuffled]
+(shuffled: the spans of every trace in a random order first)"""
 import sys
 from pathlib import Path
 
@@ -21,6 +22,10 @@ def main():
     nt = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
     sp = anomod.synth_generate_host(anomod.SynthSpec(topo, seed=20251103, p_orphan_ppm=100), nt)
     ptr = sp.trace_ptr.astype(np.int64)
+    if len(sys.argv) > 3 and sys.argv[3].startswith("shuf"):
+        rng = np.random.default_rng(1)
+        order = np.concatenate([a + rng.permutation(b - a) for a, b in zip(ptr[:-1], ptr[1:])])
+        sp = sp.take(order, sp.trace_ptr)
     chunks, t = [], 0
     while t < nt:
         a, k = ptr[t], 0
@@ -52,17 +57,65 @@ def main():
             return f
         return min(f, (i - 1 - par[i]) // nb + 1)
 
-    def cost(nf, nb):
+    def steps_meet(i, nf, nb):
+        """nf forward from the trace start + nb backward from i - 1 until the two
+        meet ([a, i) covered), then nf + nb forward (chunk.h find_parent_bidir)."""
+        if par[i] == -1:
+            return 0
+        a, b, q = ta[i], tb[i], par[i]
+        f, g, k = a, i - 1, 0
+        while True:
+            k += 1
+            if f <= g:
+                gb = max(a, g - nb + 1)
+                if f <= q < f + nf or gb <= q <= g:
+                    return k
+                f += nf
+                g -= nb
+            else:
+                if f <= q < f + nf + nb:
+                    return k
+                f += nf + nb
+            if f >= b:
+                return k
+
+    def steps_adj(i, nf, nb):
+        """unique ids: the span just before (one read) settles it, else nf forward
+        per step from the trace start"""
+        if par[i] == -1:
+            return 0
+        if par[i] == i - 1:
+            return 1
+        return steps(i, nf, 0) + 1
+
+    def steps_first(i, nf, nb):
+        """unique ids: one bidirectional step (nf forward from the trace start, nb
+        back from i - 1), then nf + nb forward per step"""
+        if par[i] == -1:
+            return 0
+        a, b, q = ta[i], tb[i], par[i]
+        if a <= q < a + nf or max(a, i - nb) <= q < i:
+            return 1
+        if q < 0:
+            return 1 + -(-(b - a - nf) // (nf + nb))
+        return 1 + (q - a - nf) // (nf + nb) + 1
+
+    def cost(nf, nb, fn=None):
+        fn = fn or steps
         tot = 0
         for t0, t1 in chunks:
             a, b = ptr[t0], ptr[t1]
             for r0 in range(a, b, 64):
-                tot += max(steps(i, nf, nb) for i in range(r0, min(r0 + 64, b)))
+                tot += max(fn(i, nf, nb) for i in range(r0, min(r0 + 64, b)))
         return tot / len(chunks)
 
     print(f"{topo}: {n / nt:.2f} spans/trace, {len(chunks)} chunks")
-    for nf, nb in ((10, 0), (16, 0), (6, 4), (8, 8)):
+    for nf, nb in ((10, 0), (6, 4), (8, 4), (10, 2), (8, 2)):
         print(f"  {'fwd' if nb == 0 else 'bidir'} {nf}+{nb}: {cost(nf, nb):.2f} row-steps/chunk")
+    for nf, nb in ((6, 4), (8, 2)):
+        print(f"  bidir-meet {nf}+{nb}: {cost(nf, nb, steps_meet):.2f} row-steps/chunk")
+    for nf, nb in ((6, 4), (8, 2), (4, 6)):
+        print(f"  first bidir {nf}+{nb}, then fwd: {cost(nf, nb, steps_first):.2f} row-steps/chunk")
 
 
 if __name__ == "__main__":
