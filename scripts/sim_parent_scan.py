@@ -110,12 +110,15 @@ def main():
         return tot / len(chunks)
 
     print(f"{topo}: {n / nt:.2f} spans/trace, {len(chunks)} chunks")
-    for nf, nb in ((10, 0), (6, 4), (8, 4), (10, 2), (8, 2)):
+    import os
+    splits = [tuple(int(x) for x in t.split("+")) for t in os.environ.get("SPLITS", "10+0 6+4").split()]
+    for nf, nb in splits:
         print(f"  {'fwd' if nb == 0 else 'bidir'} {nf}+{nb}: {cost(nf, nb):.2f} row-steps/chunk")
-    for nf, nb in ((6, 4), (8, 2)):
-        print(f"  bidir-meet {nf}+{nb}: {cost(nf, nb, steps_meet):.2f} row-steps/chunk")
-    for nf, nb in ((6, 4), (8, 2), (4, 6)):
-        print(f"  first bidir {nf}+{nb}, then fwd: {cost(nf, nb, steps_first):.2f} row-steps/chunk")
+    if os.environ.get("SIM_ALL"):
+        for nf, nb in ((6, 4), (8, 2)):
+            print(f"  bidir-meet {nf}+{nb}: {cost(nf, nb, steps_meet):.2f} row-steps/chunk")
+        for nf, nb in ((6, 4), (8, 2), (4, 6)):
+            print(f"  first bidir {nf}+{nb}, then fwd: {cost(nf, nb, steps_first):.2f} row-steps/chunk")
 
 
 if __name__ == "__main__":
