@@ -160,7 +160,7 @@ int coll_allgather(anomod_ctx* ctx, void* dbuf, size_t count_per_rank, CollType 
 // Trace cut points 0 = c_0 < ... < c_k = n_traces of a span set such that
 // every range [c_i, c_{i+1}) holds at most max_spans spans or is a single
 // trace (kernels with per-workgroup u32 counters launch once per range).
-// 2^31, or ANOMOD_MAX_LAUNCH_SPANS (tests: forces the multi-launch path).
+// 2^32 - 1, or ANOMOD_MAX_LAUNCH_SPANS (tests: forces the multi-launch path).
 uint64_t max_launch_spans();
 int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
                      std::vector<uint64_t>& cuts);

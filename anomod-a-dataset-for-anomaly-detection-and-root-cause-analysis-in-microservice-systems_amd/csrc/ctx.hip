@@ -207,9 +207,13 @@ int comm_agree(anomod_ctx* ctx, int local_rc) {
 }
 
 uint64_t max_launch_spans() {  // read per call: tests lower it at run time
+  // A workgroup's LDS counters are u32, so a launch covers < 2^32 spans (the
+  // dynamic tail may hand one workgroup any share of it).  r03: up from 2^31,
+  // so a 2^27-trace TrainTicket set (3.1e9 spans) is one launch, not two.
+  constexpr uint64_t kMax = (1ull << 32) - 1;
   const char* e = getenv("ANOMOD_MAX_LAUNCH_SPANS");
   const unsigned long long x = e ? strtoull(e, nullptr, 10) : 0ull;
-  return x > 0 && x < (1ull << 31) ? (uint64_t)x : (uint64_t)(1ull << 31);
+  return x > 0 && x < kMax ? (uint64_t)x : kMax;
 }
 
 int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
@@ -220,7 +224,7 @@ int span_launch_cuts(anomod_ctx* ctx, const anomod_spans* s, uint64_t max_spans,
     return ANOMOD_OK;
   }
   // Binary searches over the device trace_ptr, one u64 read back per probe
-  // (only sets of >= 2^31 spans get here).
+  // (only sets of >= 2^32 - 1 spans get here).
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   auto at = [&](uint64_t t, uint64_t* v) -> int {
     ANOMOD_HIP(ctx, hipMemcpy(v, s->trace_ptr + t, 8, hipMemcpyDeviceToHost));

@@ -1241,7 +1241,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     // A workgroup's LDS counters (histogram slots, errors) are u32 and the
     // dynamic tail may hand one workgroup any share of a launch, so a launch
     // covers < 2^32 spans: larger sets run as several launches over whole
-    // trace ranges (split on the device trace_ptr; one launch below 2^31).
+    // trace ranges (split on the device trace_ptr).
     std::vector<uint64_t> cuts;
     if (int rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts)) return rc;
     for (size_t k = 0; k + 1 < cuts.size(); ++k) {

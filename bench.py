@@ -466,7 +466,7 @@ def main() -> int:
     spans.free()
     if "tt_width" in legs:
         # --- TrainTicket width (BASELINE config 2 topology, 46 services:
-        # E = 2208 edges) at 2^27 traces (~3.1e9 spans, two launches)
+        # E = 2208 edges) at 2^27 traces (~3.1e9 spans, one launch)
         tt = ctx.generate(anomod.SynthSpec("TT", seed=args.seed, p_orphan_ppm=100),
                           args.traces_per_gpu, shard=rank)
         result["tt_width"] = edge_leg(ctx, tt, 3, "edge kernel on synthetic TrainTicket spans")

@@ -227,8 +227,8 @@ def test_large_synthetic_full_parity(ctx):
 
 @pytest.mark.parametrize("cap", [1000, 4096])
 def test_multi_launch_split_bit_exact(ctx, monkeypatch, cap):
-    """Span sets above the per-launch span bound (2^31: a workgroup's u32 LDS
-    counters must not wrap) run as several launches over whole trace ranges;
+    """Span sets above the per-launch span bound (2^32 - 1: a workgroup's u32
+    LDS counters must not wrap) run as several launches over whole trace ranges;
     ANOMOD_MAX_LAUNCH_SPANS lowers the bound so the split runs here: cuts
     inside runs of short traces, a trace longer than the bound alone, empty
     traces at the cuts."""
@@ -241,6 +241,22 @@ def test_multi_launch_split_bit_exact(ctx, monkeypatch, cap):
     assert_table_equal(ctx.edge_aggregate(sp), ref)
     monkeypatch.delenv("ANOMOD_MAX_LAUNCH_SPANS")
     assert_table_equal(ctx.edge_aggregate(sp), ref)
+
+
+@pytest.mark.slow
+def test_tt_full_size_one_launch_equals_two(ctx, monkeypatch):
+    """2^27 TrainTicket traces (3.1e9 spans: above 2^31, below 2^32): one
+    launch gives the same table as two launches cut at 2^31 spans."""
+    dev = ctx.generate(anomod.SynthSpec("TT", seed=20251103, p_orphan_ppm=100), 1 << 27)
+    assert (1 << 31) < dev.n_spans < (1 << 32) - 1
+    one = ctx.edge_aggregate(dev)
+    monkeypatch.setenv("ANOMOD_MAX_LAUNCH_SPANS", str(1 << 31))
+    two = ctx.edge_aggregate(dev)
+    monkeypatch.delenv("ANOMOD_MAX_LAUNCH_SPANS")
+    dev.free()
+    for k in FIELDS + ("hist", "p50_us", "p99_us"):
+        np.testing.assert_array_equal(getattr(one, k), getattr(two, k), err_msg=k)
+    assert int(one.count.sum()) > (1 << 31)
 
 
 @pytest.mark.parametrize("S,n_traces,max_len", [(12, 20000, 24), (46, 4000, 60), (3, 1, 3000)])
