@@ -126,8 +126,10 @@ struct Table {
   unsigned long long* ctr;   // trace-segment counter of the dynamic tail (zeroed per launch)
   uint32_t kb;               // key bits of a histogram slot (count in the 32 - kb above)
   unsigned long long* keys;  // kHtKeys: [n_spans] edge << 32 | dur, by span position
-  unsigned long long* big;       // long traces: [0] listed, [1] ticket of edge_big_kernel
+  unsigned long long* big;       // long traces: [0] listed, [1] / [2] tickets of the
+                                 // resolve / record kernels
   unsigned long long* big_list;  // long traces: trace indices
+  uint16_t* bpar;            // long traces: every listed span's parent row (S root, S + 1 orphan)
   uint64_t t_base;           // trace index of this launch's first trace
   unsigned long long* ovf;   // spans whose pair-form probe chain was full (counted in HBM)
 };
@@ -588,6 +590,14 @@ constexpr int kBigThreads = kThreads;  // the tables' init / flush loops assume 
 #ifndef ANOMOD_BIG_MIN
 #define ANOMOD_BIG_MIN 256
 #endif
+// resolve kernel: minimum waves per SIMD the compiler must fit (registers)
+#ifndef ANOMOD_RES_MINB
+#define ANOMOD_RES_MINB 2
+#endif
+// 1 = the r02 single-kernel long-trace pass (experiment builds, A/B)
+#ifndef ANOMOD_BIG_ONEPASS
+#define ANOMOD_BIG_ONEPASS 0
+#endif
 // traces longer than this take the long-trace pass (<= kStage)
 constexpr uint32_t kBigMin = ANOMOD_BIG_MIN;
 constexpr uint32_t kBigWin = 2048;    // ids per table window
@@ -879,6 +889,326 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
   tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
+// ---- long-trace pass, r03: resolve, then record ----------------------------
+// The pass above holds the histogram / stats tables AND the id table in one
+// workgroup's LDS, so a CU runs one workgroup and every batch's column loads,
+// inserts, lookups and records follow each other with nothing to hide their
+// latency (LONG at 2^23 traces: 3.74 ms for 1.3e8 listed spans).  Split:
+// edge_big_resolve_kernel keeps only the id table (48 KiB: three 512-thread
+// workgroups per CU) and writes every listed span's parent row — or, in the
+// exact-quantile mode, its key — and edge_big_record_kernel streams the
+// listed spans (16 traces per ticket, one load round trip per ticket) into
+// the chunk walk's tables.  Same first-match rule, same table forms.
+constexpr int kResThreads = 512;
+constexpr uint32_t kResWin = 2048;                 // ids per table window
+constexpr uint32_t kResSlots = 4096;               // load <= 1/2
+constexpr int kResPer = (int)kResWin / kResThreads;  // spans per thread in a packed window
+static_assert(kResWin % kResThreads == 0 && kResWin <= 65536, "window: whole rows, pos << 16 | svc");
+
+__device__ __forceinline__ void res_out(const Table& tab, uint64_t g, uint32_t p, uint32_t sf,
+                                        uint32_t dr, uint32_t S) {
+  if (tab.keys)
+    tab.keys[g] = ((unsigned long long)(p * S + (sf & 0xFFFFu)) << 32) | dr;
+  else
+    tab.bpar[g] = (uint16_t)p;
+}
+
+// One trace longer than a window: blocks of kResThreads * kBigPer spans,
+// each looked up against the trace's id windows in order.
+__device__ void res_one(unsigned long long* bkey, uint32_t* bval,
+                        const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+                        const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+                        uint64_t lo, uint64_t L, uint32_t S, const Table& tab) {
+  const int tid = threadIdx.x;
+  for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kResThreads * kBigPer) {
+    uint64_t pid[kBigPer];
+    uint32_t psv[kBigPer];  // ~0: not found yet
+    bool need = false;
+#pragma unroll
+    for (int r = 0; r < kBigPer; ++r) {
+      const uint64_t i = b0 + (uint64_t)r * kResThreads + tid;
+      pid[r] = i < L ? parent[lo + i] : 0ull;
+      psv[r] = 0xFFFFFFFFu;
+      need |= pid[r] != 0ull;
+    }
+    for (uint64_t w0 = 0; w0 < L; w0 += kResWin) {
+      if (!__syncthreads_or(need)) break;  // also orders the previous clear
+#pragma unroll
+      for (int u = 0; u < kResPer; ++u) {
+        const uint32_t k = (uint32_t)(u * kResThreads + tid);
+        const uint64_t id = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
+        if (id == 0ull) continue;
+        const uint32_t sv = svcfl[lo + w0 + k] & 0xFFFFu;
+        for (uint32_t sl = big_slot(id);; sl = (sl + 1u) & (kResSlots - 1u)) {
+          const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id);
+          if (prev == 0ull || prev == id) {
+            atomicMin(&bval[sl], (k << 16) | sv);  // the first position wins, with its service
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      need = false;
+#pragma unroll
+      for (int r = 0; r < kBigPer; ++r) {
+        if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
+        for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kResSlots - 1u)) {
+          const unsigned long long key = bkey[sl];
+          if (key == pid[r]) {
+            psv[r] = bval[sl] & 0xFFFFu;
+            break;
+          }
+          if (key == 0ull) break;
+        }
+        need |= psv[r] == 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      for (uint32_t k = tid; k < kResSlots; k += kResThreads) {
+        bkey[k] = 0ull;
+        bval[k] = 0xFFFFFFFFu;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kBigPer; ++r) {
+      const uint64_t i = b0 + (uint64_t)r * kResThreads + tid;
+      if (i >= L) continue;
+      const uint32_t p = pid[r] == 0ull ? S : psv[r] == 0xFFFFFFFFu ? S + 1u : psv[r];
+      res_out(tab, lo + i, p, tab.keys ? svcfl[lo + i] : 0u, tab.keys ? dur[lo + i] : 0u, S);
+    }
+  }
+  __syncthreads();  // the last window's clear before the next user of the table
+}
+
+// Up to kGroup traces (bm) packed into one window, each in a private table
+// region [2 off_i, 2 off_i + 2 L_i), as big_batch.
+__device__ void res_batch(unsigned long long* bkey, uint32_t* bval,
+                          const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+                          const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+                          const uint64_t (&lo)[kGroup], const uint64_t (&L)[kGroup], uint32_t bm,
+                          uint32_t S, const Table& tab) {
+  const int tid = threadIdx.x;
+  uint32_t off[kGroup + 1];
+  off[0] = 0;
+#pragma unroll
+  for (int i = 0; i < kGroup; ++i) off[i + 1] = off[i] + (((bm >> i) & 1u) ? (uint32_t)L[i] : 0u);
+  const uint32_t tot = off[kGroup];
+  uint64_t id[kResPer], pid[kResPer], g[kResPer];
+  uint32_t sv[kResPer], rb[kResPer], rs[kResPer], pos[kResPer];
+  bool v[kResPer];
+#pragma unroll
+  for (int u = 0; u < kResPer; ++u) {
+    const uint32_t q = (uint32_t)(u * kResThreads + tid);
+    v[u] = q < tot;
+    uint32_t a0 = 0, a1 = off[1];
+    uint64_t tl = lo[0];
+#pragma unroll
+    for (int i = 1; i < kGroup; ++i)
+      if (q >= off[i] && ((bm >> i) & 1u)) {
+        a0 = off[i];
+        a1 = off[i + 1];
+        tl = lo[i];
+      }
+    pos[u] = q - a0;
+    rb[u] = 2u * a0;
+    rs[u] = 2u * (a1 - a0);
+    g[u] = tl + pos[u];
+    id[u] = v[u] ? span_id[g[u]] : 0ull;
+    pid[u] = v[u] ? parent[g[u]] : 0ull;
+    sv[u] = v[u] ? svcfl[g[u]] & 0xFFFFu : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kResPer; ++u) {
+    if (!v[u] || id[u] == 0ull) continue;
+    uint32_t r = big_region_slot(id[u], rs[u]);
+    while (true) {
+      const uint32_t sl = rb[u] + r;
+      const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id[u]);
+      if (prev == 0ull || prev == id[u]) {
+        atomicMin(&bval[sl], (pos[u] << 16) | sv[u]);  // the first position wins
+        break;
+      }
+      r = r + 1u == rs[u] ? 0u : r + 1u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kResPer; ++u) {
+    if (!v[u]) continue;
+    uint32_t psv = 0xFFFFFFFFu;
+    if (pid[u] != 0ull) {
+      uint32_t r = big_region_slot(pid[u], rs[u]);
+      for (uint32_t probe = 0; probe < rs[u]; ++probe) {
+        const unsigned long long key = bkey[rb[u] + r];
+        if (key == pid[u]) {
+          psv = bval[rb[u] + r] & 0xFFFFu;
+          break;
+        }
+        if (key == 0ull) break;
+        r = r + 1u == rs[u] ? 0u : r + 1u;
+      }
+    }
+    const uint32_t p = pid[u] == 0ull ? S : psv == 0xFFFFFFFFu ? S + 1u : psv;
+    res_out(tab, g[u], p, tab.keys ? svcfl[g[u]] : 0u, tab.keys ? dur[g[u]] : 0u, S);
+  }
+  __syncthreads();  // every lookup done before the clear
+  for (uint32_t k = tid; k < 2u * tot; k += kResThreads) {
+    bkey[k] = 0ull;
+    bval[k] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kResThreads, ANOMOD_RES_MINB) void edge_big_resolve_kernel(
+    const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
+    const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+    const uint64_t* __restrict__ trace_ptr, uint32_t S, Table tab) {
+  __shared__ unsigned long long bkey[kResSlots];  // 0 = empty (id 0 is never a parent ref)
+  __shared__ uint32_t bval[kResSlots];            // (first position) << 16 | svc
+  __shared__ unsigned long long s_g[kGroup][2];
+  const int tid = threadIdx.x;
+  const uint64_t nbig = tab.big[0];
+  if (nbig == 0) return;
+  for (uint32_t k = tid; k < kResSlots; k += kResThreads) {
+    bkey[k] = 0ull;
+    bval[k] = 0xFFFFFFFFu;
+  }
+  unsigned long long nlo = 0, nL = 0;
+  auto fetch = [&]() {
+    unsigned long long j = 0;
+    if (tid == 0) j = atomicAdd(&tab.big[1], (unsigned long long)kGroup);
+    j = __shfl(j, 0);
+    nlo = nL = 0;
+    if (tid < kGroup && j + tid < nbig) {
+      const uint64_t t = tab.big_list[j + tid];
+      nlo = trace_ptr[t];
+      nL = trace_ptr[t + 1] - nlo;
+    }
+  };
+  if (tid < kWave) fetch();
+  while (true) {
+    __syncthreads();
+    if (tid < kGroup) {
+      s_g[tid][0] = nlo;
+      s_g[tid][1] = nL;
+    }
+    __syncthreads();
+    uint64_t glo[kGroup], gL[kGroup];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+      glo[k] = s_g[k][0];
+      gL[k] = s_g[k][1];
+      any |= gL[k] != 0;
+    }
+    if (!any) break;
+    if (tid < kWave) fetch();
+    uint32_t left = 0;
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) left |= (gL[q] != 0 ? 1u : 0u) << q;
+    while (left) {
+      const int k = __ffs(left) - 1;
+      uint64_t lk = 0, Lk = 0;
+#pragma unroll
+      for (int q = 0; q < kGroup; ++q)
+        if (q == k) {
+          lk = glo[q];
+          Lk = gL[q];
+        }
+      if (Lk > kResWin) {
+        res_one(bkey, bval, span_id, parent, svcfl, dur, lk, Lk, S, tab);
+        left &= ~(1u << k);
+        continue;
+      }
+      uint32_t bm = 0;
+      uint64_t tot = 0;
+#pragma unroll
+      for (int q = 0; q < kGroup; ++q) {
+        const bool chain = q == k || (q > 0 && ((bm >> (q - 1)) & 1u));
+        if (q >= k && chain && ((left >> q) & 1u) && gL[q] <= kResWin && tot + gL[q] <= kResWin) {
+          bm |= 1u << q;
+          tot += gL[q];
+        }
+      }
+      res_batch(bkey, bval, span_id, parent, svcfl, dur, glo, gL, bm, S, tab);
+      left &= ~bm;
+    }
+  }
+}
+
+// The listed spans into the tables, kRecGroup traces per ticket (wave 0 keeps
+// the next ticket's entries and bounds in flight).
+constexpr int kRecGroup = 16;
+constexpr int kRecPer = 4;
+template <int HT, int ST>
+__global__ __launch_bounds__(kBigThreads) void edge_big_record_kernel(
+    const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
+    const uint64_t* __restrict__ trace_ptr, uint32_t S, uint32_t E, Table tab) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kOffWave];
+  __shared__ unsigned long long s_lo[kRecGroup];
+  __shared__ uint32_t s_off[kRecGroup + 1];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint64_t nbig = tab.big[0];
+  if (nbig == 0) return;
+  tables_init<HT, ST>(smem, E, tid);
+  unsigned long long nlo = 0;
+  uint32_t nL = 0;
+  auto fetch = [&]() {
+    unsigned long long j = 0;
+    if (lane == 0) j = atomicAdd(&tab.big[2], (unsigned long long)kRecGroup);
+    j = __shfl(j, 0);
+    nlo = 0;
+    nL = 0;
+    if (lane < kRecGroup && j + lane < nbig) {
+      const uint64_t t = tab.big_list[j + lane];
+      nlo = trace_ptr[t];
+      nL = (uint32_t)(trace_ptr[t + 1] - nlo);
+    }
+  };
+  if (tid < kWave) fetch();
+  while (true) {
+    __syncthreads();  // the previous ticket is done with s_lo / s_off
+    if (tid < kWave) {
+      uint32_t inc = nL;  // inclusive scan over the ticket's traces
+#pragma unroll
+      for (int o = 1; o < kRecGroup; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (lane < kRecGroup) {
+        s_lo[lane] = nlo;
+        s_off[lane + 1] = inc;
+      }
+      if (lane == 0) s_off[0] = 0;
+      fetch();  // the next ticket, overlapping this one's work
+    }
+    __syncthreads();
+    const uint32_t tot = s_off[kRecGroup];
+    if (tot == 0) break;  // tickets exhausted (listed traces are never empty)
+    // kRecPer spans per thread loaded together, then recorded (the records'
+    // LDS / HBM atomics would otherwise keep the next loads behind them)
+    for (uint32_t q0 = tid; q0 < tot; q0 += kRecPer * kBigThreads) {
+      uint32_t sf[kRecPer], dr[kRecPer], pr[kRecPer];
+#pragma unroll
+      for (int j = 0; j < kRecPer; ++j) {
+        const uint32_t q = q0 + (uint32_t)j * kBigThreads;
+        int t = 0;
+#pragma unroll
+        for (int i = 1; i < kRecGroup; ++i) t = q >= s_off[i] ? i : t;
+        const uint64_t g = s_lo[t] + (q - s_off[t]);
+        const bool v = q < tot;
+        sf[j] = v ? svcfl[g] : 0u;
+        dr[j] = v ? dur[g] : 0u;
+        pr[j] = v ? tab.bpar[g] : 0xFFFFu;
+      }
+#pragma unroll
+      for (int j = 0; j < kRecPer; ++j)
+        if (pr[j] != 0xFFFFu) record<HT, ST>(smem, pr[j] * S + (sf[j] & 0xFFFFu), dr[j], sf[j] >> 16, tab);
+    }
+  }
+  __syncthreads();
+  tables_flush<HT, ST>(smem, E, tab, tid);
+}
+
 template <int HT, int ST, bool UNI>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
@@ -1109,28 +1439,31 @@ Pick pick_kernel(uint32_t E, bool compact, bool uni) {
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
 // all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
-// ctr (u64) | big counters (u64 x 2) | pair-table overflows (u64; all
+// ctr (u64) | big counters (u64 x 3) | pair-table overflows (u64; all
 // zeroed with them) | count | p50 |
-// p99 | mn | long-trace list.  [off_err, end_small) is copied to the host in
+// p99 | mn | long-trace list | long-trace parent rows (u16 per span).  [off_err, end_small) is copied to the host in
 // one D2H.
 struct Layout {
   uint64_t E;
   size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_ovf, off_count, off_p50,
       off_p99, off_mn, end_small, bytes;
-  Layout(uint64_t e, uint64_t big_cap) : E(e) {
+  size_t off_bpar = 0;
+  Layout(uint64_t e, uint64_t big_cap, uint64_t n_spans = 0) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
     off_sum = off_err + E * 8;
     off_mx = off_sum + E * 8;
     off_ctr = (off_mx + E * 4 + 7) & ~size_t(7);
     off_big = off_ctr + 8;
-    off_ovf = off_big + 16;
+    off_ovf = off_big + 24;
     off_count = off_ovf + 8;
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
     end_small = off_mn + E * 4;
     bytes = ((end_small + 7) & ~size_t(7)) + big_cap * 8;
+    off_bpar = bytes;                           // u16 parent rows, by span position
+    if (big_cap) bytes += (n_spans * 2 + 7) & ~size_t(7);
   }
   size_t off_list() const { return (end_small + 7) & ~size_t(7); }
 };
@@ -1148,9 +1481,23 @@ uint64_t big_capacity(const anomod_spans* s) {
 template <int HT, int ST>
 hipError_t launch_big(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S, uint32_t E,
                       const Table& tab) {
-  hipLaunchKernelGGL((edge_big_kernel<HT, ST>), dim3((unsigned)ctx->num_cus), dim3(kBigThreads),
-                     0, ctx->stream, spans->span_id, spans->parent_span_id, spans->svc_flags,
-                     spans->dur_us, spans->trace_ptr, S, E, tab);
+  if (ANOMOD_BIG_ONEPASS) {  // the r02 single-kernel pass (A/B)
+    hipLaunchKernelGGL((edge_big_kernel<HT, ST>), dim3((unsigned)ctx->num_cus), dim3(kBigThreads),
+                       0, ctx->stream, spans->span_id, spans->parent_span_id, spans->svc_flags,
+                       spans->dur_us, spans->trace_ptr, S, E, tab);
+    return hipGetLastError();
+  }
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void*>(edge_big_resolve_kernel), kResThreads, 0);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(edge_big_resolve_kernel, dim3((unsigned)(ctx->num_cus * std::max(per_cu, 1))),
+                     dim3(kResThreads), 0, ctx->stream, spans->span_id, spans->parent_span_id,
+                     spans->svc_flags, spans->dur_us, spans->trace_ptr, S, tab);
+  if ((e = hipGetLastError()) != hipSuccess || HT == kHtKeys) return e;
+  hipLaunchKernelGGL((edge_big_record_kernel<HT, ST>), dim3((unsigned)ctx->num_cus),
+                     dim3(kBigThreads), 0, ctx->stream, spans->svc_flags, spans->dur_us,
+                     spans->trace_ptr, S, E, tab);
   return hipGetLastError();
 }
 
@@ -1200,13 +1547,13 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
                      "span service index %u >= n_services %u", spans->max_svc, S);
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
   const uint64_t big_cap = big_capacity(spans);
-  const Layout L(E, big_cap);
+  const Layout L(E, big_cap, spans->n_spans);
   if (local == ANOMOD_OK) local = bind(ctx);
   if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
   if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.end_small - L.off_err);
   if (int rc = comm_agree(ctx, local)) return rc;
   char* base = static_cast<char*>(ctx->d_table);
-  Table tab;
+  Table tab{};  // keys = nullptr: the table forms, not the exact-quantile keys
   tab.hist = reinterpret_cast<unsigned long long*>(base + L.off_hist);
   tab.err = reinterpret_cast<unsigned long long*>(base + L.off_err);
   tab.sum = reinterpret_cast<unsigned long long*>(base + L.off_sum);
@@ -1215,6 +1562,7 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
   tab.big = reinterpret_cast<unsigned long long*>(base + L.off_big);
   tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
+  tab.bpar = reinterpret_cast<uint16_t*>(base + L.off_bpar);
   tab.ovf = reinterpret_cast<unsigned long long*>(base + L.off_ovf);
   tab.kb = 1;
   while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
@@ -1363,7 +1711,7 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
     const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
     std::vector<uint64_t> cuts;
     if (e == hipSuccess) rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts);
-    if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 24, ctx->stream);  // ctr + big counters
+    if (e == hipSuccess) e = hipMemsetAsync(d_ctr, 0, 32, ctx->stream);  // ctr + big counters
     for (size_t k = 0; e == hipSuccess && rc == ANOMOD_OK && k + 1 < cuts.size(); ++k) {
       if (k > 0) e = hipMemsetAsync(d_ctr, 0, 8, ctx->stream);
       if (e != hipSuccess) break;
