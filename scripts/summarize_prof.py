@@ -137,7 +137,7 @@ def main() -> int:
         rows = []
         with open(trace) as f:
             for r in csv.DictReader(f):
-                if "edge_agg_kernel<1, 1>" in r["Kernel_Name"]:
+                if "edge_agg_kernel<1, 1" in r["Kernel_Name"]:  # <1, 1> or <1, 1, UNI>
                     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
         rows.sort()
         k = bench["warmup"] + bench["steps"]
