@@ -7,7 +7,7 @@
 // fewer bytes moved: 2 record scatters + 1 coalesced record pass instead of
 // ceil(log2(n)/8) scatters + bucket fix-up + trace_ptr scan.
 //
-// Per span (n = 1.15e9: T = 20, DA = DB = 10):
+// Per span (n = 1.15e9: T = 20, DA = 9, DB = 11):
 //   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 2 (next digit out)
 //   level B: 2 (count: digits) + 32 + 32
 //   buckets: 32 (records in) + 32 (SoA columns out) + 8/trace (trace_ptr, two moves)
@@ -31,7 +31,8 @@ using chunk::wave_sync;
 // Experiment-only builds (never set in the shipped library):
 //  1 = level B counts its digits from the level-A records (no 2-B digit array);
 //  2 = level A stores nothing, then the LSD path groups (timing of level A's
-//      loads and ranking only).
+//      loads and ranking only);
+//  4 = nontemporal record stores in the scatter levels.
 
 
 #ifndef ANOMOD_BK_ABL
@@ -380,7 +381,12 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
       const uint64_t k = mix64(((uint64_t)x0.y << 32) | x0.x);
       const uint32_t dd = (uint32_t)(k >> shift) & (uint32_t)(nd - 1);
       const uint64_t g = (uint64_t)gbase[dd] + (p - tstart[dd]);
-      reinterpret_cast<uint4*>(aout)[2 * g + (c & 1u)] = x;
+      if constexpr ((ANOMOD_BK_ABL & 4) != 0) {
+        using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4{x.x, x.y, x.z, x.w},
+                                    reinterpret_cast<u32x4*>(aout) + 2 * g + (c & 1u));
+      } else
+        reinterpret_cast<uint4*>(aout)[2 * g + (c & 1u)] = x;
       if constexpr (DNEXT)
         if (!(c & 1u)) dnext[g] = (uint16_t)((k >> nshift) & nmask);
     }
@@ -867,7 +873,16 @@ BucketGeom bucket_geom(uint64_t n) {
     g.DA = g.T;
     g.DB = 0;
   } else {
-    g.DA = (g.T + 1) / 2;
+    // Level A's writes cost more with more digits (1 KiB wave stores cover
+    // shorter runs), level B's less (its writes stay inside one level-A bucket,
+    // and smaller buckets stay in the Infinity Cache): level A takes at most 9
+    // bits.  (2^27 SN traces, T = 20: A + B 25.5 + 25.1 ms at 9 + 11 bits,
+    // 30.4 + 23.8 at 10 + 10, 32.8 + 21.3 at 11 + 9; 2^25, T = 18: 9 + 9 best,
+    // 16.0 vs 16.4 / 17.8 ms grouping at 8 + 10 / 7 + 11.)
+    g.DA = std::max(g.T - kDMax, std::min((g.T + 1) / 2, 9));
+    // experiment knob: level A's share of the bits (the rest, <= kDMax, to level B)
+    const int da = env_int("ANOMOD_BUCKET_DA", 0);
+    if (da > 0) g.DA = std::min(std::max(da, g.T - kDMax), kDMax);
     g.DB = g.T - g.DA;
   }
   g.tilesA = n ? (n + kBTile - 1) / kBTile : 1;
