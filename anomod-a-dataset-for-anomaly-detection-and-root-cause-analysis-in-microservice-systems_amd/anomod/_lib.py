@@ -154,6 +154,7 @@ _SIGS = {
     "anomod_spans_free": (_i32, [_vp]),
     "anomod_spans_set_unique_ids": (_i32, [_vp, C.c_int]),
     "anomod_spans_unique_ids": (_i32, [_vp, _P(C.c_int)]),
+    "anomod_spans_scan_order": (_i32, [_vp, _P(C.c_int)]),
     "anomod_spans_hist_compact": (_i32, [_vp, _P(C.c_int)]),
     "anomod_spans_upload_ungrouped": (_i32, [_vp, _P(SpanSoA), _u64, _P(_vp)]),
     "anomod_spans_grouped": (_i32, [_vp, _P(_i32)]),

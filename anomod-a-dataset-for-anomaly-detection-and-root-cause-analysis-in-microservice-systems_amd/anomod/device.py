@@ -104,6 +104,13 @@ class DeviceSpans:
         return bool(u.value)
 
     @property
+    def scan_order(self) -> int:
+        """1 collector order / 0 shuffled inside traces / -1 not probed yet."""
+        o = C.c_int()
+        L.check(L.lib().anomod_spans_scan_order(self.handle, C.byref(o)))
+        return o.value
+
+    @property
     def hist_compact(self) -> bool:
         """True once an aggregation overflowed the pair-form LDS histogram
         (later ones use the compact form)."""

@@ -79,6 +79,11 @@ struct anomod_spans {
   // decoded / uploaded sets).  Lets the parent lookups scan from both ends
   // (any match is the first match).  false = unknown: forward scan only.
   bool unique_ids = false;
+  // Parent-scan order hint for unique-id sets: 1 = collector order (most
+  // child spans right after their parent: the bidirectional scan), 0 = not
+  // (spans shuffled inside their traces: the forward scan), -1 = unknown —
+  // probed on the device at the first aggregation (edge_agg.hip probe_order).
+  mutable int8_t order = -1;
   bool grouped = true;       // false: spans in arrival order, trace_ptr = NULL
                              // (anomod_spans_upload_ungrouped; group first)
   uint64_t* trace_hash = nullptr;

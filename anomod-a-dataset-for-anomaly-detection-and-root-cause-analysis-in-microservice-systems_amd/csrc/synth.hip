@@ -607,6 +607,7 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
   }
   s->max_svc = (uint32_t)h->services.size() - 1u;
   s->unique_ids = true;  // synth_span_id is injective in the span index
+  s->order = 1;          // the generator emits a callee's spans after its caller's
   s->max_trace_len = 0;
   for (size_t k = 0; k + 1 < h->tmpl_off.size(); ++k)
     s->max_trace_len = std::max<uint64_t>(s->max_trace_len, h->tmpl_off[k + 1] - h->tmpl_off[k]);
@@ -623,6 +624,12 @@ int anomod_spans_set_unique_ids(anomod_spans* spans, int unique) {
 int anomod_spans_hist_compact(const anomod_spans* spans, int* compact) {
   ANOMOD_REQUIRE(nullptr, spans && compact, "anomod_spans_hist_compact: NULL argument");
   *compact = spans->hist_compact ? 1 : 0;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_scan_order(const anomod_spans* spans, int* order) {
+  ANOMOD_REQUIRE(nullptr, spans && order, "anomod_spans_scan_order: NULL argument");
+  *order = spans->order;
   return ANOMOD_OK;
 }
 

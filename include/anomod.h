@@ -136,6 +136,13 @@ int anomod_hist_bin_bounds(uint32_t bin, uint32_t* lo, uint32_t* hi);
  * (unknown: the first-match scan).  Grouping and shuffling keep it.         */
 int anomod_spans_set_unique_ids(anomod_spans* spans, int unique);
 int anomod_spans_unique_ids(const anomod_spans* spans, int* unique);
+/* Order hint of a unique-id set (a performance hint the library keeps):
+ * 1 = collector order, most child spans right after their parent (the
+ * bidirectional scan from the trace start and from the span pays off);
+ * 0 = not (e.g. spans shuffled inside their traces: the forward scan);
+ * -1 = not known yet — the first aggregation probes the set's first 2^20
+ * spans on the device.  Generated sets are 1; results never depend on it.   */
+int anomod_spans_scan_order(const anomod_spans* spans, int* order);
 /* 1 once an aggregation of this set overflowed the workgroups' 8 Ki-slot
  * (pair-form) LDS histogram: its later aggregations use the 16 Ki packed-slot
  * (compact) form (same results; a performance hint the library keeps).     */

@@ -323,17 +323,35 @@ def test_unique_id_bidirectional_scan(ctx, monkeypatch, S, max_len):
     assert sp.check_unique_ids()
     ref = native.edge_aggregate(sp)
     dev = ctx.upload(sp)
-    assert dev.unique_ids
-    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    assert dev.unique_ids and dev.scan_order == -1
     shuf = ctx.shuffle(dev, seed=5, window_traces=0)  # parents anywhere in the trace
     assert shuf.unique_ids
     host = shuf.download()
     ref2 = native.edge_aggregate(host)
-    assert_table_equal(ctx.edge_aggregate(shuf), ref2)
-    monkeypatch.setenv("ANOMOD_UNIQUE_SCAN", "0")
-    assert_table_equal(ctx.edge_aggregate(shuf), ref2)
+    # the bidirectional scan forced (=1), the set's own choice, the forward scan
+    for scan in ("1", None, "0"):
+        if scan is None:
+            monkeypatch.delenv("ANOMOD_UNIQUE_SCAN", raising=False)
+        else:
+            monkeypatch.setenv("ANOMOD_UNIQUE_SCAN", scan)
+        assert_table_equal(ctx.edge_aggregate(dev), ref)
+        assert_table_equal(ctx.edge_aggregate(shuf), ref2)
+    assert shuf.scan_order == 0  # probed: shuffled inside the traces
     shuf.free()
     dev.free()
+
+
+def test_scan_order_probe(ctx):
+    """Generated sets are declared in collector order; shuffling inside the
+    traces makes the probe pick the forward scan; the table is the same."""
+    gen = ctx.generate(anomod.SynthSpec("TT", seed=9), 20000)
+    assert gen.scan_order == 1
+    shuf = ctx.shuffle(gen, seed=3, window_traces=0)
+    assert shuf.scan_order == -1
+    t1, t2 = ctx.edge_aggregate(gen), ctx.edge_aggregate(shuf)
+    assert shuf.scan_order == 0
+    for k in FIELDS + ("hist",):
+        np.testing.assert_array_equal(getattr(t1, k), getattr(t2, k), err_msg=k)
 
 
 def test_duplicate_ids_are_not_declared_unique(ctx):
