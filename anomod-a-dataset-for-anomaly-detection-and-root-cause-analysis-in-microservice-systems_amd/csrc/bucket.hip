@@ -1,22 +1,25 @@
 // Trace grouping, bucket path: two stable MSD scatter levels over the top T
-// bits of k = mix64(trace_hash), then one workgroup per bucket of ~512 spans
+// bits of k = mix64(trace_hash), then one workgroup per bucket of ~1000 spans
 // that puts the bucket in (k, arrival) order inside LDS and writes the grouped
 // SoA columns and its trace starts.  Same output as the LSD path of group.hip
 // (traces by k ascending, spans of a trace in arrival order — the order the
 // reference's first-match parent rule sees, trace_collector.py:424-443), with
-// fewer bytes moved: 2 record scatters + 1 coalesced record pass instead of
+// fewer bytes moved: 2 record scatters + 1 record pass instead of
 // ceil(log2(n)/8) scatters + bucket fix-up + trace_ptr scan.
 //
 // Per span (n = 1.15e9: T = 20, DA = 9, DB = 11):
-//   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 2 (next digit out)
+//   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 2 (next digits out)
 //   level B: 2 (count: digits) + 32 + 32
-//   buckets: 32 (records in) + 32 (SoA columns out) + 8/trace (trace_ptr, two moves)
-// = 172 B/span + tile counts (~2 B/span) against 286 B/span for the LSD path.
+//   buckets: 32 (records in) + 32 (SoA columns out) + 24/trace (trace starts, trace_ptr)
+// + tile counts (4 B per tile and digit, five touches: ~15 B/span) ≈ 220 B/span,
+// against 286 B/span for the LSD path.
 //
 // A bucket larger than the small kernel's 2048 spans (a long trace, or the
-// tail of the size distribution) goes to a list that a 1024-thread kernel of
-// 8192-span capacity works through; a bucket beyond that (a single trace of
-// thousands of spans near others) makes the caller regroup with the LSD path.
+// tail of the size distribution) goes to a list that a 1024-thread kernel
+// works through: up to 8192 spans with its keys in LDS, beyond that by a
+// one-wave walk over the bucket's distinct keys (bucket_huge).  Only a huge
+// bucket with more distinct keys than that walk holds (adversarial hashes)
+// makes the caller regroup with the LSD path.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
