@@ -262,12 +262,25 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
 // 16-B store per lane and record half 9.2 / 6.0 ms for levels A / B; whole
 // records 6.0 / 5.4; no stores at all 1.0 ms — the scattered writes are the
 // cost.)
+//
+// Workgroups are dispatched to the 8 XCDs round-robin by block index, so
+// consecutive blocks would write the two ends of a shared 128-B line from two
+// different L2s.  With nx = 8, XCD x takes a contiguous eighth of the tiles
+// instead: the tiles one XCD has in flight are neighbours, their runs of one
+// digit are neighbours in the output, and their partial lines meet in that
+// XCD's L2 before write-back.
+__device__ inline uint64_t xcd_tile(uint64_t b, uint64_t g, uint32_t nx) {
+  if (nx <= 1u) return b;
+  const uint64_t x = b % nx, s = b / nx, q = g / nx, r = g % nx;
+  return x * q + (x < r ? x : r) + s;
+}
+
 template <bool SOA_IN, bool SEG, bool DNEXT>
 __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
     int dbits, const uint32_t* __restrict__ toff, uint16_t* __restrict__ dnext, int nshift,
     uint32_t nmask, const uint32_t* __restrict__ bsA, const uint32_t* __restrict__ btile,
-    const uint32_t* __restrict__ tmap, int na) {
+    const uint32_t* __restrict__ tmap, int na, uint32_t nx) {
   constexpr bool kNoStore = (ANOMOD_BK_ABL & 2) != 0 && SOA_IN;
   static_assert(kBWaves * kNDMax * 2 <= kBTile * 32, "counters fit under the stage");
   union Lds {
@@ -280,7 +293,7 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
   __shared__ uint32_t wsum[kBWaves];
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   const int nd = 1 << dbits;
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x, nx);
   uint64_t base, nvalid;
   if constexpr (SEG) {
     if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
@@ -752,10 +765,10 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
 __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
     const GRec* __restrict__ in, SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
     uint32_t* __restrict__ dcnt, uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
-    uint32_t over_cap, unsigned long long* __restrict__ too_big) {
+    uint32_t over_cap, unsigned long long* __restrict__ too_big, uint32_t nx) {
   __shared__ BucketLds<kSmallW, kSmallPer> L;
-  bucket_sort_one<kSmallW, kSmallPer>(L, blockIdx.x, in, out, bstart, kshift, dcnt, true, over,
-                                      over_n, over_cap, too_big);
+  bucket_sort_one<kSmallW, kSmallPer>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), in, out,
+                                      bstart, kshift, dcnt, true, over, over_n, over_cap, too_big);
 }
 
 __global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
@@ -936,6 +949,10 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   hipStream_t st = ctx->stream;
   ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc, 0, kMiscWords * 8, st));
 
+  // XCD-contiguous tile order per scatter level (experiment knob
+  // ANOMOD_BK_XCD: bit 0 level A, bit 1 level B, bit 2 the bucket kernel)
+  const int xk = env_int("ANOMOD_BK_XCD", 7);
+  const uint32_t nxA = (xk & 1) ? 8u : 1u, nxB = (xk & 2) ? 8u : 1u;
   // level A
   const uint64_t nbA = (g.tilesA + kScanRows - 1) / kScanRows;
   const unsigned dgA = (unsigned)((na + 255) / 256);
@@ -959,7 +976,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
     hipLaunchKernelGGL((bk_scatter_kernel<true, false, kDnext>), dim3((unsigned)g.tilesA),
                        dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
                        dn, 64 - g.DA - kDMax, (uint32_t)((1u << kDMax) - 1u), nullptr, nullptr,
-                       nullptr, 0);
+                       nullptr, 0, nxA);
     if (ANOMOD_BK_ABL & 2) {  // timing of level A only
       *fallback = true;
       return ANOMOD_OK;
@@ -985,7 +1002,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
     }
     hipLaunchKernelGGL((bk_scatter_kernel<false, true, false>), dim3((unsigned)g.tilesB),
                        dim3(kBThreads), 0, st, sin, bufA, bufB, n, 64 - g.DA - g.DB, g.DB,
-                       ws->tcnt, nullptr, 0, 0u, ws->bsA, ws->btile, ws->tmap, na);
+                       ws->tcnt, nullptr, 0, 0u, ws->bsA, ws->btile, ws->tmap, na, nxB);
     cin = bufB;
     cols = soa_of(bufA);
     bstart = ws->bstart;
@@ -1001,7 +1018,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
     }
     hipLaunchKernelGGL((bk_scatter_kernel<true, false, false>), dim3((unsigned)g.tilesA),
                        dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
-                       nullptr, 0, 0u, nullptr, nullptr, nullptr, 0);
+                       nullptr, 0, 0u, nullptr, nullptr, nullptr, 0, nxA);
     cin = bufA;
     cols = soa_of(bufB);
     bstart = ws->bsA;
@@ -1014,7 +1031,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   const int kshift = 64 - g.T - kSubBits;
   hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, cin, cols,
                      bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
-                     ws->misc + kMiscTooBig);
+                     ws->misc + kMiscTooBig, (xk & 4) ? 8u : 1u);
   hipLaunchKernelGGL(bk_bucket_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
                      dim3(kBigW), 0, st, cin, cols, bstart, kshift, ws->dcnt, ws->over,
                      ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
