@@ -49,6 +49,7 @@ constexpr int kBTile = kBThreads * kBPer;      // 4096 records per tile
 constexpr int kDMax = 11;                      // digit bits per scatter level
 constexpr int kNDMax = 1 << kDMax;
 constexpr int kScanRows = 256;                 // tiles per block of the tile scan
+constexpr int kScanB = 16;                     // loads in flight per serial scan step
 constexpr int kSubBits = 9;                    // per-bucket split before the key compare
 constexpr int kSub = 1 << kSubBits;
 constexpr int kSmallW = 512, kSmallPer = 4;    // per-bucket kernel: 2048 spans
@@ -127,10 +128,16 @@ __global__ __launch_bounds__(1024) void bk_scan_top_kernel(uint32_t* __restrict_
     const int d = tid * dpt + i;
     if (d >= nd) continue;
     uint32_t run = 0;
-    for (uint64_t b = 0; b < nbk; ++b) {
-      const uint32_t x = bsum[b * nd + d];
-      bsum[b * nd + d] = run;
-      run += x;
+    for (uint64_t b = 0; b < nbk; b += kScanB) {
+      uint32_t x[kScanB];
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j) x[j] = b + j < nbk ? bsum[(b + j) * nd + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j)
+        if (b + j < nbk) {
+          bsum[(b + j) * nd + d] = run;
+          run += x[j];
+        }
     }
     tot[i] = run;
     til[i] = (run + kBTile - 1) / kBTile;
@@ -144,7 +151,14 @@ __global__ __launch_bounds__(1024) void bk_scan_top_kernel(uint32_t* __restrict_
     const uint32_t start = pre + (i ? tot[0] : 0u);
     bsA[d] = start;
     btile[d] = pret + (i ? til[0] : 0u);
-    for (uint64_t b = 0; b < nbk; ++b) bsum[b * nd + d] += start;
+    for (uint64_t b = 0; b < nbk; b += kScanB) {
+      uint32_t x[kScanB];
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j) x[j] = b + j < nbk ? bsum[(b + j) * nd + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j)
+        if (b + j < nbk) bsum[(b + j) * nd + d] = x[j] + start;
+    }
   }
   if (tid == 0) {
     bsA[nd] = (uint32_t)n;
@@ -224,12 +238,22 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
   const int tid = threadIdx.x, nd = 1 << db;
   const int dpt = nd > 1024 ? nd / 1024 : 1;
   const uint32_t b = blockIdx.x, t0 = btile[b], t1 = btile[b + 1], base = bsA[b];
+  // Both walks down the tiles batch kScanB loads ahead of their adds /
+  // stores (one HBM round trip per batch, not per tile: 2.8 -> 0.x ms at
+  // 2^27 SN traces).
   uint32_t tot[2] = {0u, 0u};
   for (int i = 0; i < dpt; ++i) {
     const int d = tid * dpt + i;
     if (d >= nd) continue;
     uint32_t s = 0;
-    for (uint32_t t = t0; t < t1; ++t) s += tcnt[(uint64_t)t * nd + d];
+    for (uint32_t t = t0; t < t1; t += kScanB) {
+      uint32_t x[kScanB];
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j)
+        x[j] = t + j < t1 ? tcnt[(uint64_t)(t + j) * nd + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j) s += x[j];
+    }
     tot[i] = s;
   }
   uint32_t all;
@@ -240,10 +264,17 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
     const uint32_t start = base + pre + (i ? tot[0] : 0u);
     bstart[(uint64_t)b * nd + d] = start;
     uint32_t run = start;
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t x = tcnt[(uint64_t)t * nd + d];
-      tcnt[(uint64_t)t * nd + d] = run;
-      run += x;
+    for (uint32_t t = t0; t < t1; t += kScanB) {
+      uint32_t x[kScanB];
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j)
+        x[j] = t + j < t1 ? tcnt[(uint64_t)(t + j) * nd + d] : 0u;
+#pragma unroll
+      for (int j = 0; j < kScanB; ++j)
+        if (t + j < t1) {
+          tcnt[(uint64_t)(t + j) * nd + d] = run;
+          run += x[j];
+        }
     }
   }
   if (b == (uint32_t)na - 1 && tid == 0) bstart[(uint64_t)na * nd] = bsA[na];
