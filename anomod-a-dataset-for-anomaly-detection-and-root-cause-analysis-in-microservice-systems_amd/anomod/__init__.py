@@ -16,8 +16,7 @@ from .decode import (MetricMatrix, decode_jaeger, decode_native, load_trace_file
                      decode_prometheus_csv_dir_native, decode_skywalking_payload, decode_skywalking_raw,
                      jaeger_span_rows, merge_jaeger_dumps, skywalking_parents)
 from .device import (Context, DeviceGraph, DeviceSeries, DeviceSpans, SynthSpec, device_count,
-                     device_count_safe,
-                     synth_generate_host, synth_services)
+                     device_count_safe, synth_generate_host, synth_graph_csr, synth_services)
 from .engine import (Experiment, Features, default_context, fault_target, features, hit_at,
                      load_experiment, rank)
 from . import api
@@ -33,7 +32,7 @@ __all__ = [
     "decode_prometheus_csv_dir_native", "decode_skywalking_payload",
     "decode_skywalking_raw", "default_context", "device_count", "device_count_safe", "edge_rows", "fault_target",
     "features", "hit_at", "jaeger_span_rows", "lib", "load_experiment", "merge_jaeger_dumps",
-    "rank", "skywalking_parents", "synth_generate_host", "synth_services", "TraceStructure",
+    "rank", "skywalking_parents", "synth_generate_host", "synth_graph_csr", "synth_services", "TraceStructure",
     "SegmentSet", "service_name_of", "trace_infos", "analyze_trace_patterns",
     "jaeger_to_csv", "write_jaeger_csv", "write_metric_long_csv", "decode_native",
     "load_trace_file", "api",

@@ -156,6 +156,8 @@ _SIGS = {
     "anomod_spans_unique_ids": (_i32, [_vp, _P(C.c_int)]),
     "anomod_spans_scan_order": (_i32, [_vp, _P(C.c_int)]),
     "anomod_spans_hist_compact": (_i32, [_vp, _P(C.c_int)]),
+    "anomod_spans_hints": (_i32, [_vp, _P(C.c_int), _P(C.c_int)]),
+    "anomod_spans_set_hints": (_i32, [_vp, C.c_int, C.c_int]),
     "anomod_spans_upload_ungrouped": (_i32, [_vp, _P(SpanSoA), _u64, _P(_vp)]),
     "anomod_spans_grouped": (_i32, [_vp, _P(_i32)]),
     "anomod_spans_group": (_i32, [_vp, _vp, _P(_vp)]),
@@ -182,6 +184,7 @@ _SIGS = {
     "anomod_decode_skywalking": (_i32, [C.c_char_p, _u64, _P(C.c_char_p), _u32, _P(_vp)]),
     "anomod_decoded_info": (_i32, [_vp, _P(_u64), _P(_u64), _P(_u32)]),
     "anomod_decoded_service": (C.c_char_p, [_vp, _u32]),
+    "anomod_decoded_unique_ids": (_i32, [_vp, _P(C.c_int)]),
     "anomod_decoded_columns": (_i32, [_vp, _P(SpanSoA), _P(_u64)]),
     "anomod_decoded_free": (_i32, [_vp]),
     "anomod_hash64": (_u64, [C.c_char_p, _u64]),
@@ -200,12 +203,15 @@ _SIGS = {
     "anomod_series_upload": (_i32, [_vp, _vp, _P(_f32)]),
     "anomod_series_fill_synthetic": (_i32, [_vp, _vp, _u64, _u64]),
     "anomod_series_reset_state": (_i32, [_vp, _vp]),
+    "anomod_series_download": (_i32, [_vp, _vp, _P(_f32)]),
     "anomod_series_ewma_z": (_i32, [_vp, _vp, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_free": (_i32, [_vp]),
     "anomod_pagerank": (_i32, [_vp, _P(_u32), _P(_u32), _P(_f32), _u32, _P(_f64), _f64, _u32,
                                _f64, _P(_f64), _P(_u32)]),
     "anomod_graph_create": (_i32, [_vp, _P(_u32), _P(_u32), _P(_f32), _u32, _P(_vp)]),
     "anomod_graph_synthetic": (_i32, [_vp, _u32, _u32, _u64, _P(_vp)]),
+    "anomod_graph_synthetic_csr": (_i32, [_u32, _u32, _u64, _P(_u32), _P(_u32), _P(_f32), _u64,
+                                          _P(_u64)]),
     "anomod_graph_info": (_i32, [_vp, _P(_u32), _P(_u64)]),
     "anomod_graph_last_solve": (_i32, [_vp, _P(_u32), _P(_u32)]),
     "anomod_graph_pagerank": (_i32, [_vp, _vp, _P(_f64), _f64, _u32, _f64, _P(_f64), _P(_u32)]),

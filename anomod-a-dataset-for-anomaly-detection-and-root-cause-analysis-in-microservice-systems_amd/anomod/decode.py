@@ -480,9 +480,12 @@ def decode_native(data: "bytes | MappedFile", kind: str, services: list[str] | N
             ("svc", C.c_uint16), ("flags", C.c_uint16), ("dur_us", C.c_uint32))])
         L.check(lib.anomod_decoded_columns(h, C.byref(soa), L.ptr(ptr, C.c_uint64)))
         svcs = [lib.anomod_decoded_service(h, i).decode() for i in range(nsv.value)]
+        uniq = C.c_int()
+        L.check(lib.anomod_decoded_unique_ids(h, C.byref(uniq)))
     finally:
         lib.anomod_decoded_free(h)
-    return SpanSet(svcs, ptr, **arr)
+    # the decoder checked every trace's ids exactly while decoding
+    return SpanSet(svcs, ptr, **arr, unique_ids=bool(uniq.value))
 
 
 def _first_key(data: bytes) -> str | None:
@@ -494,19 +497,20 @@ def load_trace_file(path, services: list[str] | None = None) -> SpanSet:
     """A trace file of the dataset -> SpanSet: Jaeger dumps ({"data": ...})
     and collector payloads ({"metadata": ..., "traces": ...}) go through the
     native decoder; anything else (raw GraphQL span lists) through the
-    Python decoders.  The set's unique_ids is checked exactly."""
-    spans = _load_trace_file(path, services)
-    spans.check_unique_ids()
-    return spans
-
-
-def _load_trace_file(path, services: list[str] | None = None) -> SpanSet:
+    Python decoders.  The set's unique_ids is checked exactly (by the native
+    decoder while it decodes, else on the columns)."""
     data = map_file(path)
     key = _first_key(data[:4096])
     if key == "data":
         return decode_native(data, "jaeger", services)
     if key in ("metadata", "traces"):
         return decode_native(data, "skywalking", services)
+    spans = _load_trace_file_py(data, path, services)
+    spans.check_unique_ids()
+    return spans
+
+
+def _load_trace_file_py(data, path, services: list[str] | None = None) -> SpanSet:
     doc = json.loads(data[:])
     if isinstance(doc, dict) and "traces" in doc:
         return decode_skywalking_payload(doc, services)

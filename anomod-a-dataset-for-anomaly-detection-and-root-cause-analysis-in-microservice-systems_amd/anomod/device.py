@@ -65,7 +65,7 @@ def synth_generate_host(spec: SynthSpec, n_traces: int, shard: int = 0) -> SpanS
     L.check(lib.anomod_synth_generate_host(C.byref(cs), shard, n_traces,
                                            C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)))
     # span ids are injective in the span index (csrc/synth.h synth_span_id)
-    return SpanSet(spec.services(), ptr, **arr, unique_ids=True)
+    return SpanSet(spec.services(), ptr, **arr, unique_ids=True, scan_order=1)
 
 
 def _soa_out(arr: dict) -> L.SpanSoA:
@@ -122,6 +122,16 @@ class DeviceSpans:
     def unique_ids(self, v: bool):
         L.check(L.lib().anomod_spans_set_unique_ids(self.handle, 1 if v else 0))
 
+    @property
+    def hints(self) -> tuple[int, int]:
+        """(scan_order, hist_form) the library holds for this set."""
+        o, f = C.c_int(), C.c_int()
+        L.check(L.lib().anomod_spans_hints(self.handle, C.byref(o), C.byref(f)))
+        return o.value, f.value
+
+    def set_hints(self, scan_order: int, hist_form: int):
+        L.check(L.lib().anomod_spans_set_hints(self.handle, scan_order, hist_form))
+
     def download(self) -> SpanSet:
         n = self.n_spans
         arr = dict(trace_hash=np.empty(n, np.uint64), span_id=np.empty(n, np.uint64),
@@ -131,7 +141,9 @@ class DeviceSpans:
         L.check(L.lib().anomod_spans_download(self.ctx.handle, self.handle,
                                               C.byref(_soa_out(arr)), L.ptr(ptr, C.c_uint64)),
                 self.ctx.handle)
-        return SpanSet(self.services, ptr, **arr, unique_ids=self.unique_ids)
+        order, form = self.hints
+        return SpanSet(self.services, ptr, **arr, unique_ids=self.unique_ids, scan_order=order,
+                       hist_form=form)
 
     def free(self):
         if self.handle:
@@ -261,6 +273,7 @@ class Context:
                                                   spans.n_traces, C.byref(h)))
         d = DeviceSpans(self, h, spans.services)
         d.unique_ids = spans.unique_ids
+        d.set_hints(spans.scan_order, spans.hist_form)
         return d
 
     def upload_ungrouped(self, spans: SpanSet) -> DeviceSpans:
@@ -272,6 +285,7 @@ class Context:
                                                             spans.n_spans, C.byref(h)))
         d = DeviceSpans(self, h, spans.services)
         d.unique_ids = spans.unique_ids
+        d.set_hints(spans.scan_order, spans.hist_form)
         return d
 
     def group(self, spans: DeviceSpans) -> DeviceSpans:
@@ -298,9 +312,11 @@ class Context:
         return DeviceSpans(self, h, spec.services())
 
     def edge_aggregate(self, spans: DeviceSpans | SpanSet, with_hist: bool = True) -> EdgeTable:
-        """Edge table of a span set (uploading it first if it is on the host)."""
-        tmp = None
+        """Edge table of a span set (uploading it first if it is on the host;
+        the hints learned on the device go back onto the host set)."""
+        tmp = host = None
         if isinstance(spans, SpanSet):
+            host = spans
             tmp = spans = self.upload(spans)
         try:
             table = EdgeTable.empty(spans.services, with_hist)
@@ -310,6 +326,8 @@ class Context:
             self._check(fn(self.handle, spans.handle, len(spans.services), C.byref(cs)))
             if table.hist is not None:
                 table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
+            if host is not None:
+                host.scan_order, host.hist_form = tmp.hints
             return table
         finally:
             if tmp is not None:
@@ -393,6 +411,23 @@ class Context:
                                               L.ptr(p, C.c_double), alpha, iters, tol,
                                               L.ptr(x, C.c_double), C.byref(done)))
         return x, done.value
+
+
+def synth_graph_csr(N: int, mean_degree: int = 10, seed: int = 11):
+    """Host CSR (row_ptr u32, col u32, w f32) of the synthetic config-5 graph
+    DeviceGraph(synthetic=(N, mean_degree, seed)) solves."""
+    lib = L.lib()
+    nnz = C.c_uint64()
+    nul32 = C.cast(None, C.POINTER(C.c_uint32))
+    L.check(lib.anomod_graph_synthetic_csr(N, mean_degree, seed, nul32, nul32,
+                                           C.cast(None, C.POINTER(C.c_float)), 0, C.byref(nnz)))
+    row_ptr = np.empty(N + 1, np.uint32)
+    col = np.empty(max(1, nnz.value), np.uint32)
+    w = np.empty(max(1, nnz.value), np.float32)
+    L.check(lib.anomod_graph_synthetic_csr(N, mean_degree, seed, L.ptr(row_ptr, C.c_uint32),
+                                           L.ptr(col, C.c_uint32), L.ptr(w, C.c_float),
+                                           col.shape[0], C.byref(nnz)))
+    return row_ptr, col[:nnz.value], w[:nnz.value]
 
 
 class DeviceGraph:
@@ -494,6 +529,13 @@ class DeviceSeries:
 
     def reset_state(self):
         self.ctx._check(L.lib().anomod_series_reset_state(self.ctx.handle, self.handle))
+
+    def download(self) -> np.ndarray:
+        """The resident matrix as host rows X[T][S]."""
+        X = np.empty((self.T, self.S), np.float32)
+        self.ctx._check(L.lib().anomod_series_download(self.ctx.handle, self.handle,
+                                                       L.ptr(X, C.c_float)))
+        return X
 
     def ewma_z(self, alpha: float, W: int, eps: float = 1e-12, download: bool = True):
         Z = np.empty((self.T // W, self.S), np.float32) if download else None

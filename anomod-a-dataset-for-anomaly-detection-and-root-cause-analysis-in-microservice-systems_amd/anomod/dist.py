@@ -100,12 +100,21 @@ class HostGroup:
     host-transport buffers of tests on one device."""
 
     def __init__(self, rank: int, world: int, key: str | None = None,
-                 timeout_s: float | None = None, rdzv_dir: str | None = None):
+                 timeout_s: float | None = None, rdzv_dir: str | None = None,
+                 coll_timeout_s: float | None = None):
+        """timeout_s bounds the rendezvous (ANOMOD_RCCL_TIMEOUT_S, 300 s);
+        once the group is formed a collective waits coll_timeout_s for a peer
+        (ANOMOD_HOSTGROUP_TIMEOUT_S; default: as long as it takes — a barrier
+        behind a slow rank must not fail, and a rank that dies closes its
+        socket, which every peer sees at once)."""
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"bad rank {rank} of world {world}")
         self.rank, self.world = rank, world
         self.timeout_s = float(timeout_s if timeout_s is not None
                                else os.environ.get("ANOMOD_RCCL_TIMEOUT_S", "300"))
+        if coll_timeout_s is None and os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S"):
+            coll_timeout_s = float(os.environ["ANOMOD_HOSTGROUP_TIMEOUT_S"])
+        self.coll_timeout_s = coll_timeout_s
         self._peers: list[socket.socket] = []  # rank 0: ranks 1..world-1 in order
         self._sock: socket.socket | None = None  # other ranks: the link to rank 0
         self._file: Path | None = None
@@ -135,33 +144,48 @@ class HostGroup:
                     except socket.timeout:
                         raise TimeoutError(f"anomod host group: {len(peers) + 1} of {world} "
                                            f"ranks joined within {self.timeout_s:.0f} s") from None
-                    c.settimeout(self.timeout_s)
-                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    hello = _recv(c)
-                    magic, r, w = hello[:4], *struct.unpack("<ii", hello[4:12])
+                    # a stray or stale client that stalls, closes or sends
+                    # garbage is dropped, not fatal to the rendezvous
+                    c.settimeout(min(5.0, max(0.1, deadline - time.monotonic())))
+                    try:
+                        c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                        hello = _recv(c)
+                        magic, r, w = hello[:4], *struct.unpack("<ii", hello[4:12])
+                    except (OSError, ConnectionError, struct.error):
+                        c.close()
+                        continue
                     if magic != _MAGIC or w != world or not 0 < r < world or r in peers:
                         c.close()
                         continue
                     peers[r] = c
+            except BaseException:
+                for c in peers.values():
+                    c.close()
+                raise
             finally:
                 srv.close()
             self._peers = [peers[r] for r in range(1, world)]
             for c in self._peers:
+                c.settimeout(self.coll_timeout_s)
                 _send(c, b"ok")
         else:
             while True:
+                s = None
                 try:
                     info = json.loads(path.read_text())
                     s = socket.create_connection((info["addr"], info["port"]), timeout=5.0)
-                    s.settimeout(self.timeout_s)
+                    s.settimeout(max(0.1, deadline - time.monotonic()))
                     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     _send(s, _MAGIC + struct.pack("<ii", rank, world))
                     if _recv(s) == b"ok":
-                        self._sock = s
+                        s.settimeout(self.coll_timeout_s)
+                        self._sock, s = s, None
                         break
-                    s.close()
-                except (OSError, ValueError, KeyError, ConnectionError):
+                except (OSError, ValueError, KeyError, ConnectionError, struct.error):
                     pass  # not published yet, or a stale file of an earlier run
+                finally:
+                    if s is not None:
+                        s.close()
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"anomod host group: rank {rank} found no rank 0 at "
                                        f"{path} within {self.timeout_s:.0f} s")

@@ -29,6 +29,15 @@ class SpanSet:
     # span ids unique within every trace (the producer's declaration, or
     # check_unique_ids()): lets the GPU parent lookups scan from both ends
     unique_ids: bool = False
+    # performance hints the library learns on the device at a set's first
+    # aggregation (include/anomod.h anomod_spans_hints): parent-scan order
+    # (1 collector order / 0 shuffled / -1 unknown) and histogram form (0 pair
+    # / 1 compact / -1 unknown).  Context.upload hands them to every upload
+    # and edge_aggregate keeps what was learned, so a host set that is
+    # uploaded per call (features()) learns them once.  Results never depend
+    # on them.
+    scan_order: int = field(default=-1, compare=False)
+    hist_form: int = field(default=-1, compare=False)
     _keep: list = field(default_factory=list, repr=False, compare=False)
 
     def __post_init__(self):

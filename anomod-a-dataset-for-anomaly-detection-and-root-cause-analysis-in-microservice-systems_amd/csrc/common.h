@@ -68,12 +68,13 @@ struct anomod_spans {
   // UINT64_MAX = unknown.  Lets a call skip the long-trace pass when no
   // trace outgrows a wave chunk.
   uint64_t max_trace_len = ~0ull;
-  // The SN-width (E <= 512) edge kernel privatises its histogram in the pair
-  // form (8 Ki slots) — right for sets that touch a few thousand (edge, bin)
-  // keys per workgroup.  A set whose aggregation overflowed that table
-  // (spans counted in HBM after a full probe chain) takes the compact form
-  // (16 Ki packed slots) from then on; set by anomod_edge_aggregate_spans.
-  mutable bool hist_compact = false;
+  // Histogram form of the SN / TrainTicket-width edge kernels: 0 = pair (8 Ki
+  // slots, right for sets that touch a few thousand (edge, bin) keys per
+  // workgroup), 1 = compact (16 Ki packed slots), -1 = not known yet — the
+  // aggregation then starts in the pair form and any workgroup whose table
+  // saturates hands its remaining traces to a compact-form resume launch
+  // (edge_agg.hip); the outcome is kept here for the set's next aggregation.
+  mutable int8_t hist_form = -1;
   // Span ids are unique within every trace (declared by the producer: the
   // synthetic generator by construction, anomod_spans_set_unique_ids for
   // decoded / uploaded sets).  Lets the parent lookups scan from both ends

@@ -54,6 +54,7 @@ struct anomod_decoded {
   std::vector<uint64_t> trace_hash, span_id, parent;
   std::vector<uint16_t> svc, flags;
   std::vector<uint32_t> dur;
+  bool dup_ids = false;  // some trace holds a span id twice (anomod_decoded_unique_ids)
 };
 
 namespace {
@@ -563,6 +564,14 @@ void jaeger_trace(const Dom& d, uint32_t tr, anomod_decoded* out, Names& names,
       out->dur.push_back(clamp_u32(d, d.get(sp, "duration")));
     }
   }
+  // span ids unique inside the trace? (lets the GPU parent scans run from
+  // both ends; a sort of the trace's ids, O(L log L))
+  if (!out->dup_ids) {
+    thread_local std::vector<uint64_t> ids;
+    ids.assign(out->span_id.begin() + (std::ptrdiff_t)out->trace_ptr.back(), out->span_id.end());
+    std::sort(ids.begin(), ids.end());
+    out->dup_ids = std::adjacent_find(ids.begin(), ids.end()) != ids.end();
+  }
   out->trace_ptr.push_back(out->span_id.size());
 }
 
@@ -583,7 +592,8 @@ void skywalking_trace(const Dom& d, uint32_t tr, anomod_decoded* out, Names& nam
   first.clear();
   uint64_t k = 0;
   for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next, ++k)
-    first.emplace(py_str(d, d.get(sp, "node_id")), k + 1);
+    if (!first.emplace(py_str(d, d.get(sp, "node_id")), k + 1).second)
+      out->dup_ids = true;  // a node id twice: both spans get its first occurrence's id
   for (uint32_t sp = d.at(spans).first; sp != kNone; sp = d.at(sp).next) {
     out->trace_hash.push_back(th);
     out->span_id.push_back(first[py_str(d, d.get(sp, "node_id"))]);
@@ -835,6 +845,7 @@ bool decode_parallel(const char* json, size_t len, int kind, anomod_decoded* out
     app(out->parent, part[t].parent);
     app(out->flags, part[t].flags);
     app(out->dur, part[t].dur);
+    out->dup_ids = out->dup_ids || part[t].dup_ids;
     for (size_t k = 1; k < part[t].trace_ptr.size(); ++k)
       out->trace_ptr.push_back(base + part[t].trace_ptr[k]);
   }
@@ -927,6 +938,15 @@ int anomod_decoded_info(const anomod_decoded* d, uint64_t* n_spans, uint64_t* n_
   if (n_spans) *n_spans = d->span_id.size();
   if (n_traces) *n_traces = d->trace_ptr.size() - 1;
   if (n_services) *n_services = (uint32_t)d->services.size();
+  return ANOMOD_OK;
+}
+
+int anomod_decoded_unique_ids(const anomod_decoded* d, int* unique) {
+  if (!d || !unique) {
+    anomod::set_error(nullptr, "anomod_decoded_unique_ids: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  *unique = d->dup_ids ? 0 : 1;
   return ANOMOD_OK;
 }
 

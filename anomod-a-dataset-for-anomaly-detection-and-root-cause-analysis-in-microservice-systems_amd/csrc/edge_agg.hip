@@ -107,7 +107,15 @@ constexpr int kOffWideErr = kOffSum + (int)kWideEdges * 16;
 constexpr int kStatsEnd = std::max({kOffMm + (int)(kLdsEdges * 12),   // direct
                                     kOffMm + (int)(kSlotEdges * 16),  // slot
                                     kOffWideErr + (int)kWideEdges * 4});  // wide
-constexpr int kOffWave = (kStatsEnd + 15) & ~15;
+// u32 control words: [0] pair-form inserts that found their probe chain full
+// (counted in HBM; added to tab.ovf once per workgroup at the flush)
+constexpr int kOffCtl = (kStatsEnd + 15) & ~15;
+constexpr int kOffWave = kOffCtl + 16;
+// A workgroup of a first (form-unknown) aggregation whose pair table turned
+// away this many inserts stops: its waves hand their remaining traces to the
+// compact-form resume launch (edge_agg_kernel, kModeAuto / kModeResume).
+constexpr uint32_t kSatFails = 64;
+enum LaunchMode : uint32_t { kModeNormal = 0, kModeAuto = 1, kModeResume = 2 };
 enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2, kStWide = 3 };
 constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
 constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
@@ -131,7 +139,11 @@ struct Table {
   unsigned long long* big_list;  // long traces: trace indices
   uint16_t* bpar;            // long traces: every listed span's parent row (S root, S + 1 orphan)
   uint64_t t_base;           // trace index of this launch's first trace
-  unsigned long long* ovf;   // spans whose pair-form probe chain was full (counted in HBM)
+  unsigned long long* ovf;   // [0] spans whose pair-form probe chain was full (counted in
+                             // HBM), [1] workgroups that stopped at a saturated pair table
+  unsigned long long* left;  // kModeAuto: [2 j], [2 j + 1] = trace range j a stopped wave left
+  unsigned long long* nleft; // [0] ranges left, [1] resume ticket
+  uint32_t mode;             // LaunchMode
 };
 
 struct Cols {
@@ -166,7 +178,7 @@ __device__ __forceinline__ uint32_t ht_hash(uint32_t key) { return key * 0x9E377
 __device__ __attribute__((noinline)) void ht_insert_pair(uint32_t* hk, uint32_t* hc, uint32_t key,
                                                          uint32_t s,
                                                          unsigned long long* __restrict__ ghist,
-                                                         unsigned long long* __restrict__ ovf) {
+                                                         uint32_t* ctl) {
   for (int probe = 0; probe < kPairMaxProbe; ++probe) {
     uint32_t cur = __hip_atomic_load(&hk[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == 0u) {
@@ -180,7 +192,11 @@ __device__ __attribute__((noinline)) void ht_insert_pair(uint32_t* hk, uint32_t*
     s = (s + 1u) & (kPairSlots - 1u);
   }
   atomicAdd(&ghist[key - 1u], 1ull);
-  atomicAdd(ovf, 1ull);  // the host switches this span set to the compact form
+  // counted per workgroup in LDS (one HBM add at the flush: a device-wide
+  // counter bumped per span was itself a contended hot spot); a first
+  // aggregation stops the workgroup at kSatFails, and the host switches the
+  // set to the compact form
+  atomicAdd(&ctl[0], 1u);
 }
 
 __device__ __forceinline__ void ht_wrap(uint32_t old, uint32_t key, uint32_t kb,
@@ -336,7 +352,7 @@ __device__ __forceinline__ void record(unsigned char* smem, uint32_t edge, uint3
     const bool hit = (j < 3u) | (bk.w == key);
     atomicAdd(&hc[s0 + j], hit ? 1u : 0u);
     stat_add<ST>(smem, edge, d, fl, tab, pk);
-    if (!hit) ht_insert_pair(hk, hc, key, s0, tab.hist, tab.ovf);
+    if (!hit) ht_insert_pair(hk, hc, key, s0, tab.hist, reinterpret_cast<uint32_t*>(smem + kOffCtl));
   } else {  // kHtCompact
     auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
     const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
@@ -472,6 +488,7 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
 // the device table with integer atomics (order-free) at the end.
 template <int HT, int ST>
 __device__ __forceinline__ void tables_init(unsigned char* smem, uint32_t E, int tid) {
+  if (tid < 4) reinterpret_cast<uint32_t*>(smem + kOffCtl)[tid] = 0u;
   if constexpr (HT == kHtPair || HT == kHtCompact) {
     auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);  // both forms: 64 KiB of zeros
     for (uint32_t s = tid; s < (uint32_t)kHtBytes / 4u; s += kThreads) hk[s] = 0u;
@@ -520,6 +537,11 @@ __device__ __forceinline__ void tables_flush(unsigned char* smem, uint32_t E, co
     for (uint32_t s = tid; s < kPairSlots; s += kThreads) {
       const uint32_t cnt = hc[s];
       if (cnt) atomicAdd(&tab.hist[hk[s] - 1u], (unsigned long long)cnt);
+    }
+    if (tid == 0) {
+      const uint32_t fails = reinterpret_cast<const uint32_t*>(smem + kOffCtl)[0];
+      if (fails) atomicAdd(&tab.ovf[0], (unsigned long long)fails);
+      if (tab.mode == kModeAuto && fails >= kSatFails) atomicAdd(&tab.ovf[1], 1ull);
     }
   }
   if constexpr (HT == kHtCompact) {
@@ -1209,7 +1231,7 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_record_kernel(
   tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
-template <int HT, int ST, bool UNI>
+template <int HT, int ST, bool UNI, int MODE = kModeNormal>
 __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
@@ -1219,13 +1241,6 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   const int lane = tid & (kWave - 1);
   const int wid = tid / kWave;
   const Cols col{span_id, parent, svcfl, dur};
-
-  tables_init<HT, ST>(smem, E, tid);
-  __syncthreads();
-
-  unsigned char* wsm = smem + kOffWave + wid * kWBytes;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
 #ifndef ANOMOD_DYN
 #define ANOMOD_DYN 4
 #endif
@@ -1237,8 +1252,37 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
 #endif
   constexpr uint64_t kDynSeg = ANOMOD_DYN_SEG;
   const uint64_t n_static = ANOMOD_DYN ? n_traces - n_traces / (ANOMOD_DYN ? ANOMOD_DYN : 1) : n_traces;
+  // Resume launch (compact form) after a kModeAuto launch: the trace ranges
+  // its stopped waves left, then the rest of the dynamic tail.  Nothing left
+  // (no workgroup saturated): return before touching LDS.
+  constexpr bool resume = MODE == kModeResume;
+  const uint64_t n_left = resume ? tab.nleft[0] : 0;
+  if (resume && n_left == 0 && n_static + *tab.ctr >= n_traces) return;
+
+  tables_init<HT, ST>(smem, E, tid);
+  __syncthreads();
+
+  unsigned char* wsm = smem + kOffWave + wid * kWBytes;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wid;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
   uint64_t t_begin = uniform64(n_static * gw / nw);
   uint64_t t_end = uniform64(n_static * (gw + 1) / nw);
+  bool from_left = resume;
+  auto next_left = [&]() {  // the next range a stopped wave left (false: none)
+    unsigned long long j = 0;
+    if (lane == 0) j = atomicAdd(&tab.nleft[1], 1ull);
+    j = uniform64(__shfl(j, 0));
+    if (j >= n_left) return false;
+    t_begin = uniform64(tab.left[2 * j]);
+    t_end = uniform64(tab.left[2 * j + 1]);
+    return true;
+  };
+  if (resume && !next_left()) {
+    from_left = false;
+    t_begin = t_end = 0;
+  }
+  bool stopped = false;
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + kOffCtl);
 
   while (true) {
   if (t_begin < t_end) {
@@ -1253,6 +1297,20 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     uint64_t t_next = t_begin + (cur.k ? cur.k : 1u);
     load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
     while (true) {
+      // A first aggregation (kModeAuto) whose pair table saturated: leave
+      // [t_cur, t_end) to the compact-form resume launch and stop.
+      if (MODE == kModeAuto &&
+          __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >=
+              kSatFails) {
+        if (lane == 0) {
+          const unsigned long long j = atomicAdd(&tab.nleft[0], 1ull);
+          tab.left[2 * j] = t_cur;
+          tab.left[2 * j + 1] = t_end;
+        }
+        stopped = true;
+        break;
+      }
       const bool has_next = t_next < t_end;
       const uint64_t t_nxt = t_next;
       Chunk nxt{};
@@ -1273,6 +1331,11 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       t_cur = t_nxt;
       R = Rn;
     }
+  }
+  if (stopped) break;
+  if (from_left) {
+    if (next_left()) continue;
+    from_left = false;
   }
   if (!ANOMOD_DYN || n_static == n_traces) break;
   unsigned long long g = 0;
@@ -1394,13 +1457,15 @@ __global__ __launch_bounds__(256) void exact_pick_kernel(const unsigned long lon
 using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                           const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
 
-// The histogram form an SN-width set asks for: its hint, or ANOMOD_HIST_FORM
-// = compact / pair (tests force either).
-bool want_compact(const anomod_spans* s) {
+// The histogram form a set asks for: 0 pair, 1 compact, -1 unknown (pair with
+// the saturation hand-off to a compact resume launch) — its hint, or
+// ANOMOD_HIST_FORM = pair / compact / auto (tests force each).
+int hist_form_of(const anomod_spans* s) {
   const char* f = getenv("ANOMOD_HIST_FORM");
-  if (f && !strcmp(f, "compact")) return true;
-  if (f && !strcmp(f, "pair")) return false;
-  return s->hist_compact;
+  if (f && !strcmp(f, "compact")) return 1;
+  if (f && !strcmp(f, "pair")) return 0;
+  if (f && !strcmp(f, "auto")) return -1;
+  return s->hist_form;
 }
 
 // Collector-order probe of a unique-id set: over its first kProbeSpans spans,
@@ -1464,11 +1529,23 @@ struct Pick {
   const char* name;
 };
 
-Pick pick_kernel(uint32_t E, bool compact, bool uni) {
+// mode: kModeAuto only for the pair forms, kModeResume only for the compact
+// forms of the SN / TrainTicket widths (the instantiations that exist).
+Pick pick_kernel(uint32_t E, bool compact, bool uni, int mode = kModeNormal) {
   const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
   const bool lds_hist = keys < (1ull << 31);  // >= 1 count bit above the key
 #define ANOMOD_PICK(H, S_, NAME)                                                               \
   return Pick{uni ? edge_agg_kernel<H, S_, true> : edge_agg_kernel<H, S_, false>, H, S_, NAME}
+#define ANOMOD_PICK_M(H, S_, M, NAME)                                                          \
+  return Pick{uni ? edge_agg_kernel<H, S_, true, M> : edge_agg_kernel<H, S_, false, M>, H, S_, NAME}
+  if (lds_hist && E <= kLdsEdges && mode == kModeResume)
+    ANOMOD_PICK_M(kHtCompact, kStDirect, kModeResume, "edge_agg_kernel<lds_compact_hist,lds_stats,resume>");
+  if (lds_hist && E <= kLdsEdges && !compact && mode == kModeAuto)
+    ANOMOD_PICK_M(kHtPair, kStDirect, kModeAuto, "edge_agg_kernel<lds_hist,lds_stats,auto>");
+  if (lds_hist && E > kLdsEdges && E <= kWideEdges && mode == kModeResume)
+    ANOMOD_PICK_M(kHtCompact, kStWide, kModeResume, "edge_agg_kernel<lds_compact_hist,wide_stats,resume>");
+  if (lds_hist && E > kLdsEdges && E <= kWideEdges && !compact && mode == kModeAuto)
+    ANOMOD_PICK_M(kHtPair, kStWide, kModeAuto, "edge_agg_kernel<lds_hist,wide_stats,auto>");
   if (lds_hist && E <= kLdsEdges && compact)  // a set that overflowed the pair table
     ANOMOD_PICK(kHtCompact, kStDirect, "edge_agg_kernel<lds_compact_hist,lds_stats>");
   if (lds_hist && E <= kLdsEdges) ANOMOD_PICK(kHtPair, kStDirect, "edge_agg_kernel<lds_hist,lds_stats>");
@@ -1482,20 +1559,22 @@ Pick pick_kernel(uint32_t E, bool compact, bool uni) {
   if (lds_hist) ANOMOD_PICK(kHtCompact, kStSlot, "edge_agg_kernel<lds_compact_hist,slot_stats>");
   ANOMOD_PICK(kHtHbm, kStHbm, "edge_agg_kernel<hbm_hist,hbm_stats>");
 #undef ANOMOD_PICK
+#undef ANOMOD_PICK_M
 }
 
 // Device table layout inside ctx->d_table: hist | err | sum (u64, one sum
 // all-reduce) | mx (u32, zero-initialised with them: one memset) | pad |
-// ctr (u64) | big counters (u64 x 3) + probe scratch (u64 x 2) | pair-table overflows (u64; all
-// zeroed with them) | count | p50 |
-// p99 | mn | long-trace list | long-trace parent rows (u16 per span).  [off_err, end_small) is copied to the host in
-// one D2H.
+// ctr (u64) | big counters (u64 x 3) + probe scratch (u64 x 2) | pair-table
+// overflows + stopped workgroups (u64 x 2) | ranges left + resume ticket
+// (u64 x 2; all zeroed with them) | count | p50 | p99 | mn | long-trace list |
+// ranges left by stopped waves (u64 pairs) | long-trace parent rows (u16 per
+// span).  [off_err, end_small) is copied to the host in one D2H.
 struct Layout {
   uint64_t E;
-  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_ovf, off_count, off_p50,
-      off_p99, off_mn, end_small, bytes;
+  size_t off_hist, off_err, off_sum, off_mx, off_ctr, off_big, off_ovf, off_nleft, off_count,
+      off_p50, off_p99, off_mn, end_small, off_left, bytes;
   size_t off_bpar = 0;
-  Layout(uint64_t e, uint64_t big_cap, uint64_t n_spans = 0) : E(e) {
+  Layout(uint64_t e, uint64_t big_cap, uint64_t n_spans = 0, uint64_t left_cap = 0) : E(e) {
     off_hist = 0;
     off_err = off_hist + E * kBins * 8;
     off_sum = off_err + E * 8;
@@ -1503,12 +1582,14 @@ struct Layout {
     off_ctr = (off_mx + E * 4 + 7) & ~size_t(7);
     off_big = off_ctr + 8;
     off_ovf = off_big + 40;  // listed, two tickets, two words of order-probe scratch
-    off_count = off_ovf + 8;
+    off_nleft = off_ovf + 16;
+    off_count = off_nleft + 16;
     off_p50 = off_count + E * 8;
     off_p99 = off_p50 + E * 8;
     off_mn = off_p99 + E * 8;
     end_small = off_mn + E * 4;
-    bytes = ((end_small + 7) & ~size_t(7)) + big_cap * 8;
+    off_left = ((end_small + 7) & ~size_t(7)) + big_cap * 8;
+    bytes = off_left + left_cap * 16;
     off_bpar = bytes;                           // u16 parent rows, by span position
     if (big_cap) bytes += (n_spans * 2 + 7) & ~size_t(7);
   }
@@ -1553,7 +1634,9 @@ hipError_t launch_big_for(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S
   // the LDS tables' u32 counters hold < 2^32 records per workgroup: a set
   // whose listed traces could exceed a launch's bound records to HBM
   if (spans->n_spans >= max_launch_spans()) return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
-  const Pick pk = pick_kernel(E, want_compact(spans), false);
+  // the pair form only for a set known to fit it (a form-unknown set records
+  // its long traces in the compact form, which has no probe chain)
+  const Pick pk = pick_kernel(E, hist_form_of(spans) != 0, false);
   if (pk.ht == kHtPair && pk.st == kStDirect)
     return launch_big<kHtPair, kStDirect>(ctx, spans, S, E, tab);
   if (pk.ht == kHtCompact && pk.st == kStDirect)
@@ -1594,8 +1677,30 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
                      "span service index %u >= n_services %u", spans->max_svc, S);
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
   const uint64_t big_cap = big_capacity(spans);
-  const Layout L(E, big_cap, spans->n_spans);
+  // Histogram form: a set known to fit the pair table takes it, a set that
+  // overflowed it the compact form; a set not aggregated before starts in the
+  // pair form (kModeAuto) and any workgroup whose table saturates stops and
+  // leaves its remaining traces to a compact-form resume launch — so a first
+  // call costs about what the right form costs, never a probe-chain cliff.
+  const int form = hist_form_of(spans);
+  const bool uni = use_unique(spans);
+  const bool autof = form < 0 && pick_kernel(E, false, uni).ht == kHtPair;
+  const Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal);
+  const Pick pr = autof ? pick_kernel(E, true, uni, kModeResume) : pk;  // the resume launch's form
+  // As many workgroups as are resident at once (LDS / registers decide).
+  int per_cu = 0, per_cu_r = 0;
   if (local == ANOMOD_OK) local = bind(ctx);
+  if (local == ANOMOD_OK &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(pk.fn),
+                                                    kThreads, 0) != hipSuccess ||
+       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_r, reinterpret_cast<const void*>(pr.fn),
+                                                    kThreads, 0) != hipSuccess)) {
+    set_error(ctx, "occupancy query of %s failed", pk.name);
+    local = ANOMOD_EHIP;
+  }
+  const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
+  const uint64_t grid_r = (uint64_t)ctx->num_cus * (uint64_t)(per_cu_r > 0 ? per_cu_r : 1);
+  const Layout L(E, big_cap, spans->n_spans, autof ? grid * kWavesPerWG : 0);
   if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
   if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.end_small - L.off_err);
   if (int rc = comm_agree(ctx, local)) return rc;
@@ -1611,6 +1716,9 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
   tab.bpar = reinterpret_cast<uint16_t*>(base + L.off_bpar);
   tab.ovf = reinterpret_cast<unsigned long long*>(base + L.off_ovf);
+  tab.nleft = reinterpret_cast<unsigned long long*>(base + L.off_nleft);
+  tab.left = reinterpret_cast<unsigned long long*>(base + L.off_left);
+  tab.mode = kModeNormal;
   tab.kb = 1;
   while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
   auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
@@ -1629,12 +1737,6 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     if (int rc = probe_order(ctx, spans, tab.big + 3)) return rc;  // scratch: big counters' 4th word
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
-    const KernelFn fn = pick_kernel(E, want_compact(spans), use_unique(spans)).fn;
-    // As many workgroups as are resident at once (LDS / registers decide).
-    int per_cu = 0;
-    ANOMOD_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &per_cu, reinterpret_cast<const void*>(fn), kThreads, 0));
-    const uint64_t grid = (uint64_t)ctx->num_cus * (uint64_t)(per_cu > 0 ? per_cu : 1);
     // A workgroup's LDS counters (histogram slots, errors) are u32 and the
     // dynamic tail may hand one workgroup any share of a launch, so a launch
     // covers < 2^32 spans: larger sets run as several launches over whole
@@ -1642,13 +1744,24 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     std::vector<uint64_t> cuts;
     if (int rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts)) return rc;
     for (size_t k = 0; k + 1 < cuts.size(); ++k) {
-      if (k > 0) ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
+      if (k > 0) {
+        ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
+        if (autof) ANOMOD_HIP(ctx, hipMemsetAsync(tab.nleft, 0, 16, ctx->stream));
+      }
       Table tk = tab;
       tk.t_base = cuts[k];
-      hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, spans->span_id,
-                         spans->parent_span_id, spans->svc_flags, spans->dur_us,
+      tk.mode = autof ? kModeAuto : kModeNormal;
+      hipLaunchKernelGGL(pk.fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream,
+                         spans->span_id, spans->parent_span_id, spans->svc_flags, spans->dur_us,
                          spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
       ANOMOD_HIP(ctx, hipGetLastError());
+      if (autof) {  // returns at once when no workgroup stopped
+        tk.mode = kModeResume;
+        hipLaunchKernelGGL(pr.fn, dim3((unsigned)grid_r), dim3(kThreads), 0, ctx->stream,
+                           spans->span_id, spans->parent_span_id, spans->svc_flags, spans->dur_us,
+                           spans->trace_ptr + cuts[k], cuts[k + 1] - cuts[k], S, E, tk);
+        ANOMOD_HIP(ctx, hipGetLastError());
+      }
     }
     if (big_cap) ANOMOD_HIP(ctx, launch_big_for(ctx, spans, S, E, tab));
   }
@@ -1694,13 +1807,17 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   fan(out->max_us, L.off_mx, E * 4ull);
   fan(out->p50_us, L.off_p50, E * 8ull);
   fan(out->p99_us, L.off_p99, E * 8ull);
-  // More than 1/64 of the spans counted in HBM past a full pair table: the
-  // set touches more (edge, bin) keys than 8 Ki slots hold (e.g. random call
-  // trees over every service pair); its next aggregations use the compact
-  // form (same results, exact either way).
-  unsigned long long ovf = 0;
-  memcpy(&ovf, hs + (L.off_ovf - L.off_err), 8);
-  if (ovf * 64ull > spans->n_spans) spans->hist_compact = true;
+  // The set's form from here on: compact when a workgroup of a first
+  // aggregation stopped at a saturated pair table, or when more than 1/64 of
+  // the spans were counted in HBM past a full one (the set touches more (edge,
+  // bin) keys than 8 Ki slots hold, e.g. random call trees over every service
+  // pair); else pair.  Same results either way.
+  unsigned long long ovf[2] = {0ull, 0ull};
+  memcpy(ovf, hs + (L.off_ovf - L.off_err), 16);
+  if (pk.ht == kHtPair) {
+    if (ovf[1] > 0 || ovf[0] * 64ull > spans->n_spans) spans->hist_form = 1;
+    else if (spans->hist_form < 0) spans->hist_form = 0;
+  }
   return ANOMOD_OK;
 }
 
@@ -1717,6 +1834,10 @@ int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint
   ANOMOD_REQUIRE(ctx, spans->grouped, "span set is not grouped by trace: anomod_spans_group first");
   ANOMOD_REQUIRE(ctx, spans->n_spans == 0 || spans->max_svc < S,
                  "span service index %u >= n_services %u", spans->max_svc, S);
+  // one radix sort over every span's key (u32 tile offsets inside)
+  ANOMOD_REQUIRE(ctx, spans->n_spans <= kMaxSortKeys,
+                 "exact edge quantiles: %llu spans, at most 2^32 - 4097 per call",
+                 (unsigned long long)spans->n_spans);
   if (int rc = bind(ctx)) return rc;
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
   const uint64_t n = spans->n_spans;

@@ -710,6 +710,43 @@ int anomod_series_upload(anomod_ctx* ctx, anomod_series* ser, const float* X) {
   return ANOMOD_OK;
 }
 
+int anomod_series_download(anomod_ctx* ctx, const anomod_series* ser, float* X) {
+  ANOMOD_REQUIRE(nullptr, ctx && ser && X, "anomod_series_download: NULL argument");
+  if (int rc = bind(ctx)) return rc;
+  const uint64_t T = ser->T, S = ser->S;
+  if (!ser->tiled) {
+    ANOMOD_HIP(ctx, hipMemcpyAsync(X, ser->X, T * S * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return ANOMOD_OK;
+  }
+  // tiles -> rows on the device, up to ~256 MiB of rows (whole tiles) at a time
+  uint64_t R = ((256ull << 20) / (S * 4)) / kTile * kTile;
+  if (R < (uint64_t)kTile) R = kTile;
+  if (R > padded_steps(T)) R = padded_steps(T);
+  float* stage = nullptr;
+  if (hipMalloc(&stage, R * S * 4) != hipSuccess) {
+    set_error(ctx, "hipMalloc(%llu) for the download staging buffer failed",
+              (unsigned long long)(R * S * 4));
+    return ANOMOD_ENOMEM;
+  }
+  hipError_t e = hipSuccess;
+  for (uint64_t r0 = 0; r0 < T && e == hipSuccess; r0 += R) {
+    const uint64_t rows = T - r0 < R ? T - r0 : R;
+    hipLaunchKernelGGL(series_relayout_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
+                       ser->X, stage, T, S, r0, rows, 0);
+    e = hipGetLastError();
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(X + r0 * S, stage, rows * S * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  }
+  (void)hipFree(stage);
+  if (e != hipSuccess) {
+    set_error(ctx, "series download failed: %s", hipGetErrorString(e));
+    return ANOMOD_EHIP;
+  }
+  return ANOMOD_OK;
+}
+
 int anomod_series_fill_synthetic(anomod_ctx* ctx, anomod_series* ser, uint64_t seed,
                                  uint64_t t0) {
   ANOMOD_REQUIRE(nullptr, ctx && ser, "anomod_series_fill_synthetic: NULL argument");

@@ -911,9 +911,11 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
   if (rc != ANOMOD_OK) return comm_agree(ctx, rc);  // peers learn of it before their reduce
   anomod_spans view = view_of(spans, g);
-  view.hist_compact = spans->hist_compact;
+  view.hist_form = spans->hist_form;  // the set's hints: learned once, kept on the set
+  view.order = spans->order;
   const int rc2 = anomod_edge_aggregate_spans(ctx, &view, n_services, out);
-  spans->hist_compact = view.hist_compact;  // the set's histogram-form hint
+  spans->hist_form = view.hist_form;
+  spans->order = view.order;
   return rc2;
 }
 

@@ -711,14 +711,18 @@ int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t
   return ANOMOD_OK;
 }
 
-int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, uint64_t seed,
-                           anomod_graph** out) {
-  ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_graph_synthetic: NULL argument");
-  ANOMOD_REQUIRE(ctx, N >= 2 && mean_degree >= 1, "need N >= 2 and mean_degree >= 1");
-  // Power-law (Pareto, a = 2.2) out-degrees scaled to the requested mean,
-  // 2 % dangling nodes, uniform callees, call-count weights in [1, 1000].
-  std::vector<uint32_t> row_ptr(N + 1, 0), col;
-  std::vector<float> w;
+}  // extern "C"
+
+namespace {
+// The synthetic service/pod graph of SURVEY.md §8d config 5 (host side, so
+// the CPU baseline and the parity tests see the very graph the GPU solves):
+// power-law (Pareto, a = 2.2) out-degrees scaled to the requested mean, 2 %
+// dangling nodes, uniform callees, call-count weights in [1, 1000].
+void synthetic_csr(uint32_t N, uint32_t mean_degree, uint64_t seed, std::vector<uint32_t>& row_ptr,
+                   std::vector<uint32_t>& col, std::vector<float>& w) {
+  row_ptr.assign(N + 1, 0);
+  col.clear();
+  w.clear();
   uint64_t st = seed;
   auto next = [&]() { st += 0x9E3779B97F4A7C15ull; return splitmix64(st); };
   const double a = 2.2, xmin = mean_degree * (a - 2.0) / (a - 1.0);
@@ -735,7 +739,38 @@ int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, ui
     }
     row_ptr[u + 1] = (uint32_t)col.size();
   }
+}
+}  // namespace
+
+extern "C" {
+
+int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, uint64_t seed,
+                           anomod_graph** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_graph_synthetic: NULL argument");
+  ANOMOD_REQUIRE(ctx, N >= 2 && mean_degree >= 1, "need N >= 2 and mean_degree >= 1");
+  std::vector<uint32_t> row_ptr, col;
+  std::vector<float> w;
+  synthetic_csr(N, mean_degree, seed, row_ptr, col, w);
   return anomod_graph_create(ctx, row_ptr.data(), col.data(), w.data(), N, out);
+}
+
+int anomod_graph_synthetic_csr(uint32_t N, uint32_t mean_degree, uint64_t seed,
+                               uint32_t* row_ptr, uint32_t* col, float* w, uint64_t cap,
+                               uint64_t* nnz) {
+  ANOMOD_REQUIRE(nullptr, nnz, "anomod_graph_synthetic_csr: NULL nnz");
+  ANOMOD_REQUIRE(nullptr, N >= 2 && mean_degree >= 1, "need N >= 2 and mean_degree >= 1");
+  std::vector<uint32_t> rp, c;
+  std::vector<float> ww;
+  synthetic_csr(N, mean_degree, seed, rp, c, ww);
+  *nnz = c.size();
+  if (!row_ptr && !col && !w) return ANOMOD_OK;  // size query
+  ANOMOD_REQUIRE(nullptr, row_ptr && col && w, "anomod_graph_synthetic_csr: NULL output array");
+  ANOMOD_REQUIRE(nullptr, cap >= c.size(), "anomod_graph_synthetic_csr: cap %llu < nnz %llu",
+                 (unsigned long long)cap, (unsigned long long)c.size());
+  std::copy(rp.begin(), rp.end(), row_ptr);
+  std::copy(c.begin(), c.end(), col);
+  std::copy(ww.begin(), ww.end(), w);
+  return ANOMOD_OK;
 }
 
 int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz) {

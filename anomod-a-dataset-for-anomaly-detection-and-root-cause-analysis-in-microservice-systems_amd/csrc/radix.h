@@ -16,6 +16,10 @@ namespace anomod {
 // Device scratch bytes radix_sort_u64 needs for n keys.
 size_t radix_temp_bytes(uint64_t n);
 
+// Most keys one radix_sort_u64 call takes (its per-tile counts, scan sums
+// and scatter bases are u32): larger n returns hipErrorInvalidValue.
+constexpr uint64_t kMaxSortKeys = 0xFFFFFFFFull - 4096;
+
 // Stable LSD radix sort of n u64 keys by bits [begin_bit, end_bit) (keys must
 // be < 2^end_bit), 8-bit digits: per pass the digit counts of every
 // 4096-key tile, their exclusive scan over tiles, one scatter (wave-ballot

@@ -362,6 +362,8 @@ hipError_t radix_sort_u64(const uint64_t* in, uint64_t* out, uint64_t n, int beg
   if (passes) *passes = 0;
   if (temp_bytes < radix_temp_bytes(n) || begin_bit < 0 || end_bit > 64 || begin_bit > end_bit)
     return hipErrorInvalidValue;
+  // tile counts, scan sums and scatter bases are u32: n + one tile must fit
+  if (n > kMaxSortKeys) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   const uint64_t tiles = n_tiles(n), nb = (tiles + kScanRows - 1) / kScanRows;
   char* t = static_cast<char*>(temp);

@@ -161,7 +161,7 @@ int anomod_value_summary(anomod_ctx* ctx, const double* values, uint64_t n, int 
                          anomod_value_summary_out* out) {
   ANOMOD_REQUIRE(nullptr, ctx && out, "anomod_value_summary: NULL argument");
   ANOMOD_REQUIRE(ctx, n == 0 || values, "anomod_value_summary: NULL values");
-  ANOMOD_REQUIRE(ctx, n < (1ull << 62), "anomod_value_summary: n too large");
+  ANOMOD_REQUIRE(ctx, n <= kMaxSortKeys, "anomod_value_summary: at most 2^32 - 4097 values");
   if (int rc = bind(ctx)) return rc;
   *out = anomod_value_summary_out{};
   if (n == 0) return ANOMOD_OK;
@@ -186,7 +186,7 @@ int anomod_sort_u64(anomod_ctx* ctx, const uint64_t* keys, uint64_t n, int begin
   ANOMOD_REQUIRE(ctx, n == 0 || (keys && sorted), "anomod_sort_u64: NULL buffer");
   ANOMOD_REQUIRE(ctx, 0 <= begin_bit && begin_bit <= end_bit && end_bit <= 64,
                  "bit range [%d, %d) outside [0, 64]", begin_bit, end_bit);
-  ANOMOD_REQUIRE(ctx, n <= 0xFFFFFFFFull - 4096, "anomod_sort_u64: at most 2^32 - 4096 keys");
+  ANOMOD_REQUIRE(ctx, n <= kMaxSortKeys, "anomod_sort_u64: at most 2^32 - 4097 keys");
   if (passes) *passes = 0;
   if (n == 0) return ANOMOD_OK;
   if (int rc = bind(ctx)) return rc;

@@ -623,7 +623,24 @@ int anomod_spans_set_unique_ids(anomod_spans* spans, int unique) {
 
 int anomod_spans_hist_compact(const anomod_spans* spans, int* compact) {
   ANOMOD_REQUIRE(nullptr, spans && compact, "anomod_spans_hist_compact: NULL argument");
-  *compact = spans->hist_compact ? 1 : 0;
+  *compact = spans->hist_form == 1 ? 1 : 0;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_hints(const anomod_spans* spans, int* scan_order, int* hist_form) {
+  ANOMOD_REQUIRE(nullptr, spans && scan_order && hist_form, "anomod_spans_hints: NULL argument");
+  *scan_order = spans->order;
+  *hist_form = spans->hist_form;
+  return ANOMOD_OK;
+}
+
+int anomod_spans_set_hints(anomod_spans* spans, int scan_order, int hist_form) {
+  ANOMOD_REQUIRE(nullptr, spans, "anomod_spans_set_hints: NULL span set");
+  ANOMOD_REQUIRE(nullptr, scan_order >= -1 && scan_order <= 1 && hist_form >= -1 && hist_form <= 1,
+                 "anomod_spans_set_hints: scan_order=%d / hist_form=%d outside [-1, 1]", scan_order,
+                 hist_form);
+  spans->order = (int8_t)scan_order;
+  spans->hist_form = (int8_t)hist_form;
   return ANOMOD_OK;
 }
 

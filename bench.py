@@ -74,21 +74,9 @@ def _time_oracle(sample, S: int, threads: int, min_seconds: float) -> tuple[int,
     from oracle import native
 
     bounds = np.linspace(0, sample.n_traces, threads + 1).astype(np.int64)
-
-    def work(i):
-        native.edge_aggregate(sample, S, int(bounds[i]), int(bounds[i + 1]))
-
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            return passes, el
+    return _threads_run(
+        lambda i: native.edge_aggregate(sample, S, int(bounds[i]), int(bounds[i + 1])), threads,
+        min_seconds)
 
 
 def cpu_baseline(spec, n_traces: int, min_seconds: float) -> dict:
@@ -109,6 +97,98 @@ def cpu_baseline(spec, n_traces: int, min_seconds: float) -> dict:
             "sample": f"{sample.n_spans} synthetic SN spans ({n_traces} traces) x {passes} "
                       f"passes in {el:.1f} s, C oracle, {threads} threads (every usable core); "
                       f"single core: {p1} passes in {el1:.1f} s"}
+
+
+def _threads_run(fn, threads: int, min_seconds: float) -> tuple[int, float]:
+    """Rounds of fn(i) on `threads` threads (ctypes calls drop the GIL) until
+    min_seconds have elapsed -> (rounds, seconds)."""
+    rounds, t0 = 0, time.perf_counter()
+    while True:
+        ts = [threading.Thread(target=fn, args=(i,)) for i in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            return rounds, el
+
+
+def cpu_trace_structure(spec, n_traces: int, min_seconds: float) -> dict:
+    """C oracle trace structure (oracle_trace_structure) over a host sample of
+    the headline workload, one trace range per thread, every usable core."""
+    from oracle import native
+
+    sample = anomod.synth_generate_host(spec, n_traces)
+    threads = host_cores()["usable"]
+    bounds = np.linspace(0, sample.n_traces, threads + 1).astype(np.int64)
+    parts = [sample.select_traces((np.arange(sample.n_traces) >= bounds[i])
+                                  & (np.arange(sample.n_traces) < bounds[i + 1]))
+             for i in range(threads)]
+    native.trace_structure(parts[0])  # load
+    r, el = _threads_run(lambda i: native.trace_structure(parts[i]), threads, min_seconds)
+    return {"value": sample.n_spans * r / el, "unit": "spans/s", "cores": threads, "kind": "port",
+            "sample": f"{sample.n_spans} synthetic SN spans ({n_traces} traces) x {r} passes in "
+                      f"{el:.1f} s, C oracle_trace_structure, {threads} threads"}
+
+
+def cpu_group(spec, n_traces: int, min_seconds: float) -> dict:
+    """The oracle's grouping (oracle/spec.py group_by_trace: numpy stable
+    argsort of mix64(trace_hash)) + the gather of the 5 span columns, on an
+    interleaved host sample: the CPU side of the ungrouped leg's grouping."""
+    from oracle import spec as ospec
+
+    sample = anomod.synth_generate_host(spec, n_traces)
+    rng = np.random.default_rng(1)
+    perm = rng.permutation(sample.n_spans)
+    cols = {k: getattr(sample, k)[perm] for k in ("trace_hash", "span_id", "parent_span_id", "svc",
+                                                   "flags", "dur_us")}
+    r, t0 = 0, time.perf_counter()
+    while True:
+        order, _ = ospec.group_by_trace(cols["trace_hash"])
+        for v in cols.values():
+            v.take(order)
+        r += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    return {"value": sample.n_spans * r / el, "unit": "spans/s", "cores": 1, "kind": "port",
+            "sample": f"{sample.n_spans} interleaved synthetic SN spans x {r} groupings in "
+                      f"{el:.1f} s (numpy stable argsort of mix64 + column gathers, one core)"}
+
+
+def cpu_ewma(T: int, S_slice: int, W: int, min_seconds: float) -> dict:
+    """C oracle EWMA/z (oracle_ewma_z) on a [T][S_slice] slice of config 4's
+    series, one slice per thread: samples/s, scaled from the slice."""
+    from oracle import native
+
+    rng = np.random.default_rng(7)
+    X = (100.0 + 5.0 * rng.standard_normal((T, S_slice))).astype(np.float32)
+    threads = host_cores()["usable"]
+    native.ewma_z(X[:W], 2 / (W + 1), W)
+    r, el = _threads_run(lambda i: native.ewma_z(X, 2 / (W + 1), W), threads, min_seconds)
+    return {"value": T * S_slice * threads * r / el, "unit": "samples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"[{T}][{S_slice}] f32 slice of config 4 per thread x {r} rounds in {el:.1f} s, "
+                      f"C oracle_ewma_z (f64 state), {threads} threads; the GPU leg is S = 10^5 x "
+                      f"T ~ 10^6"}
+
+
+def cpu_pagerank(N: int, iters: int, seed: int, min_seconds: float) -> dict:
+    """C oracle PageRank (oracle_pagerank) on the very synthetic graph the GPU
+    leg solves (anomod.synth_graph_csr), one independent solve per thread
+    (the replica mode of the GPU leg): solved iterations/s."""
+    from oracle import native
+
+    rp, col, w = anomod.synth_graph_csr(N, 10, seed)
+    p = np.random.default_rng(0).random(N)
+    threads = host_cores()["usable"]
+    r, el = _threads_run(lambda i: native.pagerank(rp, col, w, p, iters=iters, tol=0.0), threads,
+                         min_seconds)
+    return {"value": iters * threads * r / el, "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": f"N = {N}, {col.shape[0]} edges, {iters}-iteration solves x {threads} "
+                      f"threads x {r} rounds in {el:.1f} s, C oracle_pagerank"}
 
 
 # Chaos targets of the TrainTicket runs (chaos-experiments/*.yaml target_service
@@ -218,8 +298,11 @@ def tt_config2_files(ctx, staged: list) -> dict:
 
 
 def edge_leg(ctx, spans, reps: int, what: str) -> dict:
-    """Edge-kernel time of a resident span set (hipEvents, ctx stream)."""
+    """Edge-kernel time of a resident span set (hipEvents, ctx stream); the
+    set's first aggregation (hints not learned yet) is reported as "cold"."""
+    t0 = time.perf_counter()
     ctx.edge_aggregate(spans, with_hist=False)
+    cold = {"kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG), "wall_ms": (time.perf_counter() - t0) * 1e3}
     ms = []
     for _ in range(reps):
         ctx.edge_aggregate(spans, with_hist=False)
@@ -228,7 +311,8 @@ def edge_leg(ctx, spans, reps: int, what: str) -> dict:
     b = algorithmic_bytes(spans.n_spans, spans.n_traces)
     return {"what": what, "spans": spans.n_spans, "traces": spans.n_traces, "kernel_ms": k,
             "spans_per_s": spans.n_spans / (k * 1e-3), "bytes_per_launch": b,
-            "achieved_GBps": b / (k * 1e-3) / 1e9, "frac": b / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            "achieved_GBps": b / (k * 1e-3) / 1e9, "frac": b / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "cold": cold}
 
 
 def group_bytes(info: dict, n: int, n_traces: int) -> int:
@@ -261,7 +345,10 @@ def group_bytes(info: dict, n: int, n_traces: int) -> int:
 def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
     """Grouping + edge aggregation of an ungrouped resident set (n_traces:
     the traces it holds, all non-empty)."""
+    t0 = time.perf_counter()
     ctx.edge_aggregate(inter, with_hist=False)
+    cold = {"wall_ms": (time.perf_counter() - t0) * 1e3, "group_ms": ctx.stage_ms(L.STAGE_GROUP),
+            "edge_ms": ctx.stage_ms(L.STAGE_EDGE_AGG)}
     g, e, wall = [], [], []
     for _ in range(3):
         t0 = time.perf_counter()
@@ -278,7 +365,12 @@ def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
             "spans_per_s": allsum(n / float(np.mean(wall))), "step_ms": float(np.mean(wall)) * 1e3,
             "group_ms": g_ms, "edge_ms": e_ms,
             "group_bytes": gbytes, "group_GBps": gbytes / (g_ms * 1e-3) / 1e9,
-            "group_frac": gbytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            "group_frac": gbytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            # against what grouping must move at least: read and write each
+            # 32-B span once (64 B/span); the whole step against its 32 B/span in
+            "group_algo_frac": 64 * n / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "step_algo_frac": 32 * n / (float(np.mean(wall))) / 1e9 / HBM_PEAK_GBPS,
+            "cold": cold}
 
 
 def load_traffic(n_spans: int) -> float | None:
@@ -303,6 +395,12 @@ def main() -> int:
     ap.add_argument("--cpu-traces", type=int, default=1 << 21)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--leg-cpu-seconds", type=float, default=6.0,
+                    help="CPU-baseline time per extra leg (trace structure, grouping, EWMA, "
+                         "PageRank)")
+    ap.add_argument("--host-comm", action="store_true",
+                    help="N > 1 rehearsal on one device: the ranks merge through libanomod's "
+                         "host collective transport over the HostGroup instead of RCCL")
     ap.add_argument("--no-extras", action="store_true", help="headline line only")
     ap.add_argument("--legs", default=",".join(LEGS),
                     help="extra legs to run (comma list of " + ", ".join(LEGS) + ")")
@@ -350,15 +448,24 @@ def main() -> int:
         staged = stage_tt_files(stage_root)
         t_stage = time.perf_counter() - t_stage
 
-    ctx = anomod.Context(local)
+    ctx = anomod.Context(0 if args.host_comm else local)
     if world > 1:
-        dist.attach_rccl(ctx, dist.RankInfo(rank, world, local), group)
+        if args.host_comm:  # ranks sharing one GPU (RCCL refuses): same calls, host transport
+            dist.attach_host(ctx, group)
+        else:
+            dist.attach_rccl(ctx, dist.RankInfo(rank, world, local), group)
+    cpu_legs = rank == 0 and world == 1 and not args.no_cpu_baseline
 
     spec = anomod.SynthSpec("SN", seed=args.seed, p_orphan_ppm=100)
     spans = ctx.generate(spec, args.traces_per_gpu, shard=rank)  # this rank's traces, in HBM
 
-    for _ in range(args.warmup):
+    cold = None
+    for w in range(args.warmup):
+        t0 = time.perf_counter()
         ctx.edge_aggregate(spans, with_hist=False)
+        if w == 0:  # the set's first aggregation: histogram form not known yet
+            cold = {"kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG),
+                    "wall_ms": (time.perf_counter() - t0) * 1e3}
     ctx.synchronize()
     barrier()
     ctx.synchronize()
@@ -405,7 +512,10 @@ def main() -> int:
             "kernel": "edge_agg_kernel<lds_hist,lds_stats>", "kernel_ms": k_ms,
             "bytes_per_launch": bytes_launch,
         },
+        "cold": cold,
     }
+    if world > 1:
+        result["transport"] = "host (HostGroup, one device)" if args.host_comm else "rccl"
     if "general_scan" in legs:
         # --- the same spans without the generator's unique-id declaration
         # (ANOMOD_UNIQUE_SCAN=0): the first-match forward parent scan every
@@ -430,6 +540,9 @@ def main() -> int:
             "spans_per_s": allsum(spans.n_spans / (t_ms * 1e-3)), "kernel_ms": t_ms,
             "bytes_per_launch": ts_bytes, "achieved_GBps": ts_bytes / (t_ms * 1e-3) / 1e9,
             "frac": ts_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        if cpu_legs:
+            result["trace_structure"]["cpu_baseline"] = cpu_trace_structure(
+                spec, 1 << 19, args.leg_cpu_seconds)
     if "exact_quantiles" in legs:
         # --- §8a a11 cross-check: exact per-edge order statistics (edge keys
         # + one radix sort) against the histogram quantiles of the headline
@@ -463,6 +576,8 @@ def main() -> int:
         inter = ctx.shuffle(spans, seed=args.seed + 2, window_traces=4096)
         result["ungrouped"] = ungrouped_leg(ctx, inter, spans.n_traces, allsum)
         inter.free()
+        if cpu_legs:
+            result["ungrouped"]["cpu_baseline"] = cpu_group(spec, 1 << 18, args.leg_cpu_seconds)
     spans.free()
     if "tt_width" in legs:
         # --- TrainTicket width (BASELINE config 2 topology, 46 services:
@@ -480,12 +595,32 @@ def main() -> int:
         result["long_traces"] = edge_leg(ctx, lt, 3, "edge kernel on LONG spans (traces of "
                                          "16..4000 spans; > 256 via the workgroup-per-trace pass)")
         lt.free()
+        # the product path's first call: a host LONG set uploaded per call
+        # (Context.edge_aggregate / features()); its learned hints stay on the
+        # host SpanSet, so the second call starts from them
+        lh = ctx.generate(anomod.SynthSpec("LONG", seed=args.seed + 3, p_orphan_ppm=100),
+                          1 << 20, shard=rank)
+        host = lh.download()
+        lh.free()
+        calls = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            ctx.edge_aggregate(host, with_hist=True)
+            calls.append({"wall_ms": (time.perf_counter() - t0) * 1e3,
+                          "kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG)})
+        result["long_traces"]["host_set_calls"] = {
+            "spans": host.n_spans, "what": "Context.edge_aggregate(host SpanSet): upload + "
+                                           "aggregate + download, first call then two more",
+            "calls": calls}
+        del host
 
     if "pagerank" in legs:
         # --- PageRank RCA: replicas (one graph + personalization per GPU)
         g = anomod.DeviceGraph(ctx, synthetic=(args.ppr_nodes, 10, 11 + rank))
         p = np.random.default_rng(rank).random(g.N)
+        t0 = time.perf_counter()
         g.pagerank(p, iters=args.ppr_iters)  # capture + warm
+        ppr_cold = (time.perf_counter() - t0) * 1e3
         reps = 10
         barrier()
         t0 = time.perf_counter()
@@ -497,12 +632,17 @@ def main() -> int:
         ppr_bytes = 4 * (g.N + 1) + 8 * g.nnz + 16 * g.N  # in_ptr + (col,w) + x gather/write
         result["pagerank"] = {
             "iters_per_s": world * reps * args.ppr_iters / pel,
+            "cold_solve_ms": None,
             "device_iters_per_s_per_gpu": args.ppr_iters / (np.mean(pr_ms) * 1e-3),
             "nodes": g.N, "edges": g.nnz, "iters_per_solve": args.ppr_iters,
             "mode": "replicas (independent personalization per GPU, no collective)",
             "bytes_per_iter": ppr_bytes,
             "achieved_GBps": ppr_bytes * args.ppr_iters / (np.mean(pr_ms) * 1e-3) / 1e9,
         }
+        result["pagerank"]["cold_solve_ms"] = ppr_cold
+        if cpu_legs:
+            result["pagerank"]["cpu_baseline"] = cpu_pagerank(args.ppr_nodes, args.ppr_iters, 11,
+                                                              args.leg_cpu_seconds)
         # row-sharded solve (SURVEY §8e "sharded" series): one vector over all
         # ranks, whole 256-row blocks per rank, one grouped RCCL exchange per
         # iteration (u64 partial sums + in-place all-gather of x); at N=1 the
@@ -544,7 +684,10 @@ def main() -> int:
         W = 60
         ser = anomod.DeviceSeries(ctx, args.ewma_steps, args.ewma_series)
         ser.fill_synthetic(7 + rank, 0)
+        t0 = time.perf_counter()
         ser.ewma_z(2 / (W + 1), W, download=False)  # warm
+        ew_cold = {"wall_ms": (time.perf_counter() - t0) * 1e3,
+                   "kernel_ms": ctx.stage_ms(L.STAGE_EWMA)}
         ser.reset_state()
         ew = []
         for c in range(args.ewma_chunks):
@@ -563,8 +706,12 @@ def main() -> int:
             "achieved_GBps": e_bytes / (e_ms * 1e-3) / 1e9,
             "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "note": "config 4 at size: chunks generated in HBM outside the timing, state carried",
+            "cold_chunk": ew_cold,
         }
         ser.free()
+        if cpu_legs:
+            result["ewma"]["cpu_baseline"] = cpu_ewma(args.ewma_steps // 8 // W * W, 1000, W,
+                                                      args.leg_cpu_seconds)
 
     if "tt_config2" in legs and world == 1:
         result["tt_config2"] = tt_config2(ctx)
@@ -575,7 +722,7 @@ def main() -> int:
 
         shutil.rmtree(stage_root, ignore_errors=True)
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if cpu_legs:
         result["cpu_baseline"] = cpu_baseline(spec, args.cpu_traces, args.cpu_seconds)
 
     ctx.close()

@@ -147,6 +147,15 @@ int anomod_spans_scan_order(const anomod_spans* spans, int* order);
  * (pair-form) LDS histogram: its later aggregations use the 16 Ki packed-slot
  * (compact) form (same results; a performance hint the library keeps).     */
 int anomod_spans_hist_compact(const anomod_spans* spans, int* compact);
+/* Both hints of a set, for callers that keep a span set on the host and
+ * upload it per call (the Python SpanSet does): *scan_order as
+ * anomod_spans_scan_order; *hist_form 0 = pair, 1 = compact, -1 = not known
+ * yet (the aggregation starts in the pair form and a workgroup whose table
+ * saturates hands its remaining traces to a compact-form launch — no
+ * first-call cliff either way).  set_hints puts learned values on a freshly
+ * uploaded set (each in [-1, 1]); results never depend on them.           */
+int anomod_spans_hints(const anomod_spans* spans, int* scan_order, int* hist_form);
+int anomod_spans_set_hints(anomod_spans* spans, int scan_order, int hist_form);
 /* Copy a host span set to HBM.  Replaces the in-memory hand-off between
  * json.load and the per-span loop of jaeger_to_csv.py:12-32 /
  * trace_collector.py:519-531.                                              */
@@ -232,6 +241,10 @@ int anomod_decode_skywalking(const char* json, uint64_t len, const char* const* 
                              uint32_t n_services, anomod_decoded** out);
 int anomod_decoded_info(const anomod_decoded* d, uint64_t* n_spans, uint64_t* n_traces,
                         uint32_t* n_services);
+/* *unique = 1 when no trace of the document holds a span id twice (checked
+ * exactly while decoding: Jaeger spanIDs after their id mapping, SkyWalking
+ * node ids), else 0 — what anomod_spans_set_unique_ids takes.              */
+int anomod_decoded_unique_ids(const anomod_decoded* d, int* unique);
 const char* anomod_decoded_service(const anomod_decoded* d, uint32_t i);
 int anomod_decoded_columns(const anomod_decoded* d, const anomod_span_soa_out* dst,
                            uint64_t* trace_ptr /* [n_traces + 1] */);
@@ -291,7 +304,8 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
  * q_pct[k] / 100.0 and the product truncated — the reference's
  * sorted(x)[int(n*q)] for any q_pct (monitor_http_responses.py:180-190).
  * out: [E][nq] doubles (NaN for an empty edge); count: [E] (may be NULL).
- * Needs a grouped set; q_pct[k] in [0, 99], nq <= 16.                       */
+ * Needs a grouped set of at most 2^32 - 4097 spans (one sort); q_pct[k] in
+ * [0, 99], nq <= 16.                                                        */
 int anomod_edge_quantiles_exact(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
                                 const uint32_t* q_pct, uint32_t nq, double* out, uint64_t* count);
 /* One-shot host convenience: upload + aggregate + download.               */
@@ -370,7 +384,8 @@ int anomod_segment_summary(anomod_ctx* ctx, const uint32_t* svc, const uint32_t*
  *   min = x[0], max = x[c-1], median = x[c//2],
  *   p95 = x[int(c*0.95)], p99 = x[int(c*0.99)]   (f64 product, truncated)
  * exactly, and sum over the sorted values (fixed tree order: reproducible,
- * within c*2^-53 relative of Python's left-to-right sum).  All 0 when c = 0. */
+ * within c*2^-53 relative of Python's left-to-right sum).  All 0 when c = 0.
+ * n <= 2^32 - 4097 (the sort's limit).                                     */
 typedef struct {
   uint64_t count;             /* out: values selected                      */
   double min, max, sum;       /* out                                       */
@@ -383,7 +398,7 @@ int anomod_value_summary(anomod_ctx* ctx, const double* values, uint64_t n, int 
  * keys by bits [begin_bit, end_bit) (every key < 2^end_bit), hand-written
  * for CDNA4 (csrc/radix.hip).  Host buffers in and out (may alias);
  * *passes (may be NULL) = 8-bit digit passes run (digits equal in every key
- * are skipped).                                                            */
+ * are skipped).  n <= 2^32 - 4097 (u32 tile offsets).                      */
 int anomod_sort_u64(anomod_ctx* ctx, const uint64_t* keys, uint64_t n, int begin_bit,
                     int end_bit, uint64_t* sorted, int* passes);
 /* generate_summary's distributions in the same pass: status_id / ctype_id
@@ -426,6 +441,8 @@ int anomod_series_upload(anomod_ctx* ctx, anomod_series* ser, const float* X);
 int anomod_series_fill_synthetic(anomod_ctx* ctx, anomod_series* ser, uint64_t seed,
                                  uint64_t t0);
 int anomod_series_reset_state(anomod_ctx* ctx, anomod_series* ser);
+/* The resident matrix back as host rows X[T][S] (whatever the device layout). */
+int anomod_series_download(anomod_ctx* ctx, const anomod_series* ser, float* X);
 int anomod_series_ewma_z(anomod_ctx* ctx, anomod_series* ser, float alpha, uint32_t W,
                          float eps, float* Z_host /* may be NULL */);
 int anomod_series_free(anomod_series* ser);
@@ -445,6 +462,12 @@ int anomod_graph_create(anomod_ctx* ctx, const uint32_t* row_ptr, const uint32_t
                         const float* w, uint32_t N, anomod_graph** out);
 int anomod_graph_synthetic(anomod_ctx* ctx, uint32_t N, uint32_t mean_degree, uint64_t seed,
                            anomod_graph** out);
+/* The same synthetic graph as host CSR (config 5: Pareto out-degrees of the
+ * given mean, 2 % dangling, call-count weights): *nnz always; with every
+ * array NULL a size query, else row_ptr [N + 1], col / w [cap >= nnz].     */
+int anomod_graph_synthetic_csr(uint32_t N, uint32_t mean_degree, uint64_t seed,
+                               uint32_t* row_ptr, uint32_t* col, float* w, uint64_t cap,
+                               uint64_t* nnz);
 int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz);
 int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
                           uint32_t iters, double tol, double* x_out, uint32_t* iters_done);

@@ -115,3 +115,47 @@ def test_import_without_torch():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "False"
+
+
+def test_rendezvous_survives_stray_clients(tmp_path):
+    """Rank 0 drops clients that close at once, send garbage or a bad hello
+    (a stale rank of an earlier run) instead of aborting the rendezvous; the
+    real ranks still form the group (threads of one process here)."""
+    import json as _json
+    import socket
+    import struct
+    import threading
+    import time
+
+    from anomod import dist
+
+    key, res, errs = f"stray{os.getpid()}", {}, []
+
+    def rank(r):
+        try:
+            with dist.HostGroup(r, 2, key=key, rdzv_dir=str(tmp_path), timeout_s=30) as g:
+                res[r] = g.allreduce_scalar(r + 1.0)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    t0 = threading.Thread(target=rank, args=(0,))
+    t0.start()
+    path = tmp_path / f"anomod-rdzv-{key}.json"
+    deadline = time.monotonic() + 20
+    while not path.exists() and time.monotonic() < deadline:
+        time.sleep(0.02)
+    info = _json.loads(path.read_text())
+    addr = (info["addr"], info["port"])
+    socket.create_connection(addr).close()                      # closes at once
+    s = socket.create_connection(addr)
+    s.sendall(struct.pack("<Q", 3) + b"xyz")                    # too short a hello
+    s.close()
+    s = socket.create_connection(addr)
+    s.sendall(struct.pack("<Q", 12) + b"ANMD" + struct.pack("<ii", 5, 9))  # stale world
+    t1 = threading.Thread(target=rank, args=(1,))
+    t1.start()
+    t0.join(60)
+    t1.join(60)
+    s.close()
+    assert not errs, errs
+    assert res == {0: 3.0, 1: 3.0}

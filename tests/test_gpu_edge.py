@@ -279,12 +279,14 @@ def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
         np.testing.assert_array_equal(tab[qq][ok], [0.5 * (lo + hi) for lo, hi in b])
 
 
-@pytest.mark.parametrize("form", ["pair", "compact"])
+@pytest.mark.parametrize("form", ["pair", "compact", "auto"])
 @pytest.mark.parametrize("S", [14, 46])
 def test_histogram_forms(ctx, monkeypatch, form, S):
     """Both LDS histogram forms of the SN-width (E <= 512, direct stats) and
-    TrainTicket-width (E <= 2304, wide stats) kernels give the oracle's table
-    bit for bit (ANOMOD_HIST_FORM forces one)."""
+    TrainTicket-width (E <= 2304, wide stats) kernels, and the form-unknown
+    first aggregation (pair form; saturated workgroups hand their traces to a
+    compact resume launch), give the oracle's table bit for bit
+    (ANOMOD_HIST_FORM forces each)."""
     monkeypatch.setenv("ANOMOD_HIST_FORM", form)
     rng = np.random.default_rng(61 + S)
     sp = _random_spanset(rng, S, 30000, 40, dup=0.01)
@@ -298,18 +300,54 @@ def test_histogram_forms(ctx, monkeypatch, form, S):
 def test_pair_table_overflow_switches_form(ctx):
     """A device set touching far more (edge, bin) keys per workgroup than the
     pair table's 8 Ki slots (random call trees over 20 services, latencies
-    over the whole u32 range) overflows it on the first aggregation; later
-    aggregations of the same set take the compact form.  Every result equals
-    the oracle's."""
+    over the whole u32 range) saturates it on the first aggregation — whose
+    stopped workgroups hand their traces to the compact resume launch — and
+    later aggregations take the compact form at once.  Every result, the
+    first included, equals the oracle's."""
     rng = np.random.default_rng(62)
     sp = _random_spanset(rng, 20, 700_000, 40)
     ref = native.edge_aggregate(sp)
     dev = ctx.upload(sp)
-    assert not dev.hist_compact
+    assert not dev.hist_compact and dev.hints == (-1, -1)
     for _ in range(3):
         assert_table_equal(ctx.edge_aggregate(dev), ref)
-        assert dev.hist_compact
+        assert dev.hist_compact and dev.hints[1] == 1
     dev.free()
+
+
+def test_first_aggregation_has_no_cliff(ctx):
+    """The first aggregation of a fresh LONG set (random call trees over every
+    SN service pair: ~15 k (edge, bin) keys per workgroup, twice what the pair
+    table holds) costs about what the later ones do (r03: 140x, the probe
+    chains and contended HBM counters of a saturated pair table), equals the
+    oracle, and a host SpanSet keeps the learned form across uploads."""
+    dev = ctx.generate(anomod.SynthSpec("LONG", seed=9), 1 << 20)
+    host = dev.download()
+    assert host.hist_form == -1
+    ref = native.edge_aggregate(host)
+    ms = []
+    for _ in range(3):
+        assert_table_equal(ctx.edge_aggregate(dev), ref)
+        ms.append(ctx.stage_ms(0))
+    assert dev.hints[1] == 1
+    assert ms[0] <= 3.0 * max(ms[1:]) + 0.5, ms
+    dev.free()
+    assert_table_equal(ctx.edge_aggregate(host), ref)  # uploaded per call
+    assert host.hist_form == 1 and host.scan_order == 1
+
+
+@pytest.mark.parametrize("cap", [3000, 50000])
+def test_first_aggregation_multi_launch(ctx, monkeypatch, cap):
+    """The saturation hand-off per launch of a multi-launch split (every
+    launch's stopped workgroups resume in compact form before the next
+    launch re-zeroes the counters)."""
+    rng = np.random.default_rng(cap + 1)
+    sp = anomod.SpanSet.concat([_random_spanset(rng, 20, 100_000, 40),
+                                _random_spanset(rng, 20, 2, 4000)])
+    ref = native.edge_aggregate(sp)
+    monkeypatch.setenv("ANOMOD_MAX_LAUNCH_SPANS", str(cap))
+    monkeypatch.setenv("ANOMOD_HIST_FORM", "auto")
+    assert_table_equal(ctx.edge_aggregate(sp), ref)
 
 
 @pytest.mark.parametrize("S,max_len", [(12, 24), (46, 80), (5, 256)])

@@ -121,3 +121,47 @@ def test_two_ranks_host_transport(tmp_path):
         assert r["ppr_eq_37"] == 1 and r["ppr_eq_1000"] == 1
     assert "n_services" in str(r1["agree_err"])     # the failing rank's own reason
     assert str(r0["agree_err"]) != ""                 # its peer failed with it
+
+
+def test_bench_two_ranks_host_comm(tmp_path):
+    """bench.py's N > 1 code — HostGroup rendezvous, per-step edge-table
+    merge, barriers, allmax / allsum weak-scaling accounting — run for real
+    at world 2 on one MI355X through the host transport (--host-comm; RCCL
+    refuses two ranks on a device).  bench.py itself asserts the merged
+    count.sum() equals the spans of both shards."""
+    import json
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r), ANOMOD_RDZV_DIR=str(tmp_path))
+        procs.append(subprocess.Popen(
+            [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--host-comm", "--steps", "3",
+             "--warmup", "1", "--traces-per-gpu", "30000", "--legs", "pagerank,ungrouped",
+             "--ppr-nodes", "20000", "--ppr-iters", "20", "--no-cpu-baseline"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=100)
+            outs.append((o.decode(errors="replace"), e.decode(errors="replace")))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                if q.poll() is None:
+                    os.killpg(q.pid, 9)
+            pytest.fail("two-rank bench run timed out")
+    assert all(p.returncode == 0 for p in procs), outs
+    line = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert outs[1][0].strip() == ""  # only rank 0 prints
+    assert line["n_gpus"] == 2 and line["transport"].startswith("host")
+    n0 = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100),
+                                    30000, shard=0).n_spans
+    n1 = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100),
+                                    30000, shard=1).n_spans
+    assert line["config"]["spans_per_gpu"] == n0
+    assert line["value"] == pytest.approx((n0 + n1) * 3 / (line["ms_per_step"] * 3e-3))
+    assert line["ungrouped"]["spans"] == n0
+    assert line["pagerank"]["sharded"]["shards"] == 2

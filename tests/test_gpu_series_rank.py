@@ -124,6 +124,33 @@ def test_ewma_synthetic_fill_same_in_both_layouts(ctx, monkeypatch):
     np.testing.assert_array_equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("mode", ["1", "0"])
+def test_ewma_config4_width_matches_oracle(ctx, monkeypatch, mode):
+    """BASELINE config 4's width, S = 10^5 series (the bench's tiled layout
+    and grid: ANOMOD_EWMA_MODE=1, and whatever auto picks), generated in HBM
+    by fill_synthetic (level shifts included), T = 240 steps from t0 = 10^6
+    - 120: the z scores equal the C oracle's on the downloaded matrix."""
+    monkeypatch.setenv("ANOMOD_EWMA_MODE", mode)
+    T, S, W = 240, 100_000, 60
+    ser = anomod.DeviceSeries(ctx, T, S)
+    ser.fill_synthetic(7, t0=1_000_000 - 120)
+    Z = ser.ewma_z(2 / (W + 1), W)
+    X = ser.download()
+    ser.free()
+    assert np.isfinite(X).all()
+    np.testing.assert_allclose(Z, native.ewma_z(X, 2 / (W + 1), W), rtol=Z_RTOL, atol=Z_ATOL)
+
+
+def test_series_download_roundtrip(ctx, ewma_mode):
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((100, 333)).astype(np.float32)
+    ser = anomod.DeviceSeries(ctx, 100, 333)
+    ser.upload(X)
+    ser.ewma_z(0.2, 10)  # may re-lay the matrix out for the mode's kernel
+    np.testing.assert_array_equal(ser.download(), X)
+    ser.free()
+
+
 def test_ewma_dense_blocks_equal_general_step(ctx, monkeypatch):
     """The tiled kernel takes a select-free step for 64-step blocks in which
     every lane of the wave has started and no sample is NaN.  Waves that are
@@ -171,6 +198,22 @@ def test_pagerank_fixed_iters_matches_oracle(ctx):
         xr, itr = native.pagerank(row_ptr, col, w, p, 0.85, iters=iters, tol=0.0)
         assert it == itr == iters
         assert np.abs(x - xr).sum() < 1e-5
+
+
+def test_pagerank_config5_graph_matches_oracle(ctx):
+    """BASELINE config 5 at size: the synthetic 10^5-node graph the bench
+    solves (DeviceGraph(synthetic=...)), 100 fixed iterations and a
+    tolerance solve, against the C oracle on the same CSR from the host."""
+    g = anomod.DeviceGraph(ctx, synthetic=(100_000, 10, 11))
+    rp, col, w = anomod.synth_graph_csr(100_000, 10, 11)
+    assert g.nnz == col.shape[0]
+    p = np.random.default_rng(0).random(g.N)
+    for iters, tol in ((100, 0.0), (1000, 1e-10)):
+        x, it = g.pagerank(p, iters=iters, tol=tol)
+        xr, itr = native.pagerank(rp, col, w, p, 0.85, iters=iters, tol=tol)
+        assert abs(it - itr) <= (0 if tol == 0.0 else 1)  # L1 test: fixed-point vs f64 sums
+        assert np.abs(x - xr).sum() < 1e-5
+    g.free()
 
 
 def test_device_graph_replay(ctx):

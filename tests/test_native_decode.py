@@ -18,6 +18,23 @@ def _same(a, b):
     assert a.services == b.services
     for k in COLS:
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    # the native decoder's own per-trace id check == the exact host check
+    assert a.unique_ids == b.check_unique_ids()
+
+
+def test_decoder_unique_ids_flag():
+    """anomod_decoded_unique_ids: 1 for a payload whose node ids are unique in
+    every trace (a synthetic collector payload), 0 once one trace repeats a
+    node id; the same as SpanSet.check_unique_ids on the decoded columns."""
+    from anomod import writers
+
+    sp = anomod.synth_generate_host(anomod.SynthSpec("TT", seed=3), 40)
+    doc = writers.skywalking_payload(sp, "u")
+    got = anomod.decode_native(json.dumps(doc).encode(), "skywalking")
+    assert got.unique_ids and got.check_unique_ids()
+    doc["traces"][7]["spans"][3]["node_id"] = doc["traces"][7]["spans"][1]["node_id"]
+    got = anomod.decode_native(json.dumps(doc).encode(), "skywalking")
+    assert not got.unique_ids and not got.check_unique_ids()
 
 
 def test_hash64_matches_python():
