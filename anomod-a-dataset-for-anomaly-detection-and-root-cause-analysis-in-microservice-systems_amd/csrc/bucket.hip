@@ -1,22 +1,34 @@
-// Trace grouping, bucket path: two stable MSD scatter levels over the top T
-// bits of k = mix64(trace_hash), then one workgroup per bucket of ~1000 spans
-// that puts the bucket in (k, arrival) order inside LDS and writes the grouped
-// SoA columns and its trace starts.  Same output as the LSD path of group.hip
-// (traces by k ascending, spans of a trace in arrival order — the order the
-// reference's first-match parent rule sees, trace_collector.py:424-443), with
-// fewer bytes moved: 2 record scatters + 1 record pass instead of
-// ceil(log2(n)/8) scatters + bucket fix-up + trace_ptr scan.
+// Trace grouping, bucket path: a stable MSD scatter of the 32-B records over
+// the top DA bits of k = mix64(trace_hash), a second level over 8-B PAIRS
+// (the next 32 key bits << 32 | the record's position), then one workgroup
+// per bucket of ~1000 spans that sorts the bucket's pairs in LDS, gathers
+// each record by its position from the level-A output and writes the grouped
+// SoA columns and the bucket's trace starts.  Same output as the LSD path of
+// group.hip (traces by k ascending, spans of a trace in arrival order — the
+// order the reference's first-match parent rule sees,
+// trace_collector.py:424-443).
 //
 // Per span (n = 1.15e9: T = 20, DA = 9, DB = 11):
-//   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 2 (next digits out)
-//   level B: 2 (count: digits) + 32 + 32
-//   buckets: 32 (records in) + 32 (SoA columns out) + 24/trace (trace starts, trace_ptr)
-// + tile counts (4 B per tile and digit, five touches: ~15 B/span) ≈ 220 B/span,
-// against 286 B/span for the LSD path.
+//   level A: 8 (count: trace_hash) + 32 (SoA in) + 32 (records out) + 8 (pairs out)
+//   level B: 8 (count: pairs) + 8 + 8 (pairs in, out)
+//   buckets: 8 (pairs) + 32 (records gathered: the buckets in flight lie in one
+//            ~72 MB level-A bucket, so the gathers hit the Infinity Cache) +
+//            32 (SoA columns out) + 24/trace (trace starts, trace_ptr)
+// + tile counts (4 B per tile and digit, five touches) ≈ 180 B/span, against
+// ~220 B/span when level B moved the 32-B records (r03) and 286 B/span for
+// the LSD path.
+//
+// Pairs sort exactly: a pair's value orders by (key bits, position), and
+// positions inside a level-A bucket are arrival order (level A is stable), so
+// sorting a bucket's pairs as u64 gives (k, arrival) order — unless two
+// traces of a bucket share all T + 32 key bits the pairs see.  The bucket
+// kernel checks the gathered records' full keys and re-ranks such a bucket by
+// (k, arrival) (rare: ~1e-6 of the buckets at 1.2e8 traces; crafted hashes
+// in the tests).
 //
 // A bucket larger than the small kernel's 2048 spans (a long trace, or the
 // tail of the size distribution) goes to a list that a 1024-thread kernel
-// works through: up to 8192 spans with its keys in LDS, beyond that by a
+// works through: up to 8192 spans with its pairs in LDS, beyond that by a
 // one-wave walk over the bucket's distinct keys (bucket_huge).  Only a huge
 // bucket with more distinct keys than that walk holds (adversarial hashes)
 // makes the caller regroup with the LSD path.
@@ -32,10 +44,9 @@ namespace {
 
 using chunk::wave_sync;
 // Experiment-only builds (never set in the shipped library):
-//  1 = level B counts its digits from the level-A records (no 2-B digit array);
 //  2 = level A stores nothing, then the LSD path groups (timing of level A's
 //      loads and ranking only);
-//  4 = nontemporal record stores in the scatter levels.
+//  4 = nontemporal record stores in level A.
 
 
 #ifndef ANOMOD_BK_ABL
@@ -45,7 +56,9 @@ constexpr int kWv = 64;
 constexpr int kBThreads = 1024;                // scatter workgroup
 constexpr int kBWaves = kBThreads / kWv;       // 16
 constexpr int kBPer = 4;                       // records per thread
-constexpr int kBTile = kBThreads * kBPer;      // 4096 records per tile
+constexpr int kBTile = kBThreads * kBPer;      // 4096 records per level-A tile
+constexpr int kPPer = 16;                      // pairs per thread (level B)
+constexpr int kPTile = kBThreads * kPPer;      // 16384 pairs per level-B tile (128 KiB)
 constexpr int kDMax = 11;                      // digit bits per scatter level
 constexpr int kNDMax = 1 << kDMax;
 constexpr int kScanRows = 256;                 // tiles per block of the tile scan
@@ -119,7 +132,8 @@ __global__ __launch_bounds__(256) void bk_scan_up_kernel(const uint32_t* __restr
 __global__ __launch_bounds__(1024) void bk_scan_top_kernel(uint32_t* __restrict__ bsum,
                                                            uint64_t nbk, int nd, uint64_t n,
                                                            uint32_t* __restrict__ bsA,
-                                                           uint32_t* __restrict__ btile) {
+                                                           uint32_t* __restrict__ btile,
+                                                           uint32_t tile_b) {
   __shared__ uint32_t wsum[16];
   const int tid = threadIdx.x;
   const int dpt = nd > 1024 ? nd / 1024 : 1;  // consecutive digits per thread (nd <= 2048)
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(1024) void bk_scan_top_kernel(uint32_t* __restrict_
         }
     }
     tot[i] = run;
-    til[i] = (run + kBTile - 1) / kBTile;
+    til[i] = (run + tile_b - 1) / tile_b;
   }
   uint32_t all, allt;
   const uint32_t pre = block_excl_scan<16>(tot[0] + tot[1], wsum, &all);
@@ -189,20 +203,23 @@ __global__ __launch_bounds__(256) void bk_tilemap_kernel(const uint32_t* __restr
   for (uint32_t t = btile[b] + threadIdx.x; t < btile[b + 1]; t += 256) tmap[t] = b;
 }
 
+// Level-B tile t (kPTile pairs, never straddling a level-A bucket).
 __device__ inline bool seg_tile(uint64_t t, const uint32_t* __restrict__ bsA,
                                 const uint32_t* __restrict__ btile,
                                 const uint32_t* __restrict__ tmap, int na, uint64_t* base,
                                 uint64_t* nvalid) {
   if (t >= btile[na]) return false;
   const uint32_t b = tmap[t];
-  const uint64_t a = (uint64_t)bsA[b] + (t - btile[b]) * (uint64_t)kBTile;
-  const uint64_t e = a + kBTile < (uint64_t)bsA[b + 1] ? a + kBTile : (uint64_t)bsA[b + 1];
+  const uint64_t a = (uint64_t)bsA[b] + (t - btile[b]) * (uint64_t)kPTile;
+  const uint64_t e = a + kPTile < (uint64_t)bsA[b + 1] ? a + kPTile : (uint64_t)bsA[b + 1];
   *base = a;
   *nvalid = e - a;
   return true;
 }
 
-__global__ __launch_bounds__(256) void bk_count_b_kernel(const uint16_t* __restrict__ dn,
+// Per level-B tile: counts of the pairs' top db bits (the key bits right
+// below level A's).
+__global__ __launch_bounds__(256) void bk_count_b_kernel(const uint64_t* __restrict__ pr,
                                                          const uint32_t* __restrict__ bsA,
                                                          const uint32_t* __restrict__ btile,
                                                          const uint32_t* __restrict__ tmap,
@@ -211,18 +228,11 @@ __global__ __launch_bounds__(256) void bk_count_b_kernel(const uint16_t* __restr
   __shared__ uint32_t lh[kNDMax];
   uint64_t base, nvalid;
   if (!seg_tile(blockIdx.x, bsA, btile, tmap, na, &base, &nvalid)) return;
-  const int nd = 1 << db, tid = threadIdx.x;
+  const int nd = 1 << db, tid = threadIdx.x, sh = 64 - db;
   for (int i = tid; i < nd; i += 256) lh[i] = 0u;
   __syncthreads();
-#if ANOMOD_BK_ABL & 1
-  const GRec* rec = reinterpret_cast<const GRec*>(dn);
-  const int sh = 64 - db - (int)__builtin_ctz((unsigned)na);
-  for (uint64_t p = tid; p < nvalid; p += 256)
-    atomicAdd(&lh[(uint32_t)(mix64(rec[base + p].h) >> sh) & (uint32_t)(nd - 1)], 1u);
-#else
-  const int dsh = kDMax - db;  // dn holds the kDMax bits below level A's
-  for (uint64_t p = tid; p < nvalid; p += 256) atomicAdd(&lh[dn[base + p] >> dsh], 1u);
-#endif
+#pragma unroll 4
+  for (uint64_t p = tid; p < nvalid; p += 256) atomicAdd(&lh[(uint32_t)(pr[base + p] >> sh)], 1u);
   __syncthreads();
   for (int i = tid; i < nd; i += 256) tcnt[(uint64_t)blockIdx.x * nd + i] = lh[i];
 }
@@ -280,19 +290,18 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
   if (b == (uint32_t)na - 1 && tid == 0) bstart[(uint64_t)na * nd] = bsA[na];
 }
 
-// ---- one stable scatter level ------------------------------------------------
+// ---- level A: one stable scatter of the records ------------------------------
 // Tile = 4096 records (1024 threads x 4; wave w owns positions [256w, 256w +
-// 256)), ranked with wave ballots (dbits ballots give each lane its
-// same-digit peers; a per-wave LDS counter per digit carries the count down
-// the wave's rows), staged whole in LDS in digit order — over the per-wave
-// counters, which are dead by then — and written as 16-B chunks, a wave
-// instruction covering 32 consecutive staged records (1 KiB, runs of ~4-8
-// records to one place each at 9-10 digit bits).  Level A reads the SoA
-// columns and writes every record's level-B digit beside it.
+// 256)), ranked with wave ballots (da ballots give each lane its same-digit
+// peers; a per-wave LDS counter per digit carries the count down the wave's
+// rows), staged whole in LDS in digit order — over the per-wave counters,
+// which are dead by then — and written as 16-B chunks, a wave instruction
+// covering 32 consecutive staged records (1 KiB, runs of ~8 records to one
+// place each at 9 digit bits).  Beside every record goes its pair for level B
+// and the buckets: the next 32 key bits << 32 | the record's position.
 // (Measured at 2^25 SN traces, 9-bit levels: half-record staging with one
-// 16-B store per lane and record half 9.2 / 6.0 ms for levels A / B; whole
-// records 6.0 / 5.4; no stores at all 1.0 ms — the scattered writes are the
-// cost.)
+// 16-B store per lane and record half 9.2 ms; whole records 6.0; no stores at
+// all 1.0 ms — the scattered writes are the cost.)
 //
 // Workgroups are dispatched to the 8 XCDs round-robin by block index, so
 // consecutive blocks would write the two ends of a shared 128-B line from two
@@ -306,13 +315,16 @@ __device__ inline uint64_t xcd_tile(uint64_t b, uint64_t g, uint32_t nx) {
   return x * q + (x < r ? x : r) + s;
 }
 
-template <bool SOA_IN, bool SEG, bool DNEXT>
-__global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
-    SoaIn sin, const GRec* __restrict__ ain, GRec* __restrict__ aout, uint64_t n, int shift,
-    int dbits, const uint32_t* __restrict__ toff, uint16_t* __restrict__ dnext, int nshift,
-    uint32_t nmask, const uint32_t* __restrict__ bsA, const uint32_t* __restrict__ btile,
-    const uint32_t* __restrict__ tmap, int na, uint32_t nx) {
-  constexpr bool kNoStore = (ANOMOD_BK_ABL & 2) != 0 && SOA_IN;
+// The pair of a record at position g whose key is k (level A took the top da
+// bits): the next 32 key bits << 32 | g.
+__device__ inline uint64_t make_pair(uint64_t k, int da, uint64_t g) {
+  return (((k << da) >> 32) << 32) | (uint32_t)g;
+}
+
+__global__ __launch_bounds__(kBThreads) void bk_scatter_a_kernel(
+    SoaIn sin, GRec* __restrict__ aout, uint64_t* __restrict__ pout, uint64_t n, int da,
+    const uint32_t* __restrict__ toff, uint32_t nx) {
+  constexpr bool kNoStore = (ANOMOD_BK_ABL & 2) != 0;
   static_assert(kBWaves * kNDMax * 2 <= kBTile * 32, "counters fit under the stage");
   union Lds {
     uint4 stage[2 * kBTile];              // 128 KiB: the tile's records in digit order
@@ -323,15 +335,10 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
   __shared__ uint32_t gbase[kNDMax];      // global start of each digit's run
   __shared__ uint32_t wsum[kBWaves];
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  const int nd = 1 << dbits;
+  const int nd = 1 << da, shift = 64 - da;
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x, nx);
-  uint64_t base, nvalid;
-  if constexpr (SEG) {
-    if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
-  } else {
-    base = tile * kBTile;
-    nvalid = n - base < (uint64_t)kBTile ? n - base : (uint64_t)kBTile;
-  }
+  const uint64_t base = tile * kBTile;
+  const uint64_t nvalid = n - base < (uint64_t)kBTile ? n - base : (uint64_t)kBTile;
   uint4 ra[kBPer], rb[kBPer];
   uint32_t d[kBPer];
   bool v[kBPer];
@@ -343,15 +350,9 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
     ra[k] = make_uint4(0, 0, 0, 0);
     rb[k] = make_uint4(0, 0, 0, 0);
     if (v[k]) {
-      if constexpr (SOA_IN) {
-        const uint64_t h = sin.h[i], sid = sin.sid[i], pid = sin.pid[i];
-        ra[k] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)sid, (uint32_t)(sid >> 32));
-        rb[k] = make_uint4((uint32_t)pid, (uint32_t)(pid >> 32), sin.sf[i], sin.dur[i]);
-      } else {
-        const uint4* q = reinterpret_cast<const uint4*>(ain + i);
-        ra[k] = q[0];
-        rb[k] = q[1];
-      }
+      const uint64_t h = sin.h[i], sid = sin.sid[i], pid = sin.pid[i];
+      ra[k] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)sid, (uint32_t)(sid >> 32));
+      rb[k] = make_uint4((uint32_t)pid, (uint32_t)(pid >> 32), sin.sf[i], sin.dur[i]);
     }
     d[k] = (uint32_t)(mix64(((uint64_t)ra[k].y << 32) | ra[k].x) >> shift) & (uint32_t)(nd - 1);
   }
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
 #pragma unroll
   for (int k = 0; k < kBPer; ++k) {
     uint64_t peers = __ballot(v[k]);
-    for (int b = 0; b < dbits; ++b) {
+    for (int b = 0; b < da; ++b) {
       const bool bit = (d[k] >> b) & 1u;
       const uint64_t bb = __ballot(v[k] && bit);
       peers &= bit ? bb : ~bb;
@@ -416,7 +417,8 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
   }
   __syncthreads();
   if constexpr (kNoStore) return;
-  // 16-B chunks in staged order: chunk c is half (c & 1) of staged record c / 2
+  // 16-B chunks in staged order: chunk c is half (c & 1) of staged record c / 2;
+  // the lane holding a record's first half also writes its pair
   const uint64_t nch = 2 * nvalid;
 #pragma unroll
   for (int j = 0; j < 2 * kBPer; ++j) {
@@ -434,8 +436,108 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_kernel(
                                     reinterpret_cast<u32x4*>(aout) + 2 * g + (c & 1u));
       } else
         reinterpret_cast<uint4*>(aout)[2 * g + (c & 1u)] = x;
-      if constexpr (DNEXT)
-        if (!(c & 1u)) dnext[g] = (uint16_t)((k >> nshift) & nmask);
+      if (!(c & 1u)) pout[g] = make_pair(k, da, g);
+    }
+  }
+}
+
+// ---- level B: one stable scatter of the pairs inside every level-A bucket ----
+// Tile = 16384 pairs (1024 threads x 16, wave w owns positions [1024w, 1024w +
+// 1024)) of one level-A bucket, ranked by the top db bits of the pair with
+// the same wave multisplit, staged in LDS in digit order (128 KiB) and written
+// 8 B per lane in staged order.  An 8-B pair in place of the 32-B record: a
+// quarter of the bytes, and a tile of four times as many entries (runs of ~8
+// pairs per digit at 11 bits, against ~2 records).
+__global__ __launch_bounds__(kBThreads) void bk_scatter_b_kernel(
+    const uint64_t* __restrict__ pin, uint64_t* __restrict__ pout, int db,
+    const uint32_t* __restrict__ toff, const uint32_t* __restrict__ bsA,
+    const uint32_t* __restrict__ btile, const uint32_t* __restrict__ tmap, int na, uint32_t nx) {
+  static_assert(kBWaves * kNDMax * 2 <= kPTile * 8, "counters fit under the stage");
+  union Lds {
+    uint64_t stage[kPTile];               // 128 KiB: the tile's pairs in digit order
+    uint16_t wcnt[kBWaves][kNDMax];       // per-wave digit counts, then wave offsets
+  };
+  __shared__ Lds u;
+  __shared__ uint32_t tstart[kNDMax];
+  __shared__ uint32_t gbase[kNDMax];
+  __shared__ uint32_t wsum[kBWaves];
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const int nd = 1 << db, shift = 64 - db;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x, nx);
+  uint64_t base, nvalid;
+  if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
+  uint64_t x[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane);
+    x[k] = loc < nvalid ? pin[base + loc] : 0ull;
+  }
+  for (int ww = 0; ww < kBWaves; ++ww)
+    for (int dd = tid; dd < nd; dd += kBThreads) u.wcnt[ww][dd] = 0;
+  for (int dd = tid; dd < nd; dd += kBThreads) gbase[dd] = toff[tile * nd + dd];
+  __syncthreads();
+
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  uint32_t off[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const bool v = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane) < nvalid;
+    const uint32_t d = (uint32_t)(x[k] >> shift);
+    uint64_t peers = __ballot(v);
+    for (int b = 0; b < db; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(v && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    off[k] = 0;
+    if (v) {
+      const uint64_t lower = peers & lt_mask;
+      const uint32_t b0 = u.wcnt[w][d];
+      off[k] = b0 + (uint32_t)__popcll(lower);
+      if (lower == 0ull) u.wcnt[w][d] = (uint16_t)(b0 + (uint32_t)__popcll(peers));
+    }
+    wave_sync();
+  }
+  __syncthreads();
+
+  const int dpt = nd > kBThreads ? nd / kBThreads : 1;
+  uint32_t tot[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd >= nd) continue;
+    uint32_t run = 0;
+    for (int ww = 0; ww < kBWaves; ++ww) {
+      const uint32_t c = u.wcnt[ww][dd];
+      u.wcnt[ww][dd] = (uint16_t)run;
+      run += c;
+    }
+    tot[i] = run;
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kBWaves>(tot[0] + tot[1], wsum, &all);
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd < nd) tstart[dd] = pre + (i ? tot[0] : 0u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {  // the wave offsets into off[]
+    const bool v = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane) < nvalid;
+    const uint32_t d = (uint32_t)(x[k] >> shift);
+    off[k] = v ? tstart[d] + u.wcnt[w][d] + off[k] : 0xFFFFFFFFu;
+  }
+  __syncthreads();  // the counters are dead: the stage goes over them
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k)
+    if (off[k] != 0xFFFFFFFFu) u.stage[off[k]] = x[k];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPPer; ++j) {
+    const uint32_t c = (uint32_t)(tid + j * kBThreads);
+    if (c < nvalid) {
+      const uint64_t y = u.stage[c];
+      const uint32_t dd = (uint32_t)(y >> shift);
+      pout[(uint64_t)gbase[dd] + (c - tstart[dd])] = y;
     }
   }
 }
@@ -445,10 +547,10 @@ template <int W, int PER>
 struct BucketLds {
   static constexpr int kCap = W * PER, kNW = W / kWv;
   struct Pre {
-    uint64_t skey[kCap];          // keys in sub-digit order
+    uint64_t skey[kCap];          // pairs in sub-digit order, then full keys by final position
     uint32_t mixed[kSub];         // sub-bucket holds more than one key
     uint32_t tstart[kSub + 1];
-    uint16_t sorig[kCap];         // arrival position of every staged key
+    uint16_t sorig[kCap];         // arrival position of every staged pair
     uint16_t wcnt[kNW][kSub];
     uint8_t sflag[kCap];          // trace start at final position f
   };
@@ -457,15 +559,17 @@ struct BucketLds {
   } u;
   uint16_t sfinal[kCap];          // final position of every arrival position
   uint32_t wsum[kNW];
+  uint32_t flag;
 };
 
 // A bucket beyond the large kernel (a trace of thousands of spans, or two
 // such traces side by side): its distinct keys (at most kHugeKeys) counted in
-// an LDS hash table and ranked, then ONE wave walks the records in arrival
-// order and sends each to its trace's next row (peers of a row found by
-// ballots over the slot index; a per-slot running row in LDS) — stable, and
-// O(m) for any size.  More distinct keys than that sends the set to the LSD
-// path.  Uses the large kernel's LDS (>= 82 KiB) as raw bytes.
+// an LDS hash table and ranked, then ONE wave walks the pairs in arrival
+// order (= position order: level B is stable) and sends each record to its
+// trace's next row (peers of a row found by ballots over the slot index; a
+// per-slot running row in LDS) — stable, and O(m) for any size.  More
+// distinct keys than that sends the set to the LSD path.  Uses the large
+// kernel's LDS (>= 82 KiB) as raw bytes.
 constexpr uint32_t kHugeSlots = 4096;
 constexpr uint32_t kHugeKeys = 2048;
 constexpr uint64_t kEmptyKey = ~0ull;
@@ -483,8 +587,8 @@ __device__ inline int huge_slot(const uint64_t* hkey, uint64_t k) {
 
 template <int W>
 __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_t m,
-                            const GRec* __restrict__ in, SoaOut out, uint32_t* __restrict__ dcnt,
-                            unsigned long long* __restrict__ too_big) {
+                            uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+                            uint32_t* __restrict__ dcnt, unsigned long long* __restrict__ too_big) {
   constexpr int kNW = W / kWv;
   uint64_t* hkey = reinterpret_cast<uint64_t*>(lds);               // [kHugeSlots]
   uint32_t* hcnt = reinterpret_cast<uint32_t*>(lds + 32768);       // count, then next row
@@ -501,7 +605,7 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
   if (tid < 4) hm[tid] = 0u;
   __syncthreads();
   for (uint32_t p = tid; p < m; p += W) {
-    const uint64_t k = mix64(in[a0 + p].h);
+    const uint64_t k = mix64(rec[(uint32_t)pin[a0 + p]].h);
     bool done = k == kEmptyKey;  // the table's empty mark: LSD path
     if (done) hm[1] = 1u;
     uint32_t s = (uint32_t)k & (kHugeSlots - 1u);
@@ -556,7 +660,7 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
       const bool v = p < m;
       uint4 r0 = make_uint4(0, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
       if (v) {
-        const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+        const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)pin[a0 + p]);
         r0 = q[0];
         r1 = q[1];
       }
@@ -581,22 +685,23 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
       }
     }
   }
-  __syncthreads();  // every record read before the trace starts go over them
-  uint64_t* tsp = reinterpret_cast<uint64_t*>(const_cast<GRec*>(in)) + 4ull * a0;
-  for (uint32_t r = tid; r < d; r += W) tsp[r] = (uint64_t)a0 + rrow[r];
+  __syncthreads();  // every pair read before the trace starts go over them
+  for (uint32_t r = tid; r < d; r += W) pin[a0 + r] = (uint64_t)a0 + rrow[r];
   if (tid == 0) dcnt[c] = d;
 }
 
-// Bucket c = [bstart[c], bstart[c + 1]) of `in` (records in arrival order
-// inside the bucket; every k shares its top T bits).  Split once more by the
-// next 8 bits of k (stable); a sub-bucket holding one key is already in
-// arrival order, a mixed one ranks each key by compares:
-// rank = #{smaller k} + #{equal k earlier}.  Writes the grouped columns of the
-// bucket, its trace starts at tsp[4 * bstart[c] + ordinal] (the bucket's own
-// record region, read before) and the trace count dcnt[c].
+// Bucket c = [bstart[c], bstart[c + 1]) of the pairs `pin` (in arrival order
+// inside the bucket; every key shares its top T bits).  Split once more by the
+// next 9 key bits (stable); a sub-bucket holding one key is already in
+// arrival order, a mixed one ranks each pair by compares: rank = #{smaller
+// pair} (a pair orders by (key bits, position) and positions are arrival
+// order).  The records come from `rec` by position.  Writes the grouped
+// columns of the bucket, its trace starts over the bucket's own pairs
+// (pin[bstart[c] + ordinal], read before) and the trace count dcnt[c].
 template <int W, int PER>
-__device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __restrict__ in,
-                                SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
+__device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, uint64_t* __restrict__ pin,
+                                const GRec* __restrict__ rec, SoaOut out,
+                                const uint32_t* __restrict__ bstart, int kshift,
                                 uint32_t* __restrict__ dcnt, bool small,
                                 uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
                                 uint32_t over_cap, unsigned long long* __restrict__ too_big) {
@@ -615,7 +720,7 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
       return;
     }
     if constexpr (sizeof(BucketLds<W, PER>) >= 81920 + 16 + 4 * (W / kWv))
-      bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, in, out, dcnt, too_big);
+      bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, pin, rec, out, dcnt, too_big);
     else if (tid == 0)
       atomicAdd(too_big, 1ull);
     return;
@@ -624,12 +729,10 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
     if (tid == 0) dcnt[c] = 0;
     return;
   }
-  // REG (the small kernel): whole records held in registers; else keys only,
-  // the records read again (from L2) when staged in final order.  (2^25 SN
-  // traces: 6.14 ms re-reading, 5.32 holding; 64-bit LDS min / max atomics
-  // for the one-key test instead of the flag pass: +1.1 ms.)
+  // REG (the small kernel): whole records held in registers from the gather
+  // on; else only their keys, the records gathered again when written.
   constexpr bool REG = PER <= 4;
-  uint64_t k[PER];
+  uint64_t k[PER], fk[PER];
   uint32_t e[PER], off[PER];
   bool v[PER];
   uint4 ra[REG ? PER : 1], rb[REG ? PER : 1];
@@ -637,18 +740,27 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
   for (int j = 0; j < PER; ++j) {
     const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
     v[j] = p < m;
+    k[j] = v[j] ? pin[a0 + p] : 0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {  // the gathers: issued together, after every pair load
     if constexpr (REG) {
-      const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+      const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
       ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
       rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
-      k[j] = mix64(((uint64_t)ra[j].y << 32) | ra[j].x);
     } else {
-      k[j] = v[j] ? mix64(in[a0 + p].h) : 0ull;
+      fk[j] = v[j] ? rec[(uint32_t)k[j]].h : 0ull;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if constexpr (REG) fk[j] = ((uint64_t)ra[j].y << 32) | ra[j].x;
+    fk[j] = mix64(fk[j]);
     e[j] = (uint32_t)(k[j] >> kshift) & (kSub - 1);
   }
   for (int i = tid; i < kNW * kSub; i += W) (&P.wcnt[0][0])[i] = 0;
   for (int i = tid; i < kSub; i += W) P.mixed[i] = 0u;
+  if (tid == 0) L.flag = 0u;
   __syncthreads();
 
   const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -702,7 +814,7 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
     if (sp < m) {
       const uint64_t kp = P.skey[sp];
       const uint32_t ee = (uint32_t)(kp >> kshift) & (kSub - 1);
-      if (kp != P.skey[P.tstart[ee]]) P.mixed[ee] = 1u;
+      if ((kp >> 32) != (P.skey[P.tstart[ee]] >> 32)) P.mixed[ee] = 1u;
     }
   }
   __syncthreads();
@@ -722,17 +834,16 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
       } else {
         rank = 0;
         first = 1;
-        for (uint32_t q0 = a; q0 < b; q0 += 4) {  // 4 keys per step: one LDS round trip
+        for (uint32_t q0 = a; q0 < b; q0 += 4) {  // 4 pairs per step: one LDS round trip
           uint64_t kq[4];
 #pragma unroll
           for (int t = 0; t < 4; ++t) kq[t] = P.skey[q0 + t < b ? q0 + t : a];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const uint32_t q = q0 + t;
-            const bool in = q < b;
-            const bool eq_before = in && kq[t] == kp && q < sp;
-            rank += (in && (kq[t] < kp || eq_before)) ? 1u : 0u;
-            first &= eq_before ? 0u : 1u;
+            const bool in = q0 + t < b;
+            const bool below = in && kq[t] < kp;  // pairs are distinct
+            rank += below ? 1u : 0u;
+            first &= (below && (kq[t] >> 32) == (kp >> 32)) ? 0u : 1u;
           }
         }
       }
@@ -743,8 +854,48 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
   }
   __syncthreads();
 
-  // trace starts: ordinals in final order (written last: tsp is this bucket's
-  // own record region, read until then)
+  // Two traces of the bucket whose keys agree in every bit the pairs carry:
+  // their spans sit in one run of equal pair keys, in position order.  Seen
+  // as a run whose full keys differ; the bucket is then ranked by (full key,
+  // arrival) instead (rare: O(m^2) compares by every thread).
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if (v[j]) P.skey[L.sfinal[p]] = fk[j];  // skey is dead: full keys by final position
+  }
+  __syncthreads();
+  bool clash = false;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t f = (uint32_t)(tid + j * W);
+    clash |= f > 0 && f < m && !P.sflag[f] && P.skey[f] != P.skey[f - 1];
+  }
+  if (__syncthreads_or(clash)) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+      if (v[j]) P.skey[p] = fk[j];  // full keys by arrival position
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+      if (v[j]) {
+        uint32_t rank = 0, first = 1;
+        for (uint32_t q = 0; q < m; ++q) {
+          const uint64_t kq = P.skey[q];
+          rank += (kq < fk[j] || (kq == fk[j] && q < p)) ? 1u : 0u;
+          first &= (kq == fk[j] && q < p) ? 0u : 1u;
+        }
+        L.sfinal[p] = (uint16_t)rank;
+        P.sflag[rank] = (uint8_t)first;
+      }
+    }
+    __syncthreads();
+  }
+
+  // trace starts: ordinals in final order (written last: over the bucket's
+  // own pairs, read until then)
   uint32_t cnt = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -759,7 +910,6 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
     const uint32_t f = (uint32_t)(tid * PER + j);
     fl |= (f < m && P.sflag[f]) ? (1u << j) : 0u;
   }
-  __syncthreads();
 
   // each record straight to its final row (the bucket's rows of every column
   // are a few KiB: the stores merge in L2)
@@ -772,7 +922,7 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
         x0 = ra[j];
         x1 = rb[j];
       } else {
-        const uint4* q = reinterpret_cast<const uint4*>(in + a0 + p);
+        const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
         x0 = q[0];
         x1 = q[1];
       }
@@ -784,34 +934,34 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, const GRec* __
       out.dur[a0 + i] = x1.w;
     }
   }
-  __syncthreads();  // every record read before tsp goes over them
-  uint64_t* tsp = reinterpret_cast<uint64_t*>(const_cast<GRec*>(in)) + 4ull * a0;
-  uint32_t ord = ord0;
+  uint32_t ord = ord0;  // every pair was read into registers before the first barrier
 #pragma unroll
   for (int j = 0; j < PER; ++j)
-    if ((fl >> j) & 1u) tsp[ord++] = (uint64_t)a0 + (uint32_t)(tid * PER + j);
+    if ((fl >> j) & 1u) pin[a0 + ord++] = (uint64_t)a0 + (uint32_t)(tid * PER + j);
   if (tid == 0) dcnt[c] = nt;
 }
 
 __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
-    const GRec* __restrict__ in, SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
-    uint32_t* __restrict__ dcnt, uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
-    uint32_t over_cap, unsigned long long* __restrict__ too_big, uint32_t nx) {
+    uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+    const uint32_t* __restrict__ bstart, int kshift, uint32_t* __restrict__ dcnt,
+    uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big, uint32_t nx) {
   __shared__ BucketLds<kSmallW, kSmallPer> L;
-  bucket_sort_one<kSmallW, kSmallPer>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), in, out,
-                                      bstart, kshift, dcnt, true, over, over_n, over_cap, too_big);
+  bucket_sort_one<kSmallW, kSmallPer>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), pin, rec,
+                                      out, bstart, kshift, dcnt, true, over, over_n, over_cap,
+                                      too_big);
 }
 
 __global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
-    const GRec* __restrict__ in, SoaOut out, const uint32_t* __restrict__ bstart, int kshift,
-    uint32_t* __restrict__ dcnt, const uint32_t* __restrict__ over,
-    const unsigned long long* __restrict__ over_n, uint32_t over_cap,
-    unsigned long long* __restrict__ too_big) {
+    uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+    const uint32_t* __restrict__ bstart, int kshift, uint32_t* __restrict__ dcnt,
+    const uint32_t* __restrict__ over, const unsigned long long* __restrict__ over_n,
+    uint32_t over_cap, unsigned long long* __restrict__ too_big) {
   __shared__ BucketLds<kBigW, kBigPer> L;
   const uint64_t cnt = *over_n < over_cap ? *over_n : over_cap;
   for (uint64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    bucket_sort_one<kBigW, kBigPer>(L, over[i], in, out, bstart, kshift, dcnt, false, nullptr,
-                                    nullptr, 0, too_big);
+    bucket_sort_one<kBigW, kBigPer>(L, over[i], pin, rec, out, bstart, kshift, dcnt, false,
+                                    nullptr, nullptr, 0, too_big);
     __syncthreads();
   }
 }
@@ -884,7 +1034,7 @@ __global__ __launch_bounds__(256) void bk_ddown_kernel(uint32_t* __restrict__ dc
   }
 }
 
-// one wave per bucket: its trace starts to trace_ptr[tbase[c] ...]
+// one wave per bucket: its trace starts (over its pairs) to trace_ptr[tbase[c] ...]
 __global__ __launch_bounds__(256) void bk_tptr_kernel(const uint64_t* __restrict__ tsp,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ tbase,
@@ -896,7 +1046,7 @@ __global__ __launch_bounds__(256) void bk_tptr_kernel(const uint64_t* __restrict
   if (c >= nb) return;
   const uint32_t t0 = tbase[c];
   const uint32_t t1 = c + 1 < nb ? tbase[c + 1] : (uint32_t)*total;
-  const uint64_t src = 4ull * bstart[c];
+  const uint64_t src = bstart[c];
   for (uint32_t o = lane; o < t1 - t0; o += kWv) tptr[t0 + o] = tsp[src + o];
 }
 
@@ -933,7 +1083,7 @@ BucketGeom bucket_geom(uint64_t n) {
     g.DB = g.T - g.DA;
   }
   g.tilesA = n ? (n + kBTile - 1) / kBTile : 1;
-  g.tilesB = g.DB ? g.tilesA + (1ull << g.DA) : 0;
+  g.tilesB = g.DB ? (n + kPTile - 1) / kPTile + (1ull << g.DA) : 0;
   return g;
 }
 
@@ -974,17 +1124,20 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
                   reinterpret_cast<uint32_t*>(ob + 28 * cap)};
   };
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
-  GRec* bufA = ws->aos[0];
-  GRec* bufB = ws->aos[1];
-  uint16_t* dn = reinterpret_cast<uint16_t*>(ws->dig);
+  GRec* recs = ws->aos[0];                    // level-A records (gathered by the buckets)
+  const SoaOut cols = soa_of(ws->aos[1]);     // the grouped columns
+  uint64_t* pa = ws->pairs[0];                // level-A pairs
+  uint64_t* pb = ws->pairs[1];                // level-B pairs
   hipStream_t st = ctx->stream;
   ANOMOD_HIP(ctx, hipMemsetAsync(ws->misc, 0, kMiscWords * 8, st));
 
   // XCD-contiguous tile order per scatter level (experiment knob
-  // ANOMOD_BK_XCD: bit 0 level A, bit 1 level B, bit 2 the bucket kernel)
-  const int xk = env_int("ANOMOD_BK_XCD", 7);
+  // ANOMOD_BK_XCD: bit 0 level A, bit 1 level B, bit 2 the bucket kernel —
+  // off by default there: buckets in index order keep every XCD inside one
+  // level-A bucket, whose records the gathers then find in the Infinity Cache)
+  const int xk = env_int("ANOMOD_BK_XCD", 3);
   const uint32_t nxA = (xk & 1) ? 8u : 1u, nxB = (xk & 2) ? 8u : 1u;
-  // level A
+  // level A (its bucket starts bsA; btile: level-B tiles per level-A bucket)
   const uint64_t nbA = (g.tilesA + kScanRows - 1) / kScanRows;
   const unsigned dgA = (unsigned)((na + 255) / 256);
   hipLaunchKernelGGL(bk_count_a_kernel, dim3((unsigned)g.tilesA), dim3(256), 0, st,
@@ -992,32 +1145,25 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   hipLaunchKernelGGL(bk_scan_up_kernel, dim3((unsigned)nbA, dgA), dim3(256), 0, st, ws->tcnt,
                      g.tilesA, na, ws->bsum);
   hipLaunchKernelGGL(bk_scan_top_kernel, dim3(1), dim3(1024), 0, st, ws->bsum, nbA, na, n,
-                     ws->bsA, ws->btile);
+                     ws->bsA, ws->btile, (uint32_t)kPTile);
   hipLaunchKernelGGL(bk_scan_down_kernel, dim3((unsigned)nbA, dgA), dim3(256), 0, st, ws->tcnt,
                      g.tilesA, na, ws->bsum);
-  const GRec* cin;
-  SoaOut cols;
+  hipLaunchKernelGGL(bk_scatter_a_kernel, dim3((unsigned)g.tilesA), dim3(kBThreads), 0, st, sin,
+                     recs, pa, n, g.DA, ws->tcnt, nxA);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  if (ANOMOD_BK_ABL & 2) {  // timing of level A only
+    *fallback = true;
+    return ANOMOD_OK;
+  }
+  uint64_t* pin;
   const uint32_t* bstart;
   uint64_t mx = 0;
   if (g.DB > 0) {
-    // every record's next kDMax key bits beside it, so level B can count with
-    // any digit width up to kDMax (a wider level B is the retry for a set
-    // whose buckets outgrow the large kernel)
-    constexpr bool kDnext = (ANOMOD_BK_ABL & 1) == 0;
-    hipLaunchKernelGGL((bk_scatter_kernel<true, false, kDnext>), dim3((unsigned)g.tilesA),
-                       dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
-                       dn, 64 - g.DA - kDMax, (uint32_t)((1u << kDMax) - 1u), nullptr, nullptr,
-                       nullptr, 0, nxA);
-    if (ANOMOD_BK_ABL & 2) {  // timing of level A only
-      *fallback = true;
-      return ANOMOD_OK;
-    }
     hipLaunchKernelGGL(bk_tilemap_kernel, dim3((unsigned)na), dim3(256), 0, st, ws->btile,
                        ws->tmap);
     for (;;) {
-      hipLaunchKernelGGL(bk_count_b_kernel, dim3((unsigned)g.tilesB), dim3(256), 0, st,
-                         kDnext ? dn : reinterpret_cast<const uint16_t*>(bufA), ws->bsA,
-                         ws->btile, ws->tmap, na, g.DB, ws->tcnt);
+      hipLaunchKernelGGL(bk_count_b_kernel, dim3((unsigned)g.tilesB), dim3(256), 0, st, pa,
+                         ws->bsA, ws->btile, ws->tmap, na, g.DB, ws->tcnt);
       hipLaunchKernelGGL(bk_scan_seg_kernel, dim3((unsigned)na), dim3(1024), 0, st, ws->tcnt,
                          ws->bsA, ws->btile, na, g.DB, ws->bstart);
       ANOMOD_HIP(ctx, hipGetLastError());
@@ -1031,11 +1177,9 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       g.DB = kDMax;  // long traces side by side: split finer
       g.T = g.DA + g.DB;
     }
-    hipLaunchKernelGGL((bk_scatter_kernel<false, true, false>), dim3((unsigned)g.tilesB),
-                       dim3(kBThreads), 0, st, sin, bufA, bufB, n, 64 - g.DA - g.DB, g.DB,
-                       ws->tcnt, nullptr, 0, 0u, ws->bsA, ws->btile, ws->tmap, na, nxB);
-    cin = bufB;
-    cols = soa_of(bufA);
+    hipLaunchKernelGGL(bk_scatter_b_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st, pa,
+                       pb, g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap, na, nxB);
+    pin = pb;
     bstart = ws->bstart;
   } else {
     ANOMOD_HIP(ctx, hipGetLastError());
@@ -1047,24 +1191,21 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       *escalate = true;
       return ANOMOD_OK;
     }
-    hipLaunchKernelGGL((bk_scatter_kernel<true, false, false>), dim3((unsigned)g.tilesA),
-                       dim3(kBThreads), 0, st, sin, nullptr, bufA, n, 64 - g.DA, g.DA, ws->tcnt,
-                       nullptr, 0, 0u, nullptr, nullptr, nullptr, 0, nxA);
-    cin = bufA;
-    cols = soa_of(bufB);
+    pin = pa;
     bstart = ws->bsA;
   }
   ANOMOD_HIP(ctx, hipGetLastError());
   const uint64_t nbk = 1ull << g.T;
 
   // buckets: <= 2048 spans in the small kernel, the rest listed for the
-  // large one (<= 8192 spans, or any size holding one trace)
-  const int kshift = 64 - g.T - kSubBits;
-  hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, cin, cols,
+  // large one (<= 8192 spans, or any size holding one trace); the sub-split
+  // takes the 9 pair bits below the DB bits level B took
+  const int kshift = 64 - g.DB - kSubBits;
+  hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin, recs, cols,
                      bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                      ws->misc + kMiscTooBig, (xk & 4) ? 8u : 1u);
   hipLaunchKernelGGL(bk_bucket_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
-                     dim3(kBigW), 0, st, cin, cols, bstart, kshift, ws->dcnt, ws->over,
+                     dim3(kBigW), 0, st, pin, recs, cols, bstart, kshift, ws->dcnt, ws->over,
                      ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
   ANOMOD_HIP(ctx, hipGetLastError());
 
@@ -1077,8 +1218,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   hipLaunchKernelGGL(bk_ddown_kernel, dim3((unsigned)np), dim3(256), 0, st, ws->dcnt, nbk,
                      ws->part);
   hipLaunchKernelGGL(bk_tptr_kernel, dim3((unsigned)((nbk * kWv + 255) / 256)), dim3(256), 0, st,
-                     reinterpret_cast<const uint64_t*>(cin), bstart, ws->dcnt, nbk,
-                     ws->misc + kMiscTraces, ws->tptr);
+                     pin, bstart, ws->dcnt, nbk, ws->misc + kMiscTraces, ws->tptr);
   ANOMOD_HIP(ctx, hipGetLastError());
   ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
                                  (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost, st));
@@ -1111,7 +1251,7 @@ int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, 
   // with kDMax bits
   g.DB = kDMax;
   g.T = g.DA + g.DB;
-  g.tilesB = g.tilesA + (1ull << g.DA);
+  g.tilesB = (in->n_spans + kPTile - 1) / kPTile + (1ull << g.DA);
   return bucket_run_geom(ctx, in, g, res, fallback, &escalate);
 }
 

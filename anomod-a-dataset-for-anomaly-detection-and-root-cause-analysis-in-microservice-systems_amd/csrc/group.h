@@ -52,7 +52,8 @@ struct GroupWs {
   unsigned long long* owned = nullptr;  // mixed buckets sorted into scratch (start << 11 | size)
   uint32_t* tcnt = nullptr;           // per-tile digit counts, then run starts (both paths)
   uint32_t* bsum = nullptr;           // block sums of tcnt (both paths)
-  uint8_t* dig = nullptr;             // next-pass digits: u8 (LSD) / u16 (bucket path)
+  uint8_t* dig = nullptr;             // next-pass digits (LSD path)
+  uint64_t* pairs[2] = {nullptr, nullptr};  // bucket path: level-A / level-B pairs [cap]
   uint64_t list_cap = 0;
   uint32_t epoch = 0;
   // bucket path (bucket.hip)

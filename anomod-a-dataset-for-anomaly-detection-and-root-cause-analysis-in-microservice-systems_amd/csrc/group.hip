@@ -632,12 +632,13 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
                           ws->list_cap * 8, tcnt_words * 4, bsum_words * 4, 2 * cap + 32,
                           (ws->bucket_cap + 1) * 4, 2049 * 4, 2049 * 4, ws->tile_cap * 4,
                           (ws->bucket_cap + 1) * 4, ws->bucket_cap * 4,
-                          (ws->bucket_cap / 4096 + 2) * 4};
+                          (ws->bucket_cap / 4096 + 2) * 4, cap * 8, cap * 8};
   void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
                    (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
                    (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum, (void**)&ws->dig,
                    (void**)&ws->bstart, (void**)&ws->bsA, (void**)&ws->btile, (void**)&ws->tmap,
-                   (void**)&ws->dcnt, (void**)&ws->over, (void**)&ws->part};
+                   (void**)&ws->dcnt, (void**)&ws->over, (void**)&ws->part,
+                   (void**)&ws->pairs[0], (void**)&ws->pairs[1]};
   constexpr int kBufs = sizeof(sizes) / sizeof(sizes[0]);
   static_assert(kBufs == sizeof(ptrs) / sizeof(ptrs[0]), "one pointer per size");
   // Carved 2-MiB aligned from one allocation (the radix passes' time varies by

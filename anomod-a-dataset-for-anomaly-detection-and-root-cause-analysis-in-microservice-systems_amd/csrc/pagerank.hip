@@ -309,6 +309,12 @@ constexpr uint32_t kLdsEdgeBytes = 128 * 1024;  // (col, w) staging per workgrou
 #define ANOMOD_PPR_GATHER 4
 #endif
 constexpr int kPBatch = ANOMOD_PPR_GATHER;  // x gathers in flight per lane (persistent kernel)
+// Timing-only ablations of the persistent kernel (never set in the shipped
+// library): 1 = no x gathers (the SpMV sum is 0), 2 = no grid barrier (a
+// workgroup barrier only; wrong results), 3 = both.
+#ifndef ANOMOD_PPR_ABL
+#define ANOMOD_PPR_ABL 0
+#endif
 
 template <int SUB>
 __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     double sum = 0.0;
-    if (r < N) {
+    if (!(ANOMOD_PPR_ABL & 1) && r < N) {
       // kPBatch gathers in flight per lane (in-degrees ~ Poisson(7) here: one
       // round for nearly every row); lanes past the row's end gather x[0]
       // with weight 0 (adds +0.0: the same bits as skipping them)
@@ -442,7 +448,9 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
       __hip_atomic_store(&acc[(3 + z) * S + threadIdx.x], 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!grid_barrier(bar, it, &s_flag, spin_limit)) {
+    if constexpr ((ANOMOD_PPR_ABL & 2) != 0) {
+      __syncthreads();
+    } else if (!grid_barrier(bar, it, &s_flag, spin_limit)) {
       done = it;
       break;
     }

@@ -320,19 +320,20 @@ def group_bytes(info: dict, n: int, n_traces: int) -> int:
     tiles = -(-n // 4096)
     if info["path"] == "bucket":
         # csrc/bucket.hip: level A counts read trace_hash (8 B) and the scatter
-        # moves 32 B in + 32 B out; with two levels it writes each record's
-        # level-B digit (2 B), which the level-B counts read (2 B), and level B
-        # moves 64 B; the bucket kernel reads the records once (32 B) and writes
-        # the SoA columns (32 B); trace starts: written, read, written to
-        # trace_ptr (24 B/trace).  Tile counts (4 B per tile and digit): written,
-        # scanned (read twice, written once), read by the scatter.
+        # moves 32 B in + 32 B of records and 8 B of pairs out; with two levels
+        # the level-B counts read the pairs (8 B) and level B moves them (8 + 8
+        # B); the bucket kernel reads the pairs (8 B), gathers the records (32
+        # B) and writes the SoA columns (32 B); trace starts: written, read,
+        # written to trace_ptr (24 B/trace).  Tile counts (4 B per tile and
+        # digit; level-B tiles are 16384 pairs): written, scanned (read twice,
+        # written once), read by the scatter.
         T, two = info["bits"], info["levels"] == 2
-        da = (T + 1) // 2 if two else T
+        da = min(11, T) if not two else max(T - 11, min((T + 1) // 2, 9))
         db = T - da if two else 0
-        b = 8 * n + 64 * n + 5 * 4 * tiles * (1 << da)
+        b = 8 * n + 72 * n + 5 * 4 * tiles * (1 << da)
         if two:
-            b += 4 * n + 64 * n + 5 * 4 * tiles * (1 << db)
-        return b + 64 * n + 24 * n_traces
+            b += 8 * n + 16 * n + 5 * 4 * (-(-n // 16384)) * (1 << db)
+        return b + 72 * n + 24 * n_traces
     # csrc/group.hip (LSD): the first pass's tile counts read trace_hash, later
     # passes' the 1-B digits the previous pass wrote (written + read: 2 B);
     # each radix pass reads and writes 32 B (records, the last one the SoA

@@ -242,3 +242,29 @@ def test_group_huge_buckets(ctx):
         g = ctx.group(ctx.upload_ungrouped(flat))
         _assert_grouped_equal(g.download(), _oracle_grouped(flat))
         assert ctx.group_info()["path"] == path
+
+
+@pytest.mark.parametrize("avg", [None, "64"])
+def test_group_pair_key_collisions(ctx, env_knob, avg):
+    """The buckets sort 8-B pairs that carry 32 key bits below level A's;
+    traces whose keys agree in all those bits (here: in the top 48) land in
+    one run of equal pair keys, interleaved by arrival.  The bucket kernel
+    sees the gathered records' full keys differ and re-ranks the bucket by
+    (full key, arrival): the oracle's grouping, with one level (default) and
+    two (ANOMOD_BUCKET_AVG=64)."""
+    if avg:
+        env_knob("ANOMOD_BUCKET_AVG", avg)
+    rng = np.random.default_rng(80)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 30000, 16, dup=0.02), rng)
+    k1 = rng.integers(0, 2**64, 500, dtype=np.uint64)
+    k2 = (k1 & np.uint64(0xFFFFFFFFFFFF0000)) | rng.integers(0, 2**16, 500, dtype=np.uint64)
+    keep = k2 != k1
+    keys = np.concatenate([k1[keep], k2[keep]])
+    coll = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02,
+                                              lens=rng.integers(1, 30, keys.shape[0])),
+                              rng, _unmix64(keys))
+    flat = _interleave(anomod.SpanSet.concat([sp, coll]), rng, "time")
+    g = ctx.group(ctx.upload_ungrouped(flat))
+    _assert_grouped_equal(g.download(), _oracle_grouped(flat))
+    assert ctx.group_info()["path"] == "bucket"
+    assert ctx.group_info()["levels"] == (2 if avg else 1)
