@@ -543,9 +543,10 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_b_kernel(
 }
 
 // ---- one bucket in (k, arrival) order ---------------------------------------
-template <int W, int PER>
+template <int W, int PER, bool EDGE = false>
 struct BucketLds {
   static constexpr int kCap = W * PER, kNW = W / kWv;
+  static_assert(kNW * kSub >= kCap, "trace starts fit over the sub-digit counters");
   struct Pre {
     uint64_t skey[kCap];          // pairs in sub-digit order, then full keys by final position
     uint32_t mixed[kSub];         // sub-bucket holds more than one key
@@ -558,8 +559,17 @@ struct BucketLds {
     Pre pre;
   } u;
   uint16_t sfinal[kCap];          // final position of every arrival position
+  uint16_t ssvc[EDGE ? kCap : 1]; // edge records: services by final position
   uint32_t wsum[kNW];
   uint32_t flag;
+};
+
+// Edge-record output of the fused ungrouped aggregation: per span, its
+// (parent service row * S + service) edge << 33 | error << 32 | duration,
+// the parent found in the span's trace by the first-match rule.
+struct EdgeOut {
+  uint64_t* rec;  // [n], by grouped position
+  uint32_t S;
 };
 
 // A bucket beyond the large kernel (a trace of thousands of spans, or two
@@ -690,6 +700,87 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
   if (tid == 0) dcnt[c] = d;
 }
 
+// The bucket in final order -> one edge record per span (fused ungrouped
+// aggregation): span ids and services staged in LDS by final position, each
+// trace's bounds from its start flags, the parent found by the first-match
+// scan over the trace (the order jaeger_to_csv.py:34-38 /
+// trace_collector.py:424-443 see: arrival order inside the trace).
+template <int W, int PER, bool EDGE, int R>
+__device__ void bucket_edges(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m,
+                             const uint64_t (&k)[PER], const bool (&v)[PER], const uint4 (&ra)[R],
+                             const uint4 (&rb)[R], const GRec* __restrict__ rec, EdgeOut eo) {
+  constexpr int kNW = W / kWv;
+  constexpr bool REG = R == PER;
+  auto& P = L.u.pre;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  uint16_t* tord = P.sorig;            // trace ordinal of every final position
+  uint16_t* tsf = &P.wcnt[0][0];       // first final position of every trace
+  // ordinals of the trace starts (thread tid: final positions tid * PER + j)
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t f = (uint32_t)(tid * PER + j);
+    cnt += f < m ? P.sflag[f] : 0u;
+  }
+  uint32_t nt;
+  uint32_t ord = block_excl_scan<kNW>(cnt, L.wsum, &nt);  // its barriers order sflag / skey
+  uint4 x0[PER], x1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if constexpr (REG) {
+      x0[j] = ra[j];
+      x1[j] = rb[j];
+    } else {
+      const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
+      x0[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+      x1[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+    }
+    if (v[j]) {
+      const uint32_t f = L.sfinal[p];
+      P.skey[f] = ((uint64_t)x0[j].w << 32) | x0[j].z;  // span id
+      L.ssvc[f] = (uint16_t)x1[j].z;                     // service
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t f = (uint32_t)(tid * PER + j);
+    if (f < m) {
+      if (P.sflag[f]) tsf[ord++] = (uint16_t)f;
+      tord[f] = (uint16_t)(ord - 1u);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (!v[j]) continue;
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    const uint32_t f = L.sfinal[p], t = tord[f];
+    const uint32_t a = tsf[t], b = t + 1u < nt ? tsf[t + 1u] : m;
+    const uint64_t pid = ((uint64_t)x1[j].y << 32) | x1[j].x;
+    uint32_t prow = eo.S;  // ROOT: no parent reference
+    if (pid != 0ull) {
+      prow = eo.S + 1u;  // ORPHAN unless the trace holds the reference
+      for (uint32_t q0 = a; q0 < b; q0 += 4) {  // first match, 4 ids per LDS round trip
+        uint64_t id[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) id[u] = P.skey[q0 + u < b ? q0 + u : a];
+        int hit = -1;
+#pragma unroll
+        for (int u = 3; u >= 0; --u)
+          if (q0 + u < b && id[u] == pid) hit = u;
+        if (hit >= 0) {
+          prow = L.ssvc[q0 + hit];
+          break;
+        }
+      }
+    }
+    const uint32_t svc = x1[j].z & 0xFFFFu, fl = x1[j].z >> 16;
+    eo.rec[a0 + f] = ((uint64_t)(prow * eo.S + svc) << 33) |
+                     ((uint64_t)((fl & ANOMOD_FLAG_ERROR) ? 1u : 0u) << 32) | x1[j].w;
+  }
+}
+
 // Bucket c = [bstart[c], bstart[c + 1]) of the pairs `pin` (in arrival order
 // inside the bucket; every key shares its top T bits).  Split once more by the
 // next 9 key bits (stable); a sub-bucket holding one key is already in
@@ -698,9 +789,9 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
 // order).  The records come from `rec` by position.  Writes the grouped
 // columns of the bucket, its trace starts over the bucket's own pairs
 // (pin[bstart[c] + ordinal], read before) and the trace count dcnt[c].
-template <int W, int PER>
-__device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, uint64_t* __restrict__ pin,
-                                const GRec* __restrict__ rec, SoaOut out,
+template <int W, int PER, bool EDGE>
+__device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t* __restrict__ pin,
+                                const GRec* __restrict__ rec, SoaOut out, EdgeOut eo,
                                 const uint32_t* __restrict__ bstart, int kshift,
                                 uint32_t* __restrict__ dcnt, bool small,
                                 uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
@@ -719,14 +810,16 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, uint64_t* __re
       }
       return;
     }
-    if constexpr (sizeof(BucketLds<W, PER>) >= 81920 + 16 + 4 * (W / kWv))
+    // (the fused aggregation leaves such a bucket — traces of thousands of
+    // spans side by side — to the unfused path: too_big)
+    if constexpr (!EDGE && sizeof(BucketLds<W, PER, EDGE>) >= 81920 + 16 + 4 * (W / kWv))
       bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, pin, rec, out, dcnt, too_big);
     else if (tid == 0)
       atomicAdd(too_big, 1ull);
     return;
   }
   if (m == 0) {
-    if (tid == 0) dcnt[c] = 0;
+    if (tid == 0 && !EDGE) dcnt[c] = 0;
     return;
   }
   // REG (the small kernel): whole records held in registers from the gather
@@ -894,6 +987,10 @@ __device__ void bucket_sort_one(BucketLds<W, PER>& L, uint32_t c, uint64_t* __re
     __syncthreads();
   }
 
+  if constexpr (EDGE) {
+    bucket_edges(L, a0, m, k, v, ra, rb, rec, eo);
+    return;
+  }
   // trace starts: ordinals in final order (written last: over the bucket's
   // own pairs, read until then)
   uint32_t cnt = 0;
@@ -947,9 +1044,35 @@ __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
     uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n, uint32_t over_cap,
     unsigned long long* __restrict__ too_big, uint32_t nx) {
   __shared__ BucketLds<kSmallW, kSmallPer> L;
-  bucket_sort_one<kSmallW, kSmallPer>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), pin, rec,
-                                      out, bstart, kshift, dcnt, true, over, over_n, over_cap,
-                                      too_big);
+  bucket_sort_one<kSmallW, kSmallPer, false>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), pin,
+                                             rec, out, EdgeOut{}, bstart, kshift, dcnt, true, over,
+                                             over_n, over_cap, too_big);
+}
+
+// The fused ungrouped aggregation's bucket kernels: the same sort, then
+// edge records instead of grouped columns.
+__global__ __launch_bounds__(kSmallW) void bk_bucket_edge_kernel(
+    uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, int kshift, uint32_t* __restrict__ over,
+    unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ BucketLds<kSmallW, kSmallPer, true> L;
+  bucket_sort_one<kSmallW, kSmallPer, true>(L, blockIdx.x, pin, rec, SoaOut{}, eo, bstart, kshift,
+                                            nullptr, true, over, over_n, over_cap, too_big);
+}
+
+__global__ __launch_bounds__(kBigW) void bk_bucket_edge_big_kernel(
+    uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, int kshift, const uint32_t* __restrict__ over,
+    const unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ BucketLds<kBigW, kBigPer, true> L;
+  const uint64_t cnt = *over_n < over_cap ? *over_n : over_cap;
+  for (uint64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    bucket_sort_one<kBigW, kBigPer, true>(L, over[i], pin, rec, SoaOut{}, eo, bstart, kshift,
+                                          nullptr, false, nullptr, nullptr, 0, too_big);
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
@@ -960,8 +1083,8 @@ __global__ __launch_bounds__(kBigW) void bk_bucket_big_kernel(
   __shared__ BucketLds<kBigW, kBigPer> L;
   const uint64_t cnt = *over_n < over_cap ? *over_n : over_cap;
   for (uint64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    bucket_sort_one<kBigW, kBigPer>(L, over[i], pin, rec, out, bstart, kshift, dcnt, false,
-                                    nullptr, nullptr, 0, too_big);
+    bucket_sort_one<kBigW, kBigPer, false>(L, over[i], pin, rec, out, EdgeOut{}, bstart, kshift,
+                                           dcnt, false, nullptr, nullptr, 0, too_big);
     __syncthreads();
   }
 }
@@ -1104,7 +1227,7 @@ int max_bucket(anomod_ctx* ctx, const uint32_t* bstart, uint64_t nbk, uint64_t* 
 }
 
 int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, GroupResult* res,
-                    bool* fallback, bool* escalate) {
+                    bool* fallback, bool* escalate, const EdgeOut* eo) {
   *fallback = false;
   *escalate = false;
   GroupWs* ws = ctx->group_ws;
@@ -1201,6 +1324,23 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   // large one (<= 8192 spans, or any size holding one trace); the sub-split
   // takes the 9 pair bits below the DB bits level B took
   const int kshift = 64 - g.DB - kSubBits;
+  if (eo) {  // the fused ungrouped aggregation: edge records, no columns, no trace_ptr
+    hipLaunchKernelGGL(bk_bucket_edge_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
+                       recs, *eo, bstart, kshift, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                       ws->misc + kMiscTooBig);
+    hipLaunchKernelGGL(bk_bucket_edge_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
+                       dim3(kBigW), 0, st, pin, recs, *eo, bstart, kshift, ws->over,
+                       ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
+    ANOMOD_HIP(ctx, hipGetLastError());
+    ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
+                                   (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost, st));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(st));
+    *fallback = ws->h_misc[kMiscTooBig] != 0;
+    res->passes = g.DB ? 2 : 1;
+    res->bits = g.T;
+    res->bucket = true;
+    return ANOMOD_OK;
+  }
   hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin, recs, cols,
                      bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                      ws->misc + kMiscTooBig, (xk & 4) ? 8u : 1u);
@@ -1242,17 +1382,20 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
 
 }  // namespace
 
-int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback) {
+int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback,
+                     uint64_t* erec, uint32_t S) {
   BucketGeom g = bucket_geom(in->n_spans);
   bool escalate = false;
-  if (int rc = bucket_run_geom(ctx, in, g, res, fallback, &escalate)) return rc;
+  const EdgeOut eo{erec, S};
+  const EdgeOut* pe = erec ? &eo : nullptr;
+  if (int rc = bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe)) return rc;
   if (!escalate) return ANOMOD_OK;
   // one level was not enough for the set's longest traces: two, the second
   // with kDMax bits
   g.DB = kDMax;
   g.T = g.DA + g.DB;
   g.tilesB = (in->n_spans + kPTile - 1) / kPTile + (1ull << g.DA);
-  return bucket_run_geom(ctx, in, g, res, fallback, &escalate);
+  return bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe);
 }
 
 }  // namespace anomod

@@ -177,6 +177,12 @@ int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_
 void free_spans(anomod_spans* s);
 // Trace-grouping workspace (group.hip), released with the ctx.
 void free_group_ws(anomod_ctx* ctx);
+// Edge table of n per-span edge records (the fused ungrouped aggregation:
+// (parent row * S + service) << 33 | error << 32 | duration, csrc/bucket.hip)
+// into `out`, merged over an attached communicator; *hist_form is the set's
+// histogram-form hint (read, and updated with what the run learned).
+int edge_aggregate_records(anomod_ctx* ctx, const uint64_t* rec, uint64_t n, uint32_t S,
+                           int8_t* hist_form, anomod_edge_table* out);
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
 int ensure_host_stage(anomod_ctx* ctx, size_t bytes);

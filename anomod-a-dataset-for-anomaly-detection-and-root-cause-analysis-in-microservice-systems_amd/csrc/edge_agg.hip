@@ -1350,6 +1350,48 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
   tables_flush<HT, ST>(smem, E, tab, tid);
 }
 
+// Edge records (the fused ungrouped aggregation, bucket.hip): one 8-B record
+// per span — (parent row * S + service) << 33 | error << 32 | duration — into
+// the chunk walk's LDS table forms.  A plain stream: 8 records per thread
+// loaded together, then recorded.  The compact form also reports its largest
+// workgroup occupancy (tab.ovf[1], atomic max), so a set learns whether the
+// pair table would hold it.
+constexpr int kRecLoad = 8;
+template <int HT, int ST>
+__global__ __launch_bounds__(kThreads) void edge_rec_kernel(const uint64_t* __restrict__ rec,
+                                                            uint64_t n, uint32_t E, Table tab) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kOffWave];
+  const int tid = threadIdx.x;
+  tables_init<HT, ST>(smem, E, tid);
+  __syncthreads();
+  constexpr uint64_t kPerBlock = (uint64_t)kThreads * kRecLoad;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kPerBlock; b0 < n; b0 += (uint64_t)gridDim.x * kPerBlock) {
+    uint64_t x[kRecLoad];
+#pragma unroll
+    for (int j = 0; j < kRecLoad; ++j) {
+      const uint64_t i = b0 + (uint64_t)(j * kThreads + tid);
+      x[j] = i < n ? rec[i] : ~0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kRecLoad; ++j)
+      if (x[j] != ~0ull)
+        record<HT, ST>(smem, (uint32_t)(x[j] >> 33), (uint32_t)x[j],
+                       ((x[j] >> 32) & 1ull) ? ANOMOD_FLAG_ERROR : 0u, tab);
+  }
+  __syncthreads();
+  tables_flush<HT, ST>(smem, E, tab, tid);
+  if constexpr (HT == kHtCompact) {
+    auto* ctl = reinterpret_cast<uint32_t*>(smem + kOffCtl);
+    const auto* hk = reinterpret_cast<const uint32_t*>(smem + kOffHt);
+    uint32_t used = 0;
+    for (uint32_t s = tid; s < kCmpSlots; s += kThreads) used += hk[s] ? 1u : 0u;
+    for (int o = 32; o > 0; o >>= 1) used += __shfl_xor(used, o);
+    if ((tid & (kWave - 1)) == 0) atomicAdd(&ctl[1], used);
+    __syncthreads();
+    if (tid == 0) atomicMax(&tab.ovf[1], (unsigned long long)ctl[1]);
+  }
+}
+
 // Count + nearest-rank quantiles per edge from the merged histogram: one
 // wave per edge, 14 contiguous bins per lane, wave prefix sum.
 constexpr int kBinsPerLane = (kBins + kWave - 1) / kWave;
@@ -1456,6 +1498,7 @@ __global__ __launch_bounds__(256) void exact_pick_kernel(const unsigned long lon
 
 using KernelFn = void (*)(const uint64_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                           const uint64_t*, uint64_t, uint32_t, uint32_t, Table);
+using KernelFn1 = void (*)(const uint64_t*, uint64_t, uint32_t, Table);
 
 // The histogram form a set asks for: 0 pair, 1 compact, -1 unknown (pair with
 // the saturation hand-off to a compact resume launch) — its hint, or
@@ -1650,7 +1693,149 @@ hipError_t launch_big_for(anomod_ctx* ctx, const anomod_spans* spans, uint32_t S
   return launch_big<kHtHbm, kStHbm>(ctx, spans, S, E, tab);
 }
 
+// Pointers of every section of the device table for layout L.
+Table table_at(anomod_ctx* ctx, const Layout& L, uint32_t E) {
+  char* base = static_cast<char*>(ctx->d_table);
+  Table tab{};  // keys = nullptr: the table forms, not the exact-quantile keys
+  tab.hist = reinterpret_cast<unsigned long long*>(base + L.off_hist);
+  tab.err = reinterpret_cast<unsigned long long*>(base + L.off_err);
+  tab.sum = reinterpret_cast<unsigned long long*>(base + L.off_sum);
+  tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
+  tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
+  tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
+  tab.big = reinterpret_cast<unsigned long long*>(base + L.off_big);
+  tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
+  tab.bpar = reinterpret_cast<uint16_t*>(base + L.off_bpar);
+  tab.ovf = reinterpret_cast<unsigned long long*>(base + L.off_ovf);
+  tab.nleft = reinterpret_cast<unsigned long long*>(base + L.off_nleft);
+  tab.left = reinterpret_cast<unsigned long long*>(base + L.off_left);
+  tab.mode = kModeNormal;
+  tab.kb = 1;
+  while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
+  return tab;
+}
+
+// hist | err | sum | mx | counters to zero, mn to all ones (one launch).
+int table_clear(anomod_ctx* ctx, const Layout& L, const Table& tab, uint32_t E) {
+  const uint64_t nz = L.off_count / 8;  // hist|err|sum|mx|ctr|big|ovf|nleft
+  const uint64_t blocks = std::min<uint64_t>((nz / 2 + 255) / 256 + 1, 4ull * ctx->num_cus);
+  hipLaunchKernelGGL(edge_table_init_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                     static_cast<unsigned long long*>(ctx->d_table), nz, tab.mn, E);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  return ANOMOD_OK;
+}
+
+// After the aggregation kernels: the merge over an attached communicator, the
+// quantiles, and the table to the caller's arrays; ovf[0..1] = the table's
+// two overflow words.
+int table_finish(anomod_ctx* ctx, const Layout& L, const Table& tab, uint32_t E,
+                 anomod_edge_table* out, unsigned long long* ovf) {
+  char* base = static_cast<char*>(ctx->d_table);
+  auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
+  auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
+  auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
+  // Any attached communicator merges, a 1-rank one included (an identity
+  // reduce, so the RCCL call sequence is exercised on a single-GPU box too).
+  if (comm_attached(ctx)) {
+    if (int rc = stage_begin(ctx, kStageEdgeReduce)) return rc;
+    if (int rc = coll_begin(ctx)) return rc;
+    // hist | err | sum are contiguous u64: one sum all-reduce.
+    if (int rc = coll_allreduce(ctx, base, (size_t)E * kBins + 2ull * E, kCollU64, kCollSum))
+      return rc;
+    if (int rc = coll_allreduce(ctx, tab.mn, E, kCollU32, kCollMin)) return rc;
+    if (int rc = coll_allreduce(ctx, tab.mx, E, kCollU32, kCollMax)) return rc;
+    if (int rc = coll_end(ctx)) return rc;
+    if (int rc = stage_end(ctx, kStageEdgeReduce)) return rc;
+  }
+
+  if (int rc = stage_begin(ctx, kStageEdgeFinal)) return rc;
+  hipLaunchKernelGGL(edge_finalize_kernel, dim3(E), dim3(kWave), 0, ctx->stream, tab, count, p50,
+                     p99);
+  ANOMOD_HIP(ctx, hipGetLastError());
+  if (int rc = stage_end(ctx, kStageEdgeFinal)) return rc;
+
+  // The per-edge vectors come back in one D2H into pinned staging, then
+  // fan out on the host; the histogram (when asked for) goes straight.
+  const size_t small = L.end_small - L.off_err;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, base + L.off_err, small, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  if (out->hist)
+    ANOMOD_HIP(ctx, hipMemcpyAsync(out->hist, tab.hist, (size_t)E * kBins * 8ull,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+  if (int rc = stream_wait(ctx)) return rc;
+  const char* hs = static_cast<const char*>(ctx->h_stage);
+  auto fan = [&](void* dst, size_t off, size_t bytes) {  // off: device layout offset
+    if (dst) memcpy(dst, hs + (off - L.off_err), bytes);
+  };
+  fan(out->count, L.off_count, E * 8ull);
+  fan(out->errors, L.off_err, E * 8ull);
+  fan(out->sum_us, L.off_sum, E * 8ull);
+  fan(out->min_us, L.off_mn, E * 4ull);
+  fan(out->max_us, L.off_mx, E * 4ull);
+  fan(out->p50_us, L.off_p50, E * 8ull);
+  fan(out->p99_us, L.off_p99, E * 8ull);
+  memcpy(ovf, hs + (L.off_ovf - L.off_err), 16);
+  return ANOMOD_OK;
+}
+
 }  // namespace
+
+int edge_aggregate_records(anomod_ctx* ctx, const uint64_t* rec, uint64_t n, uint32_t S,
+                           int8_t* hist_form, anomod_edge_table* out) {
+  int local = ANOMOD_OK;
+  ANOMOD_CHECK_LOCAL(ctx, local, S >= 1 && S <= 4096, "n_services=%u out of range [1, 4096]", S);
+  ANOMOD_CHECK_LOCAL(ctx, local, out->n_services == S, "out->n_services=%u != n_services=%u",
+                     out->n_services, S);
+  ANOMOD_CHECK_LOCAL(ctx, local, out->n_bins == kBins, "out->n_bins=%u != ANOMOD_HIST_BINS=%u",
+                     out->n_bins, kBins);
+  ANOMOD_CHECK_LOCAL(ctx, local, n < max_launch_spans(),
+                     "%llu edge records: at most 2^32 - 2 per call", (unsigned long long)n);
+  const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
+  const Layout L(E, 0);
+  if (local == ANOMOD_OK) local = bind(ctx);
+  if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
+  if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.end_small - L.off_err);
+  if (int rc = comm_agree(ctx, local)) return rc;
+  const Table tab = table_at(ctx, L, E);
+  if (int rc = table_clear(ctx, L, tab, E)) return rc;
+  // the pair form for a set known to fit it, else the compact form (no probe
+  // chain: nothing to saturate), which measures whether the pair form would do
+  int form = *hist_form;
+  if (const char* f = getenv("ANOMOD_HIST_FORM")) form = !strcmp(f, "pair") ? 0 : 1;
+  const uint64_t keys = (uint64_t)E * kBins + 1;
+  const bool lds_hist = keys < (1ull << 31);
+  KernelFn1 fn = nullptr;
+  int ht = kHtCompact;
+#define ANOMOD_REC(H, S_) fn = edge_rec_kernel<H, S_>, ht = H
+  if (!lds_hist) ANOMOD_REC(kHtHbm, kStHbm);
+  else if (E <= kLdsEdges && form == 0) ANOMOD_REC(kHtPair, kStDirect);
+  else if (E <= kLdsEdges) ANOMOD_REC(kHtCompact, kStDirect);
+  else if (E <= kWideEdges && form == 0) ANOMOD_REC(kHtPair, kStWide);
+  else if (E <= kWideEdges) ANOMOD_REC(kHtCompact, kStWide);
+  else ANOMOD_REC(kHtCompact, kStSlot);
+#undef ANOMOD_REC
+  if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
+  if (n > 0) {
+    int per_cu = 0;
+    ANOMOD_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per_cu, reinterpret_cast<const void*>(fn), kThreads, 0));
+    const uint64_t want = (n + (uint64_t)kThreads * kRecLoad - 1) / ((uint64_t)kThreads * kRecLoad);
+    const uint64_t grid = std::min<uint64_t>((uint64_t)ctx->num_cus * (per_cu > 0 ? per_cu : 1), want);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, rec, n, E, tab);
+    ANOMOD_HIP(ctx, hipGetLastError());
+  }
+  if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
+  unsigned long long ovf[2] = {0ull, 0ull};
+  if (int rc = table_finish(ctx, L, tab, E, out, ovf)) return rc;
+  // what was learned: a compact run whose fullest workgroup used at most half
+  // the pair table's slots says pair; a pair run that overflowed, compact
+  if (n > 0 && lds_hist) {
+    if (ht == kHtCompact && *hist_form < 0) *hist_form = ovf[1] <= kPairSlots / 2 ? 0 : 1;
+    if (ht == kHtPair && ovf[0] * 64ull > n) *hist_form = 1;
+  }
+  return ANOMOD_OK;
+}
+
 }  // namespace anomod
 
 using namespace anomod;
@@ -1704,34 +1889,8 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   if (local == ANOMOD_OK) local = ensure_table(ctx, L.bytes);
   if (local == ANOMOD_OK) local = ensure_host_stage(ctx, L.end_small - L.off_err);
   if (int rc = comm_agree(ctx, local)) return rc;
-  char* base = static_cast<char*>(ctx->d_table);
-  Table tab{};  // keys = nullptr: the table forms, not the exact-quantile keys
-  tab.hist = reinterpret_cast<unsigned long long*>(base + L.off_hist);
-  tab.err = reinterpret_cast<unsigned long long*>(base + L.off_err);
-  tab.sum = reinterpret_cast<unsigned long long*>(base + L.off_sum);
-  tab.mn = reinterpret_cast<unsigned int*>(base + L.off_mn);
-  tab.mx = reinterpret_cast<unsigned int*>(base + L.off_mx);
-  tab.ctr = reinterpret_cast<unsigned long long*>(base + L.off_ctr);
-  tab.big = reinterpret_cast<unsigned long long*>(base + L.off_big);
-  tab.big_list = reinterpret_cast<unsigned long long*>(base + L.off_list());
-  tab.bpar = reinterpret_cast<uint16_t*>(base + L.off_bpar);
-  tab.ovf = reinterpret_cast<unsigned long long*>(base + L.off_ovf);
-  tab.nleft = reinterpret_cast<unsigned long long*>(base + L.off_nleft);
-  tab.left = reinterpret_cast<unsigned long long*>(base + L.off_left);
-  tab.mode = kModeNormal;
-  tab.kb = 1;
-  while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
-  auto* count = reinterpret_cast<unsigned long long*>(base + L.off_count);
-  auto* p50 = reinterpret_cast<double*>(base + L.off_p50);
-  auto* p99 = reinterpret_cast<double*>(base + L.off_p99);
-
-  {
-    const uint64_t nz = L.off_count / 8;  // hist|err|sum|mx|ctr|big
-    const uint64_t blocks = std::min<uint64_t>((nz / 2 + 255) / 256 + 1, 4ull * ctx->num_cus);
-    hipLaunchKernelGGL(edge_table_init_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
-                       reinterpret_cast<unsigned long long*>(base), nz, tab.mn, E);
-    ANOMOD_HIP(ctx, hipGetLastError());
-  }
+  const Table tab = table_at(ctx, L, E);
+  if (int rc = table_clear(ctx, L, tab, E)) return rc;
 
   if (spans->n_traces > 0)
     if (int rc = probe_order(ctx, spans, tab.big + 3)) return rc;  // scratch: big counters' 4th word
@@ -1766,54 +1925,13 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     if (big_cap) ANOMOD_HIP(ctx, launch_big_for(ctx, spans, S, E, tab));
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
-
-  // Any attached communicator merges, a 1-rank one included (an identity
-  // reduce, so the RCCL call sequence is exercised on a single-GPU box too).
-  if (comm_attached(ctx)) {
-    if (int rc = stage_begin(ctx, kStageEdgeReduce)) return rc;
-    if (int rc = coll_begin(ctx)) return rc;
-    // hist | err | sum are contiguous u64: one sum all-reduce.
-    if (int rc = coll_allreduce(ctx, base, (size_t)E * kBins + 2ull * E, kCollU64, kCollSum))
-      return rc;
-    if (int rc = coll_allreduce(ctx, tab.mn, E, kCollU32, kCollMin)) return rc;
-    if (int rc = coll_allreduce(ctx, tab.mx, E, kCollU32, kCollMax)) return rc;
-    if (int rc = coll_end(ctx)) return rc;
-    if (int rc = stage_end(ctx, kStageEdgeReduce)) return rc;
-  }
-
-  if (int rc = stage_begin(ctx, kStageEdgeFinal)) return rc;
-  hipLaunchKernelGGL(edge_finalize_kernel, dim3(E), dim3(kWave), 0, ctx->stream, tab, count, p50,
-                     p99);
-  ANOMOD_HIP(ctx, hipGetLastError());
-  if (int rc = stage_end(ctx, kStageEdgeFinal)) return rc;
-
-  // The per-edge vectors come back in one D2H into pinned staging, then
-  // fan out on the host; the histogram (when asked for) goes straight.
-  const size_t small = L.end_small - L.off_err;
-  ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, base + L.off_err, small, hipMemcpyDeviceToHost,
-                                 ctx->stream));
-  if (out->hist)
-    ANOMOD_HIP(ctx, hipMemcpyAsync(out->hist, tab.hist, (size_t)E * kBins * 8ull,
-                                   hipMemcpyDeviceToHost, ctx->stream));
-  if (int rc = stream_wait(ctx)) return rc;
-  const char* hs = static_cast<const char*>(ctx->h_stage);
-  auto fan = [&](void* dst, size_t off, size_t bytes) {  // off: device layout offset
-    if (dst) memcpy(dst, hs + (off - L.off_err), bytes);
-  };
-  fan(out->count, L.off_count, E * 8ull);
-  fan(out->errors, L.off_err, E * 8ull);
-  fan(out->sum_us, L.off_sum, E * 8ull);
-  fan(out->min_us, L.off_mn, E * 4ull);
-  fan(out->max_us, L.off_mx, E * 4ull);
-  fan(out->p50_us, L.off_p50, E * 8ull);
-  fan(out->p99_us, L.off_p99, E * 8ull);
+  unsigned long long ovf[2] = {0ull, 0ull};
+  if (int rc = table_finish(ctx, L, tab, E, out, ovf)) return rc;
   // The set's form from here on: compact when a workgroup of a first
   // aggregation stopped at a saturated pair table, or when more than 1/64 of
   // the spans were counted in HBM past a full one (the set touches more (edge,
   // bin) keys than 8 Ki slots hold, e.g. random call trees over every service
   // pair); else pair.  Same results either way.
-  unsigned long long ovf[2] = {0ull, 0ull};
-  memcpy(ovf, hs + (L.off_ovf - L.off_err), 16);
   if (pk.ht == kHtPair) {
     if (ovf[1] > 0 || ovf[0] * 64ull > spans->n_spans) spans->hist_form = 1;
     else if (spans->hist_form < 0) spans->hist_form = 0;

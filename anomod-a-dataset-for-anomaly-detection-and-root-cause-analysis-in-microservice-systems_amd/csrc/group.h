@@ -100,6 +100,11 @@ BucketGeom bucket_geom(uint64_t n);
 // Runs the bucket path over `in` (ws sized by ensure_group_ws).  *fallback =
 // true when a bucket outgrew the large per-bucket kernel: the caller groups
 // with the LSD path instead (results are identical; only speed differs).
-int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback);
+// With erec (the fused ungrouped aggregation): no grouped columns; every
+// span's edge record (parent service row * S + service) << 33 | error << 32 |
+// duration goes to erec[grouped position] instead (*fallback also when a
+// bucket of long traces needs the unfused path).
+int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback,
+                     uint64_t* erec = nullptr, uint32_t S = 0);
 
 }  // namespace anomod

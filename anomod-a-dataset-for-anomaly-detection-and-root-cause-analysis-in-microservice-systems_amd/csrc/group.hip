@@ -907,6 +907,31 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   }
   GroupResult g;
   if (rc == ANOMOD_OK) rc = bind(ctx);
+  // Fused path (bucket grouping only): the buckets write one 8-B edge record
+  // per span instead of the grouped columns, and the edge table is taken from
+  // those records — no grouped columns, no trace_ptr, no walk over them.  A
+  // set whose buckets hold traces of thousands of spans side by side (or
+  // ANOMOD_UNGROUPED_FUSED=0) takes the unfused path below.
+  const char* fz = std::getenv("ANOMOD_UNGROUPED_FUSED");
+  const uint64_t n = spans->n_spans;
+  if (rc == ANOMOD_OK && n > 0 && !force_lsd() && !(fz && fz[0] == '0') && n_services >= 1 &&
+      n_services <= 4096 && spans->max_svc < n_services && n <= 0xFFFFFFFFull - 4096) {
+    rc = ensure_group_ws(ctx, n);
+    bool fallback = true;
+    if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
+    if (rc == ANOMOD_OK) {
+      uint64_t* erec = reinterpret_cast<uint64_t*>(ctx->group_ws->aos[1]);
+      rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
+      if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
+      if (rc == ANOMOD_OK && !fallback) {
+        ctx->group_path = 1;
+        ctx->group_levels = g.passes;
+        ctx->group_bits = g.bits;
+        return edge_aggregate_records(ctx, erec, n, n_services, &spans->hist_form, out);
+      }
+    }
+    if (rc != ANOMOD_OK) return comm_agree(ctx, rc);
+  }
   if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
   if (rc == ANOMOD_OK) rc = group_run(ctx, spans, &g);
   if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);

@@ -268,3 +268,47 @@ def test_group_pair_key_collisions(ctx, env_knob, avg):
     _assert_grouped_equal(g.download(), _oracle_grouped(flat))
     assert ctx.group_info()["path"] == "bucket"
     assert ctx.group_info()["levels"] == (2 if avg else 1)
+
+
+@pytest.mark.parametrize("S,max_len,form", [(12, 24, None), (46, 60, None), (20, 40, None),
+                                            (12, 24, "pair"), (100, 30, None)])
+def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, form):
+    """anomod_edge_aggregate_ungrouped's fused path (the buckets write one
+    edge record per span, the table is taken from those records) against the
+    unfused one (ANOMOD_UNGROUPED_FUSED=0: grouped columns, then the chunk
+    walk) and the oracle: SN / TrainTicket widths (direct, wide, slot stats),
+    wide latencies (a compact-form run that learns the set's form), duplicate
+    ids, orphans, interleaved arrival."""
+    if form:
+        env_knob("ANOMOD_HIST_FORM", form)
+    rng = np.random.default_rng(S * 3 + max_len)
+    sp = _with_trace_hashes(_random_spanset(rng, S, 40000, max_len, dup=0.03,
+                                            wide_dur=S == 20), rng)
+    flat = _interleave(sp, rng, "time")
+    ref = native.edge_aggregate(_oracle_grouped(flat))
+    dev = ctx.upload_ungrouped(flat)
+    fused = ctx.edge_aggregate(dev)
+    assert ctx.group_info()["path"] == "bucket"
+    assert_table_equal(fused, ref)
+    monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "0")
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    monkeypatch.delenv("ANOMOD_UNGROUPED_FUSED")
+    if form is None:  # learned from the compact run (wide latencies: far too many keys)
+        assert dev.hints[1] in ((1,) if S == 20 else (0, 1))
+    assert_table_equal(ctx.edge_aggregate(dev), ref)  # again, with the learned form
+    dev.free()
+
+
+def test_ungrouped_fused_long_traces_fall_back(ctx):
+    """Buckets of several traces of thousands of spans (beyond the large
+    bucket kernel) leave the fused path for the unfused one; the table is
+    the oracle's either way."""
+    rng = np.random.default_rng(90)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 5000, 16, dup=0.02), rng)
+    base = rng.integers(0, 2**64, 1, dtype=np.uint64)[0] & np.uint64(0xFFFFFFFFFF000000)
+    low = rng.choice(2**24, 3, replace=False).astype(np.uint64)
+    big = _with_trace_hashes(_random_spanset(rng, 12, 0, 0, dup=0.02, lens=[4000, 4000, 3000]),
+                             rng, _unmix64((base | low).astype(np.uint64)))
+    flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "random")
+    dev = ctx.upload_ungrouped(flat)
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(_oracle_grouped(flat)))
