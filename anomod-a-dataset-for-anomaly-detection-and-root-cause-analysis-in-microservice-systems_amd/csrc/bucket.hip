@@ -781,69 +781,33 @@ __device__ void bucket_edges(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m
   }
 }
 
-// Bucket c = [bstart[c], bstart[c + 1]) of the pairs `pin` (in arrival order
-// inside the bucket; every key shares its top T bits).  Split once more by the
-// next 9 key bits (stable); a sub-bucket holding one key is already in
-// arrival order, a mixed one ranks each pair by compares: rank = #{smaller
-// pair} (a pair orders by (key bits, position) and positions are arrival
-// order).  The records come from `rec` by position.  Writes the grouped
-// columns of the bucket, its trace starts over the bucket's own pairs
-// (pin[bstart[c] + ordinal], read before) and the trace count dcnt[c].
-template <int W, int PER, bool EDGE>
-__device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t* __restrict__ pin,
-                                const GRec* __restrict__ rec, SoaOut out, EdgeOut eo,
-                                const uint32_t* __restrict__ bstart, int kshift,
-                                uint32_t* __restrict__ dcnt, bool small,
-                                uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
-                                uint32_t over_cap, unsigned long long* __restrict__ too_big) {
+// Bucket c = [a0, a0 + m) of the pairs `pin` (in arrival order inside the
+// bucket; every key shares its top T bits), its pairs k / v and — REG, the
+// small kernel — its records ra / rb already in registers (the big kernel
+// gathers the keys itself).  Split once more by the next 9 key bits (stable);
+// a sub-bucket holding one key is already in arrival order, a mixed one ranks
+// each pair by compares: rank = #{smaller pair} (a pair orders by (key bits,
+// position) and positions are arrival order).  The records come from `rec` by
+// position.  Writes the grouped columns of the bucket, its trace starts over
+// the bucket's own pairs (pin[a0 + ordinal], read before) and the trace count
+// dcnt[c] — or, EDGE, its edge records.
+template <int W, int PER, bool EDGE, int R>
+__device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
+                            uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+                            EdgeOut eo, int kshift, uint32_t* __restrict__ dcnt,
+                            const uint64_t (&k)[PER], const bool (&v)[PER], const uint4 (&ra)[R],
+                            const uint4 (&rb)[R]) {
   constexpr int kCap = W * PER, kNW = W / kWv;
   static_assert(W >= kSub, "one thread per sub-digit");
+  constexpr bool REG = R == PER;
   auto& P = L.u.pre;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
-  if (m > (uint32_t)kCap) {
-    if (small) {
-      if (tid == 0) {
-        const unsigned long long i = atomicAdd(over_n, 1ull);
-        if (i < over_cap) over[i] = c;
-        else atomicAdd(too_big, 1ull);
-      }
-      return;
-    }
-    // (the fused aggregation leaves such a bucket — traces of thousands of
-    // spans side by side — to the unfused path: too_big)
-    if constexpr (!EDGE && sizeof(BucketLds<W, PER, EDGE>) >= 81920 + 16 + 4 * (W / kWv))
-      bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, pin, rec, out, dcnt, too_big);
-    else if (tid == 0)
-      atomicAdd(too_big, 1ull);
-    return;
-  }
-  if (m == 0) {
-    if (tid == 0 && !EDGE) dcnt[c] = 0;
-    return;
-  }
-  // REG (the small kernel): whole records held in registers from the gather
-  // on; else only their keys, the records gathered again when written.
-  constexpr bool REG = PER <= 4;
-  uint64_t k[PER], fk[PER];
+  (void)kCap;
+  uint64_t fk[PER];
   uint32_t e[PER], off[PER];
-  bool v[PER];
-  uint4 ra[REG ? PER : 1], rb[REG ? PER : 1];
+  if constexpr (!REG) {
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-    v[j] = p < m;
-    k[j] = v[j] ? pin[a0 + p] : 0ull;
-  }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {  // the gathers: issued together, after every pair load
-    if constexpr (REG) {
-      const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
-      ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
-      rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
-    } else {
-      fk[j] = v[j] ? rec[(uint32_t)k[j]].h : 0ull;
-    }
+    for (int j = 0; j < PER; ++j) fk[j] = v[j] ? rec[(uint32_t)k[j]].h : 0ull;
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -1038,6 +1002,64 @@ __device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t
   if (tid == 0) dcnt[c] = nt;
 }
 
+
+// One bucket by one workgroup: the size checks (over-size buckets listed for
+// the big kernel, or the huge walk), the pair loads and gathers, the body.
+template <int W, int PER, bool EDGE>
+__device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t* __restrict__ pin,
+                                const GRec* __restrict__ rec, SoaOut out, EdgeOut eo,
+                                const uint32_t* __restrict__ bstart, int kshift,
+                                uint32_t* __restrict__ dcnt, bool small,
+                                uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n,
+                                uint32_t over_cap, unsigned long long* __restrict__ too_big) {
+  constexpr int kCap = W * PER;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
+  if (m > (uint32_t)kCap) {
+    if (small) {
+      if (tid == 0) {
+        const unsigned long long i = atomicAdd(over_n, 1ull);
+        if (i < over_cap) over[i] = c;
+        else atomicAdd(too_big, 1ull);
+      }
+      return;
+    }
+    // (the fused aggregation leaves such a bucket — traces of thousands of
+    // spans side by side — to the unfused path: too_big)
+    if constexpr (!EDGE && sizeof(BucketLds<W, PER, EDGE>) >= 81920 + 16 + 4 * (W / kWv))
+      bucket_huge<W>(reinterpret_cast<unsigned char*>(&L), c, a0, m, pin, rec, out, dcnt, too_big);
+    else if (tid == 0)
+      atomicAdd(too_big, 1ull);
+    return;
+  }
+  if (m == 0) {
+    if (tid == 0 && !EDGE) dcnt[c] = 0;
+    return;
+  }
+  // REG (the small kernel): whole records held in registers from the gather
+  // on; else only their keys, the records gathered again when written.
+  constexpr bool REG = PER <= 4;
+  constexpr int R = REG ? PER : 1;
+  uint64_t k[PER];
+  bool v[PER];
+  uint4 ra[R], rb[R];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    v[j] = p < m;
+    k[j] = v[j] ? pin[a0 + p] : 0ull;
+  }
+  if constexpr (REG) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {  // the gathers: issued together, after every pair load
+      const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
+      ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+      rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  bucket_body<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, eo, kshift, dcnt, k, v, ra, rb);
+}
+
 __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
     uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
     const uint32_t* __restrict__ bstart, int kshift, uint32_t* __restrict__ dcnt,
@@ -1047,6 +1069,85 @@ __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
   bucket_sort_one<kSmallW, kSmallPer, false>(L, (uint32_t)xcd_tile(blockIdx.x, gridDim.x, nx), pin,
                                              rec, out, EdgeOut{}, bstart, kshift, dcnt, true, over,
                                              over_n, over_cap, too_big);
+}
+
+// Persistent, pipelined form of the small bucket kernel (the default): the
+// workgroups take buckets b, b + G, b + 2G, ... (so the buckets in flight are
+// neighbours: every XCD inside one level-A bucket, whose records the gathers
+// then find in the Infinity Cache), and while one sorts bucket c, the records
+// of c + G are being gathered and the pairs of c + 2G loaded — the gather
+// latency hides behind the sort instead of stalling it.
+#ifndef ANOMOD_BK_PIPE_MINB
+#define ANOMOD_BK_PIPE_MINB 2  // waves per SIMD the registers must allow
+#endif
+template <bool EDGE>
+__global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_kernel(
+    uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, uint32_t nbk, int kshift, uint32_t* __restrict__ dcnt,
+    uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ BucketLds<kSmallW, kSmallPer, EDGE> L;
+  constexpr int PER = kSmallPer, kCap = kSmallW * kSmallPer;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const uint32_t G = gridDim.x;
+  struct Slot {
+    uint32_t a0, m;
+    uint64_t k[PER];
+    bool v[PER];
+  };
+  auto load = [&](Slot& s, uint32_t c) {
+    s.a0 = 0u;
+    s.m = 0u;
+    if (c < nbk) {
+      s.a0 = bstart[c];
+      s.m = bstart[c + 1] - s.a0;
+    }
+    const bool fits = s.m <= (uint32_t)kCap;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+      s.v[j] = fits && p < s.m;
+      s.k[j] = s.v[j] ? pin[s.a0 + p] : 0ull;
+    }
+  };
+  auto gather = [&](const Slot& s, uint4 (&ra)[PER], uint4 (&rb)[PER]) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)s.k[j]);
+      ra[j] = s.v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+      rb[j] = s.v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  Slot cur, nxt, nx2;
+  uint4 ra[PER], rb[PER], ran[PER], rbn[PER];
+  uint32_t c = blockIdx.x;
+  load(cur, c);
+  gather(cur, ra, rb);
+  load(nxt, c + G);
+  for (; c < nbk; c += G) {
+    gather(nxt, ran, rbn);
+    load(nx2, c + 2u * G);
+    if (cur.m > (uint32_t)kCap) {  // for the big kernel (or, EDGE, the unfused path)
+      if (tid == 0) {
+        const unsigned long long i = atomicAdd(over_n, 1ull);
+        if (i < over_cap) over[i] = c;
+        else atomicAdd(too_big, 1ull);
+      }
+    } else if (cur.m == 0u) {
+      if (tid == 0 && !EDGE) dcnt[c] = 0;
+    } else {
+      bucket_body<kSmallW, PER, EDGE, PER>(L, c, cur.a0, cur.m, pin, rec, out, eo, kshift, dcnt,
+                                           cur.k, cur.v, ra, rb);
+    }
+    __syncthreads();  // the next bucket reuses the LDS
+    cur = nxt;
+    nxt = nx2;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      ra[j] = ran[j];
+      rb[j] = rbn[j];
+    }
+  }
 }
 
 // The fused ungrouped aggregation's bucket kernels: the same sort, then
@@ -1324,10 +1425,27 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   // large one (<= 8192 spans, or any size holding one trace); the sub-split
   // takes the 9 pair bits below the DB bits level B took
   const int kshift = 64 - g.DB - kSubBits;
+  // the persistent pipelined bucket kernel (ANOMOD_BK_PIPE=0: one workgroup
+  // per bucket), as many workgroups as are resident at once
+  const bool pipe = env_int("ANOMOD_BK_PIPE", 1) != 0;
+  auto pipe_grid = [&](const void* fn) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSmallW, 0) != hipSuccess)
+      per_cu = 1;
+    return (unsigned)std::min<uint64_t>(nbk, (uint64_t)std::max(ctx->num_cus, 1) *
+                                                 (uint64_t)std::max(per_cu, 1));
+  };
   if (eo) {  // the fused ungrouped aggregation: edge records, no columns, no trace_ptr
-    hipLaunchKernelGGL(bk_bucket_edge_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
-                       recs, *eo, bstart, kshift, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
-                       ws->misc + kMiscTooBig);
+    if (pipe)
+      hipLaunchKernelGGL(bk_bucket_pipe_kernel<true>,
+                         dim3(pipe_grid(reinterpret_cast<const void*>(bk_bucket_pipe_kernel<true>))),
+                         dim3(kSmallW), 0, st, pin, recs, SoaOut{}, *eo, bstart, (uint32_t)nbk,
+                         kshift, nullptr, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                         ws->misc + kMiscTooBig);
+    else
+      hipLaunchKernelGGL(bk_bucket_edge_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
+                         recs, *eo, bstart, kshift, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                         ws->misc + kMiscTooBig);
     hipLaunchKernelGGL(bk_bucket_edge_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
                        dim3(kBigW), 0, st, pin, recs, *eo, bstart, kshift, ws->over,
                        ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
@@ -1341,9 +1459,16 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
     res->bucket = true;
     return ANOMOD_OK;
   }
-  hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin, recs, cols,
-                     bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
-                     ws->misc + kMiscTooBig, (xk & 4) ? 8u : 1u);
+  if (pipe)
+    hipLaunchKernelGGL(bk_bucket_pipe_kernel<false>,
+                       dim3(pipe_grid(reinterpret_cast<const void*>(bk_bucket_pipe_kernel<false>))),
+                       dim3(kSmallW), 0, st, pin, recs, cols, EdgeOut{}, bstart, (uint32_t)nbk,
+                       kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                       ws->misc + kMiscTooBig);
+  else
+    hipLaunchKernelGGL(bk_bucket_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin, recs,
+                       cols, bstart, kshift, ws->dcnt, ws->over, ws->misc + kMiscBigN,
+                       (uint32_t)nbk, ws->misc + kMiscTooBig, (xk & 4) ? 8u : 1u);
   hipLaunchKernelGGL(bk_bucket_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
                      dim3(kBigW), 0, st, pin, recs, cols, bstart, kshift, ws->dcnt, ws->over,
                      ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);

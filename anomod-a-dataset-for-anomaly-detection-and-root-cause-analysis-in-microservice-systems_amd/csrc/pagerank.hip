@@ -55,6 +55,9 @@ struct anomod_graph {
   uint32_t last_path = 0;   // ANOMOD_PPR_PATH_* of the last single-vector solve
   uint32_t fallbacks = 0;   // persistent solves rerun per launch (barrier timed out)
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
+  // persistent solve: one fresh vector per iteration (see ppr_persistent_kernel)
+  double* ring = nullptr;
+  uint64_t ring_slots = 0;  // vectors of `grid * 256` doubles the ring holds
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
   uint32_t exec_iters = 0;
@@ -175,15 +178,16 @@ __device__ __forceinline__ void ppr_iter_body(
     const uint32_t b = in_ptr[r], e = in_ptr[r + 1];
     // In-degrees are short (uniform callees): one lane per row, kEdgeBatch
     // (col, w) pairs loaded together, then the x gathers together (lanes past
-    // the row's end gather x[0] with weight 0: adds +0.0, the same bits as
-    // skipping them).
+    // the row's end gather their own row's x with weight 0: adds +0.0, the
+    // same bits as skipping them; padding with x[0] sent every padded load of
+    // the grid to one address).
     for (uint32_t k0 = b; k0 < e; k0 += kEdgeBatch) {
       uint32_t c[kEdgeBatch];
       float wv[kEdgeBatch];
 #pragma unroll
       for (int j = 0; j < kEdgeBatch; ++j) {
         const bool ok = k0 + j < e;
-        c[j] = ok ? in_col[k0 + j] : 0u;
+        c[j] = ok ? in_col[k0 + j] : r;  // padding: the row's own x (weight 0)
         wv[j] = ok ? in_w[k0 + j] : 0.f;
       }
       double xv[kEdgeBatch];
@@ -305,6 +309,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
 // the per-launch kernel's whatever SUB, only the number of workgroups meeting
 // at the grid barrier shrinks (391 -> 98 at N = 10^5 with SUB = 4).
 constexpr uint32_t kLdsEdgeBytes = 128 * 1024;  // (col, w) staging per workgroup
+constexpr uint64_t kRingBytes = 2ull << 30;       // most HBM the per-iteration vectors take
 #ifndef ANOMOD_PPR_GATHER
 #define ANOMOD_PPR_GATHER 4
 #endif
@@ -316,12 +321,22 @@ constexpr int kPBatch = ANOMOD_PPR_GATHER;  // x gathers in flight per lane (per
 #define ANOMOD_PPR_ABL 0
 #endif
 
-template <int SUB>
+// RING: iteration `it` writes its vector to a slot of `ring` no load of this
+// launch has touched before (slot it; iteration 0 reads x0, which an earlier
+// launch wrote) and reads the previous one, so the x gathers can be PLAIN
+// loads: a line of a fresh slot cannot be stale in any L1 or L2 (it was never
+// cached there), the first gather of it misses to the coherent memory side,
+// and later gathers of that line on the same XCD hit its L2 — against one
+// agent-scope (sc1) load per gather that goes to the memory side every time.
+// The owner's stores stay agent-scope and are drained before the grid
+// barrier, as without the ring.
+template <int SUB, bool RING>
 __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
     const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
     const double* __restrict__ p, double alpha, double x0v, double* x0, double* x1,
-    unsigned long long* acc, uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit) {
+    unsigned long long* acc, uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit,
+    double* ring, uint64_t slot) {
   constexpr uint32_t kLdsE = SUB == 1 ? 6144u : kLdsEdgeBytes / 8u;  // SUB 1: 48 KB, 3 per CU
   __shared__ uint32_t lcol[kLdsE];
   __shared__ float lw[kLdsE];
@@ -356,8 +371,8 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t it = 0; it < iters; ++it) {
     const bool odd = it & 1u;
-    const double* x_in = odd ? x1 : x0;
-    double* x_out = odd ? x0 : x1;
+    const double* x_in = RING ? (it == 0 ? x0 : ring + (uint64_t)(it - 1u) * slot) : odd ? x1 : x0;
+    double* x_out = RING ? ring + (uint64_t)it * slot : odd ? x0 : x1;
     const int rr = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
     // wave 0 first issues the reads of the previous iteration's slots — its
     // dangling mass and (tolerance mode) its L1 change, whose stopping test
@@ -375,8 +390,8 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
     double sum = 0.0;
     if (!(ANOMOD_PPR_ABL & 1) && r < N) {
       // kPBatch gathers in flight per lane (in-degrees ~ Poisson(7) here: one
-      // round for nearly every row); lanes past the row's end gather x[0]
-      // with weight 0 (adds +0.0: the same bits as skipping them)
+      // round for nearly every row); lanes past the row's end gather their own
+      // row's x with weight 0 (adds +0.0: the same bits as skipping them)
       for (uint32_t k0 = rb; k0 < re; k0 += kPBatch) {
         uint32_t c[kPBatch];
         float wv[kPBatch];
@@ -384,13 +399,14 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_persistent_kernel(
         for (int j = 0; j < kPBatch; ++j) {
           const uint32_t k = k0 + j, li = k - e0;
           const bool ok = k < re;
-          c[j] = !ok ? 0u : li < nc ? lcol[li] : in_col[k];
+          c[j] = !ok ? r : li < nc ? lcol[li] : in_col[k];
           wv[j] = !ok ? 0.f : li < nc ? lw[li] : in_w[k];
         }
         double xv[kPBatch];
 #pragma unroll
         for (int j = 0; j < kPBatch; ++j)
-          xv[j] = __hip_atomic_load(&x_in[c[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          xv[j] = RING ? x_in[c[j]]
+                       : __hip_atomic_load(&x_in[c[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int j = 0; j < kPBatch; ++j)
           if (k0 + j < re) sum = ppr_edge(sum, xv[j], wv[j]);
@@ -493,7 +509,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
 #pragma unroll
       for (int j = 0; j < kEdgeBatch; ++j) {
         const bool ok = k0 + j < e;
-        c[j] = ok ? in_col[k0 + j] : 0u;
+        c[j] = ok ? in_col[k0 + j] : r;  // padding: the row's own x (weight 0)
         wv[j] = ok ? in_w[k0 + j] : 0.f;
       }
 #pragma unroll
@@ -546,10 +562,14 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
 constexpr int kPprSub = ANOMOD_PPR_SUB;  // 256-row blocks per persistent workgroup
 using PersistentFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*,
                               const uint8_t*, const double*, double, double, double*, double*,
-                              unsigned long long*, uint32_t, double, unsigned int*, uint32_t);
-PersistentFn persistent_fn(int sub) {
-  return sub >= 4 ? ppr_persistent_kernel<4> : sub == 2 ? ppr_persistent_kernel<2>
-                                                        : ppr_persistent_kernel<1>;
+                              unsigned long long*, uint32_t, double, unsigned int*, uint32_t,
+                              double*, uint64_t);
+PersistentFn persistent_fn(int sub, bool ring) {
+  if (ring)
+    return sub >= 4 ? ppr_persistent_kernel<4, true> : sub == 2 ? ppr_persistent_kernel<2, true>
+                                                                : ppr_persistent_kernel<1, true>;
+  return sub >= 4 ? ppr_persistent_kernel<4, false> : sub == 2 ? ppr_persistent_kernel<2, false>
+                                                               : ppr_persistent_kernel<1, false>;
 }
 
 void free_graph(anomod_graph* g) {
@@ -558,7 +578,7 @@ void free_graph(anomod_graph* g) {
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
   if (g->h_pin) (void)hipHostFree(g->h_pin);
   void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,    g->x[0], g->x[1],
-                g->acc,    g->bp,     g->bx[0], g->bx[1],    g->bacc, g->bar};
+                g->acc,    g->bp,     g->bx[0], g->bx[1],    g->bacc, g->bar, g->ring};
   for (void* q : ps)
     if (q) (void)hipFree(q);
   delete g;
@@ -841,7 +861,7 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
     // when another process holds CUs: the grid barrier's bounded spin then
     // ends the launch and the solve reruns per launch (below), not a hang.
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_fn(sub),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_fn(sub, true),
                                                      kPprThreads * sub, 0) != hipSuccess)
       per_cu = 0;
     g->coop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
@@ -862,9 +882,23 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   if (persistent) {
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
-    hipLaunchKernelGGL(persistent_fn(sub), dim3(pgrid), dim3(kPprThreads * sub), 0, ctx->stream,
-                       g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha, x0v,
-                       g->x[0], g->x[1], g->acc, iters, ntol, g->bar, spin);
+    // a fresh vector slot per iteration (grow-only; ANOMOD_PPR_RING=0 or more
+    // than kRingBytes of slots: the two-buffer form with agent-scope gathers)
+    const uint64_t slot = (uint64_t)g->grid * kRowsPerBlock;
+    const char* ring_env = getenv("ANOMOD_PPR_RING");
+    bool ring = !(ring_env && ring_env[0] == '0') && (uint64_t)iters * slot * 8 <= kRingBytes;
+    if (ring && g->ring_slots < iters) {
+      if (g->ring) ANOMOD_HIP(ctx, hipFree(g->ring));
+      g->ring = nullptr;
+      g->ring_slots = 0;
+      if (hipMalloc(&g->ring, (uint64_t)iters * slot * 8) == hipSuccess) g->ring_slots = iters;
+      else ring = false;
+      (void)hipGetLastError();
+    }
+    hipLaunchKernelGGL(persistent_fn(sub, ring), dim3(pgrid), dim3(kPprThreads * sub), 0,
+                       ctx->stream, g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha,
+                       x0v, g->x[0], g->x[1], g->acc, iters, ntol, g->bar, spin,
+                       ring ? g->ring : nullptr, slot);
     ANOMOD_HIP(ctx, hipGetLastError());
     if (int rc = stage_end(ctx, kStagePagerank)) return rc;  // the copies are not timed
     // the persistent solve leaves its result in x[0]: one copy, one wait
