@@ -464,8 +464,10 @@ class DeviceGraph:
     PATHS = {1: "graph", 2: "readback", 3: "persistent"}
 
     def last_solve(self) -> tuple[str, int]:
-        """(path of the last pagerank() solve, persistent-launch fallbacks so
-        far); the path is "graph" / "readback" / "persistent", with a
+        """(path of the last pagerank() / pagerank_batch() solve, persistent-
+        launch fallbacks so far); the path is "graph" / "readback" /
+        "persistent" (a per-launch batch reports "graph" for fixed iterations,
+        "readback" in tolerance mode), with a
         "fallback:" prefix when a persistent launch timed out at its grid
         barrier and the solve was rerun per launch."""
         path, fb = C.c_uint32(), C.c_uint32()

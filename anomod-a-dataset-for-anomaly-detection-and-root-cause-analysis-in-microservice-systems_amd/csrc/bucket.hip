@@ -55,7 +55,10 @@ using chunk::wave_sync;
 constexpr int kWv = 64;
 constexpr int kBThreads = 1024;                // scatter workgroup
 constexpr int kBWaves = kBThreads / kWv;       // 16
-constexpr int kBPer = 4;                       // records per thread
+#ifndef ANOMOD_BK_APER
+#define ANOMOD_BK_APER 4
+#endif
+constexpr int kBPer = ANOMOD_BK_APER;          // records per thread
 constexpr int kBTile = kBThreads * kBPer;      // 4096 records per level-A tile
 constexpr int kPPer = 16;                      // pairs per thread (level B)
 constexpr int kPTile = kBThreads * kPPer;      // 16384 pairs per level-B tile (128 KiB)
@@ -65,7 +68,10 @@ constexpr int kScanRows = 256;                 // tiles per block of the tile sc
 constexpr int kScanB = 16;                     // loads in flight per serial scan step
 constexpr int kSubBits = 9;                    // per-bucket split before the key compare
 constexpr int kSub = 1 << kSubBits;
-constexpr int kSmallW = 512, kSmallPer = 4;    // per-bucket kernel: 2048 spans
+#ifndef ANOMOD_BK_SPER
+#define ANOMOD_BK_SPER 4
+#endif
+constexpr int kSmallW = 512, kSmallPer = ANOMOD_BK_SPER;  // per-bucket kernel: 2048 spans
 constexpr int kBigW = 1024, kBigPer = 8;       // oversized buckets: 8192 spans
 constexpr int kDChunk = 4096;                  // entries per partial sum of the trace-count scan
 
@@ -331,7 +337,7 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_a_kernel(
     uint16_t wcnt[kBWaves][kNDMax];       // per-wave digit counts, then wave offsets
   };
   __shared__ Lds u;
-  __shared__ uint32_t tstart[kNDMax];     // tile-local start of each digit
+  __shared__ uint16_t tstart[kNDMax];     // tile-local start of each digit (<= kBTile)
   __shared__ uint32_t gbase[kNDMax];      // global start of each digit's run
   __shared__ uint32_t wsum[kBWaves];
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
@@ -401,7 +407,7 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_a_kernel(
   const uint32_t pre = block_excl_scan<kBWaves>(tot[0] + tot[1], wsum, &all);
   for (int i = 0; i < dpt; ++i) {
     const int dd = tid * dpt + i;
-    if (dd < nd) tstart[dd] = pre + (i ? tot[0] : 0u);
+    if (dd < nd) tstart[dd] = (uint16_t)(pre + (i ? tot[0] : 0u));
   }
   __syncthreads();
   uint32_t lp[kBPer];
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
                                              over_n, over_cap, too_big);
 }
 
-// Persistent, pipelined form of the small bucket kernel (the default): the
+// Persistent, pipelined form of the small bucket kernel (ANOMOD_BK_PIPE=1): the
 // workgroups take buckets b, b + G, b + 2G, ... (so the buckets in flight are
 // neighbours: every XCD inside one level-A bucket, whose records the gathers
 // then find in the Infinity Cache), and while one sorts bucket c, the records
@@ -1335,7 +1341,8 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   const uint64_t n = in->n_spans;
   const int na = 1 << g.DA;
   if ((1ull << g.T) > ws->bucket_cap || g.tilesB > ws->tile_cap ||  // sized for the geometry
-      g.DA > kDMax || g.DB > kDMax) {
+      g.DA > kDMax || g.DB > kDMax || (g.tilesA << g.DA) > ws->tcnt_words ||
+      (g.tilesB << kDMax) > ws->tcnt_words) {
     *fallback = true;
     return ANOMOD_OK;
   }
@@ -1425,9 +1432,10 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   // large one (<= 8192 spans, or any size holding one trace); the sub-split
   // takes the 9 pair bits below the DB bits level B took
   const int kshift = 64 - g.DB - kSubBits;
-  // the persistent pipelined bucket kernel (ANOMOD_BK_PIPE=0: one workgroup
-  // per bucket), as many workgroups as are resident at once
-  const bool pipe = env_int("ANOMOD_BK_PIPE", 1) != 0;
+  // one workgroup per bucket; ANOMOD_BK_PIPE=1: the persistent pipelined
+  // bucket kernel, as many workgroups as are resident at once (measured
+  // slower: 93 vs 64 ms grouping at 2^27 SN traces, gpurun_out/r4c_pipe_f0.log)
+  const bool pipe = env_int("ANOMOD_BK_PIPE", 0) != 0;
   auto pipe_grid = [&](const void* fn) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSmallW, 0) != hipSuccess)

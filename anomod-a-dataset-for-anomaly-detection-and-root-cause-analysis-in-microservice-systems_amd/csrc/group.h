@@ -66,6 +66,7 @@ struct GroupWs {
   uint32_t* part = nullptr;           // partial sums of the dcnt scan
   uint64_t bucket_cap = 0;            // 2^T the arrays above hold
   uint64_t tile_cap = 0;              // level-B tiles tmap holds
+  uint64_t tcnt_words = 0;            // u32 words of tcnt (tile x digit counts)
   unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
   void* block = nullptr;  // one allocation the device buffers are carved from
 };

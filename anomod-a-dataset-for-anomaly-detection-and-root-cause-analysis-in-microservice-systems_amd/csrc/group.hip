@@ -626,6 +626,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   ws->bucket_cap = 1ull << std::min(22, tmax + 11);  // + a retry with 11-bit level B
   ws->tile_cap = tiles + 2048;
   const size_t tcnt_words = std::max<size_t>(tiles * kDig, ws->tile_cap * 2048);
+  ws->tcnt_words = tcnt_words;
   const size_t bsum_words = (tiles / kTScanRows + 2) * 2048;
   const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
                           ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
@@ -909,12 +910,15 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   if (rc == ANOMOD_OK) rc = bind(ctx);
   // Fused path (bucket grouping only): the buckets write one 8-B edge record
   // per span instead of the grouped columns, and the edge table is taken from
-  // those records — no grouped columns, no trace_ptr, no walk over them.  A
-  // set whose buckets hold traces of thousands of spans side by side (or
-  // ANOMOD_UNGROUPED_FUSED=0) takes the unfused path below.
+  // those records — no grouped columns, no trace_ptr, no walk over them.
+  // Opt-in (ANOMOD_UNGROUPED_FUSED=1): measured slower than grouping then
+  // aggregating (71.0 + 2.1 vs 63.7 + 5.7 ms at 2^27 SN traces,
+  // gpurun_out/r4c_pipe_f*.log: the edge scan in LDS costs the bucket kernel
+  // more than the columns' write and re-read).  A set whose buckets hold
+  // traces of thousands of spans side by side takes the unfused path below.
   const char* fz = std::getenv("ANOMOD_UNGROUPED_FUSED");
   const uint64_t n = spans->n_spans;
-  if (rc == ANOMOD_OK && n > 0 && !force_lsd() && !(fz && fz[0] == '0') && n_services >= 1 &&
+  if (rc == ANOMOD_OK && n > 0 && !force_lsd() && fz && fz[0] == '1' && n_services >= 1 &&
       n_services <= 4096 && spans->max_svc < n_services && n <= 0xFFFFFFFFull - 4096) {
     rc = ensure_group_ws(ctx, n);
     bool fallback = true;

@@ -52,12 +52,15 @@ struct anomod_graph {
   unsigned int* bar = nullptr;
   int coop_blocks = -1;  // co-resident workgroups of the persistent kernel (-1: not queried)
   int coop_sub = 0;      // its 256-row blocks per workgroup
+  int bcoop_blocks = -1; // the same for the persistent batch kernel of width bcoop_kb
+  uint32_t bcoop_kb = 0;
+  bool bcoop_ring = false;
   uint32_t last_path = 0;   // ANOMOD_PPR_PATH_* of the last single-vector solve
   uint32_t fallbacks = 0;   // persistent solves rerun per launch (barrier timed out)
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
   // persistent solve: one fresh vector per iteration (see ppr_persistent_kernel)
   double* ring = nullptr;
-  uint64_t ring_slots = 0;  // vectors of `grid * 256` doubles the ring holds
+  uint64_t ring_bytes = 0;  // bytes the ring holds (single solves and batches share it)
   // cached fixed-iteration graph
   hipGraphExec_t exec = nullptr;
   uint32_t exec_iters = 0;
@@ -309,7 +312,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
 // the per-launch kernel's whatever SUB, only the number of workgroups meeting
 // at the grid barrier shrinks (391 -> 98 at N = 10^5 with SUB = 4).
 constexpr uint32_t kLdsEdgeBytes = 128 * 1024;  // (col, w) staging per workgroup
-constexpr uint64_t kRingBytes = 2ull << 30;       // most HBM the per-iteration vectors take
+constexpr uint64_t kRingBytes = 1ull << 30;       // most HBM the per-iteration vectors take
 #ifndef ANOMOD_PPR_GATHER
 #define ANOMOD_PPR_GATHER 4
 #endif
@@ -556,6 +559,186 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
     }
 }
 
+// All iterations of a K-vector batch in one launch: ppr_persistent_kernel's
+// grid barrier, LDS-staged in-edges and vector ring, with the per-vector
+// arithmetic, edge order, 256-row block partition, reduction tree and
+// fixed-point slots of ppr_batch_iter_kernel, so every column equals its
+// per-launch batch (and single-vector) solve bit for bit.  Tolerance mode:
+// every block reads iteration it-1's per-vector L1 changes at the top of
+// iteration it, freezes the converged vectors (carried unchanged, as the
+// host loop of the per-launch batch does) and stops once all are frozen.
+// The final vectors land in x0 ([N][K], node-major); bar[2] = iterations.
+template <int K, bool RING>
+__global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
+    uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
+    const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
+    const double* __restrict__ p, double alpha, double* x0, double* x1, unsigned long long* acc,
+    uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit, double* ring,
+    uint64_t slot) {
+  constexpr uint32_t kLdsE = 6144u;  // 48 KB of (col, w): 3 workgroups per CU
+  constexpr int S = kAccSlots * K;   // one accumulator block: K x kAccSlots
+  constexpr int kNW = kPprThreads / 64;
+  __shared__ uint32_t lcol[kLdsE];
+  __shared__ float lw[kLdsE];
+  __shared__ double red[2 * K * kNW];
+  __shared__ double s_dsum[K];
+  __shared__ uint32_t s_conv;
+  __shared__ int s_flag;
+  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
+  const uint32_t r0 = blockIdx.x * kRowsPerBlock;
+  const uint32_t r0e = r0 < N ? r0 : N;
+  const uint32_t r1 = r0 + kRowsPerBlock < N ? r0 + kRowsPerBlock : N;
+  const uint32_t e0 = in_ptr[r0e], e1 = in_ptr[r1];
+  const uint32_t nc = e1 - e0 < kLdsE ? e1 - e0 : kLdsE;
+  for (uint32_t i = threadIdx.x; i < nc; i += kPprThreads) {
+    lcol[i] = in_col[e0 + i];
+    lw[i] = in_w[e0 + i];
+  }
+  uint32_t rb = 0, re = 0;
+  double pr[K], xr[K];
+  bool dg = false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    pr[k] = 0.0;
+    xr[k] = 0.0;
+  }
+  if (r < N) {
+    rb = in_ptr[r];
+    re = in_ptr[r + 1];
+    dg = dangling[r] != 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      pr[k] = p[(uint64_t)r * K + k];
+      xr[k] = x0[(uint64_t)r * K + k];
+    }
+  }
+  if (threadIdx.x == 0) s_conv = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t all = K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u);
+  uint32_t frozen = 0, done = iters;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const bool odd = it & 1u;
+    const double* x_in = RING ? (it == 0 ? x0 : ring + (uint64_t)(it - 1u) * slot) : odd ? x1 : x0;
+    double* x_out = RING ? ring + (uint64_t)it * slot : odd ? x0 : x1;
+    const int rr = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
+    // the previous iteration's per-vector slots: dangling mass, and (tolerance
+    // mode) L1 change -> the vectors converged by then
+    const bool check = ntol > 0.0 && it > 0;
+    for (int k = wid; k < K; k += kNW) {
+      unsigned long long dv = __hip_atomic_load(&acc[rr * S + k * kAccSlots + lane],
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long ev = check ? __hip_atomic_load(&acc[(3 + rr) * S + k * kAccSlots + lane],
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0ull;
+      for (int off = 32; off > 0; off >>= 1) {
+        dv += __shfl_xor(dv, off);
+        ev += __shfl_xor(ev, off);
+      }
+      if (lane == 0) {
+        s_dsum[k] = (double)dv * (1.0 / kDScale);
+        if (check && (double)ev * (1.0 / kEScale) < ntol) atomicOr(&s_conv, 1u << k);
+      }
+    }
+    double sum[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sum[k] = 0.0;
+    if (r < N) {
+      for (uint32_t k0 = rb; k0 < re; k0 += kEdgeBatch) {
+        uint32_t c[kEdgeBatch];
+        float wv[kEdgeBatch];
+#pragma unroll
+        for (int j = 0; j < kEdgeBatch; ++j) {
+          const uint32_t e = k0 + j, li = e - e0;
+          const bool ok = e < re;
+          c[j] = !ok ? r : li < nc ? lcol[li] : in_col[e];
+          wv[j] = !ok ? 0.f : li < nc ? lw[li] : in_w[e];
+        }
+#pragma unroll
+        for (int j = 0; j < kEdgeBatch; ++j) {
+          if (k0 + j < re) {
+            const double* xs = x_in + (uint64_t)c[j] * K;
+            double xv[K];
+            if constexpr (RING) {
+#pragma unroll
+              for (int k = 0; k < K; k += 2) {
+                const double2 v2 = *reinterpret_cast<const double2*>(xs + k);
+                xv[k] = v2.x;
+                xv[k + 1] = v2.y;
+              }
+            } else {
+#pragma unroll
+              for (int k = 0; k < K; ++k)
+                xv[k] = __hip_atomic_load(&xs[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) sum[k] = ppr_edge(sum[k], xv[k], wv[j]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    frozen |= s_conv;
+    if (check && (frozen & all) == all) {
+      done = it;
+      break;
+    }
+    double dacc[K], eacc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      dacc[k] = 0.0;
+      eacc[k] = 0.0;
+      if (r < N) {
+        const double y = (frozen >> k) & 1u ? xr[k] : ppr_row(alpha, sum[k], s_dsum[k], pr[k]);
+        __hip_atomic_store(&x_out[(uint64_t)r * K + k], y, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        if (dg) dacc[k] = y;
+        eacc[k] = fabs(y - xr[k]);
+        xr[k] = y;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        dacc[k] += __shfl_xor(dacc[k], off);
+        eacc[k] += __shfl_xor(eacc[k], off);
+      }
+      if (lane == 0) {
+        red[(2 * k) * kNW + wid] = dacc[k];
+        red[(2 * k + 1) * kNW + wid] = eacc[k];
+      }
+    }
+    __syncthreads();
+    // block_sum's order: thread 0 of the per-launch kernel adds the 4 wave
+    // partials from 0.0 in wave order; here thread k does it for vector k
+    if (threadIdx.x < K) {
+      const int k = threadIdx.x;
+      double ds = 0.0, es = 0.0;
+      for (int q = 0; q < kNW; ++q) {
+        ds += red[(2 * k) * kNW + q];
+        es += red[(2 * k + 1) * kNW + q];
+      }
+      const int sl = k * kAccSlots + (blockIdx.x & (kAccSlots - 1));
+      atomicAdd(&acc[w * S + sl], __double2ull_rn(ds * kDScale));
+      atomicAdd(&acc[(3 + w) * S + sl], __double2ull_rn(es * kEScale));
+    }
+    if (blockIdx.x == 0)
+      for (int i = threadIdx.x; i < S; i += kPprThreads) {
+        __hip_atomic_store(&acc[z * S + i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&acc[(3 + z) * S + i], 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    if (threadIdx.x == 0) s_conv = 0u;  // (read by every thread before the barrier above)
+    if (!grid_barrier(bar, it, &s_flag, spin_limit)) {
+      done = it;
+      break;
+    }
+  }
+  if (r < N)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      __hip_atomic_store(&x0[(uint64_t)r * K + k], xr[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x == 0) bar[2] = done;
+}
+
 #ifndef ANOMOD_PPR_SUB
 #define ANOMOD_PPR_SUB 1
 #endif
@@ -572,6 +755,17 @@ PersistentFn persistent_fn(int sub, bool ring) {
                                                                : ppr_persistent_kernel<1, false>;
 }
 
+using BatchFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*, const uint8_t*,
+                        const double*, double, double*, double*, unsigned long long*, uint32_t,
+                        double, unsigned int*, uint32_t, double*, uint64_t);
+BatchFn batch_persistent_fn(uint32_t kb, bool ring) {
+  if (ring)
+    return kb == 2 ? ppr_batch_persistent_kernel<2, true> : kb == 4 ? ppr_batch_persistent_kernel<4, true>
+         : kb == 8 ? ppr_batch_persistent_kernel<8, true> : ppr_batch_persistent_kernel<16, true>;
+  return kb == 2 ? ppr_batch_persistent_kernel<2, false> : kb == 4 ? ppr_batch_persistent_kernel<4, false>
+       : kb == 8 ? ppr_batch_persistent_kernel<8, false> : ppr_batch_persistent_kernel<16, false>;
+}
+
 void free_graph(anomod_graph* g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
@@ -582,6 +776,19 @@ void free_graph(anomod_graph* g) {
   for (void* q : ps)
     if (q) (void)hipFree(q);
   delete g;
+}
+
+// The per-iteration vector ring of the persistent solves, grown to `bytes`
+// (false: no ring — the caller takes the two-buffer form).
+bool ensure_ring(anomod_ctx* ctx, anomod_graph* g, uint64_t bytes) {
+  (void)ctx;
+  if (g->ring_bytes >= bytes) return true;
+  if (g->ring) (void)hipFree(g->ring);
+  g->ring = nullptr;
+  g->ring_bytes = 0;
+  if (hipMalloc(&g->ring, bytes) == hipSuccess) g->ring_bytes = bytes;
+  (void)hipGetLastError();
+  return g->ring != nullptr;
 }
 
 // Launch iteration `it` (x[it&1] -> x[(it+1)&1]) over row blocks
@@ -876,25 +1083,20 @@ int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, dou
   const uint32_t pgrid = (g->grid + sub - 1) / sub;
   bool persistent = (int)pgrid <= g->coop_blocks && mode != 1;
   unsigned int* hb = reinterpret_cast<unsigned int*>(g->h_pin + N);  // pinned, past the vector
+  // a fresh vector slot per iteration for the persistent solve (grow-only;
+  // ANOMOD_PPR_RING=0, or more than kRingBytes of slots — e.g. a tolerance
+  // solve allowed 1000 iterations —: the two-buffer form, agent-scope gathers)
+  const uint64_t slot = (uint64_t)g->grid * kRowsPerBlock;
+  const char* ring_env = getenv("ANOMOD_PPR_RING");
+  bool ring = persistent && !(ring_env && ring_env[0] == '0') &&
+              (uint64_t)iters * slot * 8 <= kRingBytes;
+  if (ring) ring = ensure_ring(ctx, g, (uint64_t)iters * slot * 8);
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
   g->last_path = 0;
   bool fell_back = false;
   if (persistent) {
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
     double x0v = 1.0 / N;
-    // a fresh vector slot per iteration (grow-only; ANOMOD_PPR_RING=0 or more
-    // than kRingBytes of slots: the two-buffer form with agent-scope gathers)
-    const uint64_t slot = (uint64_t)g->grid * kRowsPerBlock;
-    const char* ring_env = getenv("ANOMOD_PPR_RING");
-    bool ring = !(ring_env && ring_env[0] == '0') && (uint64_t)iters * slot * 8 <= kRingBytes;
-    if (ring && g->ring_slots < iters) {
-      if (g->ring) ANOMOD_HIP(ctx, hipFree(g->ring));
-      g->ring = nullptr;
-      g->ring_slots = 0;
-      if (hipMalloc(&g->ring, (uint64_t)iters * slot * 8) == hipSuccess) g->ring_slots = iters;
-      else ring = false;
-      (void)hipGetLastError();
-    }
     hipLaunchKernelGGL(persistent_fn(sub, ring), dim3(pgrid), dim3(kPprThreads * sub), 0,
                        ctx->stream, g->N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->p, alpha,
                        x0v, g->x[0], g->x[1], g->acc, iters, ntol, g->bar, spin,
@@ -1049,7 +1251,76 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   };
   uint32_t done = 0, frozen = 0;
   const uint32_t all = kb >= 32 ? 0xFFFFFFFFu : ((1u << kb) - 1u);
+  // One persistent launch for the whole batch when its workgroups are all
+  // resident (ANOMOD_PPR_MODE=1: the per-launch loop below); a barrier
+  // timeout reruns the batch per launch from x0.
+  const char* mode_env = getenv("ANOMOD_PPR_MODE");
+  const int mode = mode_env ? atoi(mode_env) : 0;
+  const char* spin_env = getenv("ANOMOD_PPR_SPIN");
+  const long spin_v = spin_env && *spin_env ? atol(spin_env) : -1;
+  const uint32_t spin = spin_v >= 0 && spin_v < (long)kSpinLimit ? (uint32_t)spin_v : kSpinLimit;
+  const uint64_t slot = (uint64_t)g->grid * kRowsPerBlock * kb;  // doubles per ring slot
+  const char* ring_env = getenv("ANOMOD_PPR_RING");
+  bool ring = !(ring_env && ring_env[0] == '0') && (uint64_t)iters * slot * 8 <= kRingBytes;
+  const BatchFn bfn = batch_persistent_fn(kb, ring);
+  if (g->bcoop_kb != kb || g->bcoop_ring != ring) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfn, kPprThreads, 0) != hipSuccess)
+      per_cu = 0;
+    (void)hipGetLastError();
+    g->bcoop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
+    g->bcoop_kb = kb;
+    g->bcoop_ring = ring;
+  }
+  bool persistent = mode != 1 && (int)g->grid <= g->bcoop_blocks;
+  if (persistent && ring) {
+    ring = ensure_ring(ctx, g, (uint64_t)iters * slot * 8);
+    if (!ring) {  // no ring: the two-buffer instantiation (its own residency)
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, batch_persistent_fn(kb, false),
+                                                       kPprThreads, 0) != hipSuccess)
+        per_cu = 0;
+      (void)hipGetLastError();
+      persistent = (int)g->grid <= (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
+    }
+  }
+  if (persistent) ANOMOD_HIP(ctx, hipMemsetAsync(g->bar, 0, kBarWords * sizeof(unsigned int),
+                                                 ctx->stream));
   if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  g->last_path = 0;
+  bool fell_back = false;
+  if (persistent) {
+    const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
+    hipLaunchKernelGGL(batch_persistent_fn(kb, ring), dim3(g->grid), dim3(kPprThreads), 0,
+                       ctx->stream, N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->bp, alpha,
+                       g->bx[0], g->bx[1], g->bacc, iters, ntol, g->bar, spin,
+                       ring ? g->ring : nullptr, slot);
+    ANOMOD_HIP(ctx, hipGetLastError());
+    if (int rc = stage_end(ctx, kStagePagerank)) return rc;
+    unsigned int hb[4];
+    ANOMOD_HIP(ctx, hipMemcpyAsync(hb, g->bar, sizeof(hb), hipMemcpyDeviceToHost, ctx->stream));
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (hb[1] == 0u) {
+      done = hb[2];
+      g->last_path = ANOMOD_PPR_PATH_PERSISTENT;
+      std::vector<double> xs((size_t)N * kb);
+      ANOMOD_HIP(ctx, hipMemcpyAsync(xs.data(), g->bx[0], xs.size() * 8, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      for (uint32_t k = 0; k < K; ++k)
+        for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];
+      if (iters_done) *iters_done = done;
+      return ANOMOD_OK;
+    }
+    // a workgroup never became resident: start over per launch from x0
+    ++g->fallbacks;
+    fell_back = true;
+    ANOMOD_HIP(ctx, hipMemcpyAsync(g->bx[0], x0.data(), x0.size() * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+    ANOMOD_HIP(ctx, hipMemcpyAsync(g->bacc, g->host_bacc.data(), g->host_bacc.size() * 8,
+                                   hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
+  }
   for (uint32_t it = 0; it < iters; ++it) {
     launch(it, frozen);
     ANOMOD_HIP(ctx, hipGetLastError());
@@ -1069,6 +1340,8 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
       if ((frozen & all) == all) break;
     }
   }
+  g->last_path = tol > 0.0 ? ANOMOD_PPR_PATH_READBACK : ANOMOD_PPR_PATH_GRAPH;
+  if (fell_back) g->last_path |= ANOMOD_PPR_PATH_FALLBACK;
   if (int rc = stage_end(ctx, kStagePagerank)) return rc;
   std::vector<double> xs((size_t)N * kb);
   ANOMOD_HIP(ctx, hipMemcpyAsync(xs.data(), g->bx[done & 1], xs.size() * 8, hipMemcpyDeviceToHost,

@@ -471,8 +471,9 @@ int anomod_graph_synthetic_csr(uint32_t N, uint32_t mean_degree, uint64_t seed,
 int anomod_graph_info(const anomod_graph* g, uint32_t* N, uint64_t* nnz);
 int anomod_graph_pagerank(anomod_ctx* ctx, anomod_graph* g, const double* p, double alpha,
                           uint32_t iters, double tol, double* x_out, uint32_t* iters_done);
-/* Which path the last anomod_graph_pagerank solve of g took: 1 = replayed
- * hipGraph of per-iteration launches (fixed iterations), 2 = per-iteration
+/* Which path the last anomod_graph_pagerank / _batch solve of g took: 1 =
+ * replayed hipGraph of per-iteration launches (fixed iterations; a batch:
+ * per-iteration launches), 2 = per-iteration
  * launches with a host read-back of the L1 change (tolerance), 3 = one
  * persistent launch (grid barrier); | 4 = the persistent launch timed out at
  * its grid barrier (a workgroup never became resident, e.g. another process
@@ -488,7 +489,9 @@ int anomod_graph_last_solve(const anomod_graph* g, uint32_t* path, uint32_t* fal
  * iteration for all K.  P and X are [K][N]; every column equals its
  * anomod_graph_pagerank solve bit for bit (same arithmetic and reduction
  * order).  tol > 0: each vector stops at its own convergence iteration
- * (later iterations carry it unchanged); iters_done = iterations launched. */
+ * (later iterations carry it unchanged); iters_done = iterations run.  One
+ * persistent launch (grid barrier) when the batch's workgroups are all
+ * resident (N = 10^5: K <= 8), else one launch per iteration.             */
 int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* P, uint32_t K,
                                 double alpha, uint32_t iters, double tol, double* X,
                                 uint32_t* iters_done);

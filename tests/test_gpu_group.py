@@ -190,16 +190,20 @@ def env_knob(monkeypatch):
     return monkeypatch.setenv
 
 
-@pytest.mark.parametrize("path,avg", [("lsd", None), ("bucket", "64"), ("bucket", "1024")])
+@pytest.mark.parametrize("path,avg", [("lsd", None), ("bucket", "64"), ("bucket", "1024"),
+                                      ("pipe", "1024"), ("pipe", "64")])
 def test_group_paths_agree(ctx, env_knob, path, avg):
     """The LSD path (ANOMOD_GROUP_PATH=lsd) and the bucket path at the
     smallest / largest mean bucket size (ANOMOD_BUCKET_AVG: one or two
     scatter levels, most buckets in the small or the large per-bucket
-    kernel) give the oracle's grouping."""
+    kernel), also with the persistent pipelined bucket kernel
+    (ANOMOD_BK_PIPE=1), give the oracle's grouping."""
     if path == "lsd":
         env_knob("ANOMOD_GROUP_PATH", "lsd")
     else:
         env_knob("ANOMOD_BUCKET_AVG", avg)
+    if path == "pipe":
+        env_knob("ANOMOD_BK_PIPE", "1")
     rng = np.random.default_rng(77)
     sp = _with_trace_hashes(_random_spanset(rng, 12, 60000, 40, dup=0.02), rng)
     big = _with_trace_hashes(_random_spanset(rng, 12, 4, 1500, dup=0.02), rng)
@@ -273,12 +277,12 @@ def test_group_pair_key_collisions(ctx, env_knob, avg):
 @pytest.mark.parametrize("S,max_len,form", [(12, 24, None), (46, 60, None), (20, 40, None),
                                             (12, 24, "pair"), (100, 30, None)])
 def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, form):
-    """anomod_edge_aggregate_ungrouped's fused path (the buckets write one
-    edge record per span, the table is taken from those records) against the
-    unfused one (ANOMOD_UNGROUPED_FUSED=0: grouped columns, then the chunk
-    walk) and the oracle: SN / TrainTicket widths (direct, wide, slot stats),
-    wide latencies (a compact-form run that learns the set's form), duplicate
-    ids, orphans, interleaved arrival."""
+    """anomod_edge_aggregate_ungrouped's fused path (opt-in,
+    ANOMOD_UNGROUPED_FUSED=1: the buckets write one edge record per span, the
+    table is taken from those records) against the default unfused one
+    (grouped columns, then the chunk walk) and the oracle: SN / TrainTicket
+    widths (direct, wide, slot stats), wide latencies (a compact-form run that
+    learns the set's form), duplicate ids, orphans, interleaved arrival."""
     if form:
         env_knob("ANOMOD_HIST_FORM", form)
     rng = np.random.default_rng(S * 3 + max_len)
@@ -287,19 +291,19 @@ def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, 
     flat = _interleave(sp, rng, "time")
     ref = native.edge_aggregate(_oracle_grouped(flat))
     dev = ctx.upload_ungrouped(flat)
+    monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "1")
     fused = ctx.edge_aggregate(dev)
     assert ctx.group_info()["path"] == "bucket"
     assert_table_equal(fused, ref)
-    monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "0")
-    assert_table_equal(ctx.edge_aggregate(dev), ref)
     monkeypatch.delenv("ANOMOD_UNGROUPED_FUSED")
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
     if form is None:  # learned from the compact run (wide latencies: far too many keys)
         assert dev.hints[1] in ((1,) if S == 20 else (0, 1))
     assert_table_equal(ctx.edge_aggregate(dev), ref)  # again, with the learned form
     dev.free()
 
 
-def test_ungrouped_fused_long_traces_fall_back(ctx):
+def test_ungrouped_fused_long_traces_fall_back(ctx, monkeypatch):
     """Buckets of several traces of thousands of spans (beyond the large
     bucket kernel) leave the fused path for the unfused one; the table is
     the oracle's either way."""
@@ -311,4 +315,5 @@ def test_ungrouped_fused_long_traces_fall_back(ctx):
                              rng, _unmix64((base | low).astype(np.uint64)))
     flat = _interleave(anomod.SpanSet.concat([sp, big]), rng, "random")
     dev = ctx.upload_ungrouped(flat)
+    monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "1")
     assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(_oracle_grouped(flat)))

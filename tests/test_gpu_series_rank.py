@@ -289,6 +289,36 @@ def test_pagerank_batch_equals_single_solves(ctx, K):
     g.free()
 
 
+@pytest.mark.parametrize("K", [2, 5, 8])
+def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K):
+    """The persistent batch (one launch, grid barrier, vector ring or the
+    two-buffer form) == the per-launch batch loop (ANOMOD_PPR_MODE=1), bit
+    for bit, in fixed-iteration and tolerance mode (per-vector freezing);
+    a barrier timeout (ANOMOD_PPR_SPIN=0) reruns per launch, same bits."""
+    g = anomod.DeviceGraph(ctx, synthetic=(40000, 9, 12))
+    rng = np.random.default_rng(K + 40)
+    P = rng.random((K, g.N))
+    P[1, rng.random(g.N) < 0.9] = 0.0  # a sparser vector converges at another iteration
+    cases = ((1, 0.0), (23, 0.0), (400, 1e-11))
+    monkeypatch.setenv("ANOMOD_PPR_MODE", "1")
+    ref = [g.pagerank_batch(P, iters=it, tol=tol) for it, tol in cases]
+    assert g.last_solve()[0] == "readback"
+    monkeypatch.delenv("ANOMOD_PPR_MODE")
+    for ring in ("1", "0"):
+        monkeypatch.setenv("ANOMOD_PPR_RING", ring)
+        for (it, tol), (Xr, dr) in zip(cases, ref):
+            X, d = g.pagerank_batch(P, iters=it, tol=tol)
+            assert g.last_solve()[0] == "persistent"
+            assert d == dr
+            np.testing.assert_array_equal(X, Xr)
+    monkeypatch.setenv("ANOMOD_PPR_SPIN", "0")
+    fb0 = g.last_solve()[1]
+    X, d = g.pagerank_batch(P, iters=23)
+    assert g.last_solve() == ("fallback:graph", fb0 + 1)
+    np.testing.assert_array_equal(X, ref[1][0])
+    g.free()
+
+
 @pytest.mark.parametrize("G", [1, 2, 3, 8, 500])
 def test_pagerank_row_sharded_equals_unsharded(ctx, monkeypatch, G):
     """Row-sharded solve rehearsed on one device (G row shards of whole 256-row
