@@ -55,11 +55,15 @@ using chunk::wave_sync;
 constexpr int kWv = 64;
 constexpr int kBThreads = 1024;                // scatter workgroup
 constexpr int kBWaves = kBThreads / kWv;       // 16
+// Level-A records per thread: 2 -> 2048-record tiles, 76 KiB of LDS, two
+// workgroups per CU (one tile's loads and ranking overlap the other's
+// scattered stores): grouping 62.7 -> 58.7 ms at 2^27 SN traces against
+// 4096-record tiles at one workgroup per CU (gpurun_out/r4d_aper2.log).
 #ifndef ANOMOD_BK_APER
-#define ANOMOD_BK_APER 4
+#define ANOMOD_BK_APER 2
 #endif
 constexpr int kBPer = ANOMOD_BK_APER;          // records per thread
-constexpr int kBTile = kBThreads * kBPer;      // 4096 records per level-A tile
+constexpr int kBTile = kBThreads * kBPer;      // 2048 records per level-A tile
 constexpr int kPPer = 16;                      // pairs per thread (level B)
 constexpr int kPTile = kBThreads * kPPer;      // 16384 pairs per level-B tile (128 KiB)
 constexpr int kDMax = 11;                      // digit bits per scatter level
@@ -297,13 +301,14 @@ __global__ __launch_bounds__(1024) void bk_scan_seg_kernel(uint32_t* __restrict_
 }
 
 // ---- level A: one stable scatter of the records ------------------------------
-// Tile = 4096 records (1024 threads x 4; wave w owns positions [256w, 256w +
-// 256)), ranked with wave ballots (da ballots give each lane its same-digit
-// peers; a per-wave LDS counter per digit carries the count down the wave's
-// rows), staged whole in LDS in digit order — over the per-wave counters,
-// which are dead by then — and written as 16-B chunks, a wave instruction
-// covering 32 consecutive staged records (1 KiB, runs of ~8 records to one
-// place each at 9 digit bits).  Beside every record goes its pair for level B
+// Tile = kBTile records (1024 threads x kBPer; wave w owns positions
+// [64 kBPer w, 64 kBPer (w + 1))), ranked with wave ballots (da ballots give
+// each lane its same-digit peers; a per-wave LDS counter per digit carries the
+// count down the wave's rows), staged whole in LDS in digit order — over the
+// per-wave counters, which are dead by then — and written as 16-B chunks, a
+// wave instruction covering 32 consecutive staged records (1 KiB, runs of ~4
+// records to one place each at 9 digit bits and 2048-record tiles; the XCD
+// tile order below lets neighbouring tiles' runs meet in L2).  Beside every record goes its pair for level B
 // and the buckets: the next 32 key bits << 32 | the record's position.
 // (Measured at 2^25 SN traces, 9-bit levels: half-record staging with one
 // 16-B store per lane and record half 9.2 ms; whole records 6.0; no stores at
@@ -693,7 +698,7 @@ __device__ void bucket_huge(unsigned char* lds, uint32_t c, uint32_t a0, uint32_
       if (v && (peers >> lane) == 1ull) hcnt[su] += (uint32_t)__popcll(peers);
       wave_sync();
       if (v) {
-        out.h[a0 + row] = ((uint64_t)r0.y << 32) | r0.x;
+        if (out.h) out.h[a0 + row] = ((uint64_t)r0.y << 32) | r0.x;
         out.sid[a0 + row] = ((uint64_t)r0.w << 32) | r0.z;
         out.pid[a0 + row] = ((uint64_t)r1.y << 32) | r1.x;
         out.sf[a0 + row] = r1.z;
@@ -994,7 +999,7 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
         x1 = q[1];
       }
       const uint32_t i = L.sfinal[p];
-      out.h[a0 + i] = ((uint64_t)x0.y << 32) | x0.x;
+      if (out.h) out.h[a0 + i] = ((uint64_t)x0.y << 32) | x0.x;  // (aggregate-only calls: none)
       out.sid[a0 + i] = ((uint64_t)x0.w << 32) | x0.z;
       out.pid[a0 + i] = ((uint64_t)x1.y << 32) | x1.x;
       out.sf[a0 + i] = x1.z;
@@ -1066,7 +1071,10 @@ __device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t
   bucket_body<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, eo, kshift, dcnt, k, v, ra, rb);
 }
 
-__global__ __launch_bounds__(kSmallW) void bk_bucket_kernel(
+#ifndef ANOMOD_BK_MINW
+#define ANOMOD_BK_MINW 1  // waves per SIMD the small bucket kernel's registers must allow
+#endif
+__global__ __launch_bounds__(kSmallW, ANOMOD_BK_MINW) void bk_bucket_kernel(
     uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
     const uint32_t* __restrict__ bstart, int kshift, uint32_t* __restrict__ dcnt,
     uint32_t* __restrict__ over, unsigned long long* __restrict__ over_n, uint32_t over_cap,
@@ -1334,7 +1342,7 @@ int max_bucket(anomod_ctx* ctx, const uint32_t* bstart, uint64_t nbk, uint64_t* 
 }
 
 int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, GroupResult* res,
-                    bool* fallback, bool* escalate, const EdgeOut* eo) {
+                    bool* fallback, bool* escalate, const EdgeOut* eo, bool want_h) {
   *fallback = false;
   *escalate = false;
   GroupWs* ws = ctx->group_ws;
@@ -1356,7 +1364,8 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   };
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
   GRec* recs = ws->aos[0];                    // level-A records (gathered by the buckets)
-  const SoaOut cols = soa_of(ws->aos[1]);     // the grouped columns
+  SoaOut cols = soa_of(ws->aos[1]);           // the grouped columns
+  if (!want_h) cols.h = nullptr;              // an aggregation reads no trace_hash column
   uint64_t* pa = ws->pairs[0];                // level-A pairs
   uint64_t* pb = ws->pairs[1];                // level-B pairs
   hipStream_t st = ctx->stream;
@@ -1516,19 +1525,19 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
 }  // namespace
 
 int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback,
-                     uint64_t* erec, uint32_t S) {
+                     uint64_t* erec, uint32_t S, bool want_h) {
   BucketGeom g = bucket_geom(in->n_spans);
   bool escalate = false;
   const EdgeOut eo{erec, S};
   const EdgeOut* pe = erec ? &eo : nullptr;
-  if (int rc = bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe)) return rc;
+  if (int rc = bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe, want_h)) return rc;
   if (!escalate) return ANOMOD_OK;
   // one level was not enough for the set's longest traces: two, the second
   // with kDMax bits
   g.DB = kDMax;
   g.T = g.DA + g.DB;
   g.tilesB = (in->n_spans + kPTile - 1) / kPTile + (1ull << g.DA);
-  return bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe);
+  return bucket_run_geom(ctx, in, g, res, fallback, &escalate, pe, want_h);
 }
 
 }  // namespace anomod

@@ -104,8 +104,10 @@ BucketGeom bucket_geom(uint64_t n);
 // With erec (the fused ungrouped aggregation): no grouped columns; every
 // span's edge record (parent service row * S + service) << 33 | error << 32 |
 // duration goes to erec[grouped position] instead (*fallback also when a
-// bucket of long traces needs the unfused path).
+// bucket of long traces needs the unfused path).  want_h = false: the
+// grouped trace_hash column is not written (res->cols.h = NULL; an edge
+// aggregation of the grouped view reads no trace_hash).
 int bucket_group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool* fallback,
-                     uint64_t* erec = nullptr, uint32_t S = 0);
+                     uint64_t* erec = nullptr, uint32_t S = 0, bool want_h = true);
 
 }  // namespace anomod

@@ -687,7 +687,7 @@ bool force_lsd() {
   return e && e[0] == 'l';
 }
 
-int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
+int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool want_h = true) {
   const uint64_t n = in->n_spans;
   if (n > 0xFFFFFFFFull - kSTile) {  // u32 run starts (the workspace alone would be > 300 GB)
     set_error(ctx, "trace grouping of %llu spans: at most 2^32 - %d per call",
@@ -698,7 +698,7 @@ int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res) {
   GroupWs* ws = ctx->group_ws;
   if (n > 0 && !force_lsd()) {
     bool fallback = false;
-    if (int rc = bucket_group_run(ctx, in, res, &fallback)) return rc;
+    if (int rc = bucket_group_run(ctx, in, res, &fallback, nullptr, 0, want_h)) return rc;
     if (!fallback) {
       ctx->group_path = 1;
       ctx->group_levels = res->passes;
@@ -937,7 +937,7 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
     if (rc != ANOMOD_OK) return comm_agree(ctx, rc);
   }
   if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
-  if (rc == ANOMOD_OK) rc = group_run(ctx, spans, &g);
+  if (rc == ANOMOD_OK) rc = group_run(ctx, spans, &g, /*want_h=*/false);
   if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
   if (rc != ANOMOD_OK) return comm_agree(ctx, rc);  // peers learn of it before their reduce
   anomod_spans view = view_of(spans, g);

@@ -17,3 +17,7 @@ for v in ship sper3 aper2 both; do
   ANOMOD_LIB=$LIB AB_VAR=ANOMOD_BUCKET_DEBUG AB_VALS=0,1 timeout -k 10 240 python3 scripts/time_env_ab.py 27 2 \
     > gpurun_out/r4d_$v.log 2>&1 || exit 2
 done
+for v in ship bm128 bm64; do
+  if [ $v = ship ]; then LIB=$PWD/anomod-a-dataset-for-anomaly-detection-and-root-cause-analysis-in-microservice-systems_amd/anomod/libanomod.so; else LIB=$PWD/$V/libanomod_$v.so; fi
+  ANOMOD_LIB=$LIB TG_TOPO=LONG timeout -k 10 120 python3 scripts/time_edge_leg.py 23 5 >> gpurun_out/r4d_long.log 2>&1 || exit 5
+done

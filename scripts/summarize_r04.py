@@ -18,6 +18,7 @@ from __future__ import annotations
 import csv
 import json
 import math
+import re
 import shutil
 import sys
 from pathlib import Path
@@ -49,9 +50,12 @@ def pmc(paths: list[Path]) -> dict:
 
 
 def select(data: dict, match: str, counter: str, sl: slice) -> list[float]:
+    """Values of `counter` for kernels whose name contains `match` (or, with a
+    "re:" prefix, matches that regular expression), in dispatch order."""
     vals = []
     for (k, c), v in data.items():
-        if c == counter and match in k:
+        hit = re.search(match[3:], k) if match.startswith("re:") else match in k
+        if c == counter and hit:
             vals.extend(v)
     return vals[sl]
 
@@ -82,8 +86,8 @@ def main() -> int:
             targets.append(("trace structure", "trace_struct_kernel<true>",
                             ref["trace_structure"]["bytes_per_launch"], slice(None)))
         if "tt_width" in ref:
-            targets.append(("TrainTicket width edge_agg <pair, wide stats>",
-                            "edge_agg_kernel<1, 3, true, 0>", ref["tt_width"]["bytes_per_launch"],
+            targets.append(("TrainTicket width edge_agg <either histogram form, wide stats>",
+                            r"re:edge_agg_kernel<[12], 3, true, 0>", ref["tt_width"]["bytes_per_launch"],
                             slice(0, 3)))
         if "long_traces" in ref:
             lt = ref["long_traces"]
@@ -96,6 +100,12 @@ def main() -> int:
             p = ref["pagerank"]
             targets.append(("PageRank persistent solve (100 iterations)", "ppr_persistent_kernel",
                             p["bytes_per_iter"] * p["iters_per_solve"], slice(1, None)))
+            if "batched" in p:
+                nn, ne, kb = p["nodes"], p["edges"], p["batched"]["vectors"]
+                targets.append((f"PageRank persistent batch ({kb} vectors, 100 iterations)",
+                                "ppr_batch_persistent_kernel",
+                                (4 * (nn + 1) + 8 * ne + 16 * nn * kb) * p["iters_per_solve"],
+                                slice(1, None)))
         if "ewma" in ref:
             e = ref["ewma"]
             samples = e["steps_per_chunk"] * e["S"]
