@@ -807,6 +807,7 @@ anomod_spans view_of(const anomod_spans* in, const GroupResult& g) {
   v.max_svc = in->max_svc;
   v.grouped = true;
   v.unique_ids = in->unique_ids;  // grouping permutes spans, ids stay per trace
+  v.max_trace_len = in->max_trace_len;  // and traces keep their spans (long-trace pass sizing)
   v.trace_hash = g.cols.h;
   v.span_id = g.cols.sid;
   v.parent_span_id = g.cols.pid;

@@ -251,6 +251,9 @@ __global__ __launch_bounds__(kPprThreads) void ppr_iter_kernel(
 // that forces the timeout) raises the flag and every block leaves; the host
 // then reruns the solve through the per-launch path.
 constexpr uint32_t kSpinLimit = 1u << 22;
+#ifndef ANOMOD_PPR_FLATPOLL
+#define ANOMOD_PPR_FLATPOLL 0
+#endif
 constexpr int kBarGroups = 8;  // 16 / 32 groups measured slower
 constexpr int kBarStride = 32;  // u32 words between counters (128 B)
 // bar[0] top counter, bar[1] timeout flag, bar[2] iterations done,
@@ -266,6 +269,44 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+#if ANOMOD_PPR_FLATPOLL
+  // Flat poll: each block adds to its group counter (no return awaited) and
+  // lanes 0..ng-1 of wave 0 poll the ng group counters together — no
+  // second (top-counter) atomic round trip on the critical path.
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nb = gridDim.x;
+    const uint32_t ng = nb < (uint32_t)kBarGroups ? nb : (uint32_t)kBarGroups;
+    if (lane == 0)
+      __hip_atomic_fetch_add(&bar[kBarStride * (1 + blockIdx.x % ng)], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t gl = lane < ng ? lane : 0u;
+    const uint32_t target = ((nb - gl + ng - 1) / ng) * (k + 1u);  // group gl's arrivals
+    uint32_t spins = 0;
+    int fail = 0;
+    while (true) {
+      const uint32_t v = lane < ng ? __hip_atomic_load(&bar[kBarStride * (1 + gl)], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0xFFFFFFFFu;
+      if (__ballot(v < target) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > spin_limit) {
+        if (lane == 0) atomicOr(&bar[1], 1u);
+        fail = 1;
+        break;
+      }
+      if ((spins & 1023u) == 0u &&
+          __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        fail = 1;
+        break;
+      }
+    }
+    if (lane == 0) *s_flag = fail;
+  }
+  __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  return *s_flag == 0;
+#endif
   if (threadIdx.x == 0) {
     const uint32_t nb = gridDim.x;
     const uint32_t ng = nb < (uint32_t)kBarGroups ? nb : (uint32_t)kBarGroups;

@@ -12,3 +12,7 @@ for v in ship m8 s3m8 a4; do
   ANOMOD_LIB=$LIB AB_VAR=ANOMOD_BUCKET_DEBUG AB_VALS=0 timeout -k 10 240 python3 scripts/time_env_ab.py 27 3 \
     > gpurun_out/r4e_$v.log 2>&1 || exit 2
 done
+for v in ship flat; do
+  if [ $v = ship ]; then LIB=$PWD/anomod-a-dataset-for-anomaly-detection-and-root-cause-analysis-in-microservice-systems_amd/anomod/libanomod.so; else LIB=$PWD/$V/libanomod_$v.so; fi
+  ANOMOD_LIB=$LIB timeout -k 10 200 python3 scripts/time_ppr_ring.py 4 > gpurun_out/r4e_ppr_$v.log 2>&1 || exit 3
+done
