@@ -683,7 +683,8 @@ int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_
   anomod_spans* s = nullptr;
   if (int rc = alloc_spans(ctx, n_spans, n_traces, soa->trace_hash != nullptr, &s)) return rc;
   s->max_svc = max_svc;
-  s->max_trace_len = max_len;
+  // (no trace_ptr: an ungrouped set, its trace lengths unknown until grouped)
+  s->max_trace_len = n_traces || !n_spans ? max_len : ~0ull;
   hipError_t e = hipSuccess;
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (e == hipSuccess && bytes)
