@@ -167,7 +167,13 @@ __device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], i
 // a callee's spans after the calling span) or near the trace start (the
 // caller's entry span); simulated row-steps per 256-span chunk: TrainTicket
 // 18.8 -> 9.2, SocialNetwork 6.5 -> 4.0.
-constexpr uint32_t kFwd = 6, kBwd = 4;
+#ifndef ANOMOD_FWD
+#define ANOMOD_FWD 6
+#endif
+#ifndef ANOMOD_BWD
+#define ANOMOD_BWD 4
+#endif
+constexpr uint32_t kFwd = ANOMOD_FWD, kBwd = ANOMOD_BWD;
 static_assert(kFwd % 2 == 0 && kBwd % 2 == 0 && kFwd + kBwd <= 16, "bidirectional step");
 
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,

@@ -58,6 +58,8 @@ struct anomod_graph {
   uint32_t last_path = 0;   // ANOMOD_PPR_PATH_* of the last single-vector solve
   uint32_t fallbacks = 0;   // persistent solves rerun per launch (barrier timed out)
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
+  double* h_bpin = nullptr;  // pinned [N][kb] staging of a batch's P in / X out
+  uint64_t h_bpin_n = 0;
   // persistent solve: one fresh vector per iteration (see ppr_persistent_kernel)
   double* ring = nullptr;
   uint64_t ring_bytes = 0;  // bytes the ring holds (single solves and batches share it)
@@ -609,6 +611,14 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_iter_kernel(
 // iteration it, freezes the converged vectors (carried unchanged, as the
 // host loop of the per-launch batch does) and stops once all are frozen.
 // The final vectors land in x0 ([N][K], node-major); bar[2] = iterations.
+// One 16-B store written through to the coherent level (`sc1`, what an
+// agent-scope relaxed store compiles to, at 16 B: HIP has no 16-B atomic
+// store).  Drained by grid_barrier's wait before the arrival.
+using v4u32 = uint32_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_wt(void* p, v4u32 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+}
+
 template <int K, bool RING>
 __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
@@ -623,6 +633,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
   __shared__ float lw[kLdsE];
   __shared__ double red[2 * K * kNW];
   __shared__ double s_dsum[K];
+  __shared__ v4u32 stg[kNW * 64 * (K / 2 + 1)];  // per wave: 64 rows of K doubles (+ a pad piece)
   __shared__ uint32_t s_conv;
   __shared__ int s_flag;
   const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
@@ -731,12 +742,35 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
       eacc[k] = 0.0;
       if (r < N) {
         const double y = (frozen >> k) & 1u ? xr[k] : ppr_row(alpha, sum[k], s_dsum[k], pr[k]);
-        __hip_atomic_store(&x_out[(uint64_t)r * K + k], y, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
         if (dg) dacc[k] = y;
         eacc[k] = fabs(y - xr[k]);
         xr[k] = y;
       }
+    }
+    // The wave's 64 rows x K doubles, written through (16-B sc1 stores): lane
+    // l stages its row in LDS, then every store instruction covers 1 KiB of
+    // consecutive rows — 8-B stores per lane and value wrote each line in
+    // eight partial pieces (4x the bytes at the fabric, PMC r04).
+    {
+      constexpr int Q = K / 2;  // 16-B pieces per row
+      v4u32* st = stg + wid * (64 * (Q + 1));
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint64_t a0 = __double_as_longlong(xr[2 * q]), a1 = __double_as_longlong(xr[2 * q + 1]);
+        st[lane * (Q + 1) + q] = v4u32{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1,
+                                      (uint32_t)(a1 >> 32)};
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t row0 = r - (uint32_t)lane;  // the wave's first row
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {
+        const uint32_t i = (uint32_t)(j * 64 + lane), row = i / Q, q = i % Q;
+        if (row0 + row < N)
+          store16_wt(x_out + (uint64_t)(row0 + row) * K + 2 * q, st[row * (Q + 1) + q]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
       for (int off = 32; off > 0; off >>= 1) {
         dacc[k] += __shfl_xor(dacc[k], off);
         eacc[k] += __shfl_xor(eacc[k], off);
@@ -812,6 +846,7 @@ void free_graph(anomod_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
   if (g->h_pin) (void)hipHostFree(g->h_pin);
+  if (g->h_bpin) (void)hipHostFree(g->h_bpin);
   void* ps[] = {g->in_ptr, g->in_col, g->in_w, g->dangling, g->p,    g->x[0], g->x[1],
                 g->acc,    g->bp,     g->bx[0], g->bx[1],    g->bacc, g->bar, g->ring};
   for (void* q : ps)
@@ -1235,16 +1270,30 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   const uint32_t N = g->N;
   const uint32_t kb = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;  // padded with vector 0
   // node-major, normalised personalizations
-  std::vector<double> pn((size_t)N * kb);
+  std::vector<double> psums(kb);
   for (uint32_t k = 0; k < kb; ++k) {
     const double* pk = P + (size_t)(k < K ? k : 0) * N;
     double s = 0.0;
     const uint32_t bad = personalization_sum<false>(pk, N, nullptr, s);
     ANOMOD_REQUIRE(ctx, bad == N, "personalization[%u][%u] invalid", k, bad);
     ANOMOD_REQUIRE(ctx, s > 0.0, "personalization %u sums to zero", k);
-    for (uint32_t i = 0; i < N; ++i) pn[(size_t)i * kb + k] = pk[i] / s;
+    psums[k] = s;
   }
   if (int rc = bind(ctx)) return rc;
+  // pinned node-major staging of P in and X out (grow-only)
+  if (g->h_bpin_n < (uint64_t)N * kb) {
+    if (g->h_bpin) ANOMOD_HIP(ctx, hipHostFree(g->h_bpin));
+    g->h_bpin = nullptr;
+    g->h_bpin_n = 0;
+    ANOMOD_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&g->h_bpin), (uint64_t)N * kb * 8,
+                                  hipHostMallocDefault));
+    g->h_bpin_n = (uint64_t)N * kb;
+  }
+  double* pn = g->h_bpin;
+  for (uint32_t k = 0; k < kb; ++k) {
+    const double* pk = P + (size_t)(k < K ? k : 0) * N;
+    for (uint32_t i = 0; i < N; ++i) pn[(size_t)i * kb + k] = pk[i] / psums[k];
+  }
   if (g->kb < kb) {
     for (void* q : {(void*)g->bp, (void*)g->bx[0], (void*)g->bx[1], (void*)g->bacc})
       if (q) (void)hipFree(q);
@@ -1262,11 +1311,16 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
     g->host_bacc.assign(6ull * kb * kAccSlots, 0ull);
   }
   const int S = kAccSlots * (int)kb;  // one accumulator block = kb x kAccSlots
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bp, pn.data(), pn.size() * 8, hipMemcpyHostToDevice,
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bp, pn, (size_t)N * kb * 8, hipMemcpyHostToDevice,
                                  ctx->stream));
-  std::vector<double> x0((size_t)N * kb, 1.0 / N);
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bx[0], x0.data(), x0.size() * 8, hipMemcpyHostToDevice,
-                                 ctx->stream));
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the staging is reused for X
+  const uint32_t nx = N * kb;  // x0 = 1/N everywhere, on the device
+  auto init_x0 = [&]() {
+    hipLaunchKernelGGL(ppr_init_kernel, dim3(std::min<uint32_t>((nx + kPprThreads - 1) / kPprThreads, 2048)),
+                       dim3(kPprThreads), 0, ctx->stream, nx, 1.0 / N, g->bx[0]);
+    return hipGetLastError();
+  };
+  ANOMOD_HIP(ctx, init_x0());
   std::fill(g->host_bacc.begin(), g->host_bacc.end(), 0ull);
   for (uint32_t k = 0; k < kb; ++k)
     g->host_bacc[k * kAccSlots] =
@@ -1344,8 +1398,8 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
     if (hb[1] == 0u) {
       done = hb[2];
       g->last_path = ANOMOD_PPR_PATH_PERSISTENT;
-      std::vector<double> xs((size_t)N * kb);
-      ANOMOD_HIP(ctx, hipMemcpyAsync(xs.data(), g->bx[0], xs.size() * 8, hipMemcpyDeviceToHost,
+      const double* xs = g->h_bpin;
+      ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_bpin, g->bx[0], (size_t)N * kb * 8, hipMemcpyDeviceToHost,
                                      ctx->stream));
       ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
       for (uint32_t k = 0; k < K; ++k)
@@ -1356,8 +1410,7 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
     // a workgroup never became resident: start over per launch from x0
     ++g->fallbacks;
     fell_back = true;
-    ANOMOD_HIP(ctx, hipMemcpyAsync(g->bx[0], x0.data(), x0.size() * 8, hipMemcpyHostToDevice,
-                                   ctx->stream));
+    ANOMOD_HIP(ctx, init_x0());
     ANOMOD_HIP(ctx, hipMemcpyAsync(g->bacc, g->host_bacc.data(), g->host_bacc.size() * 8,
                                    hipMemcpyHostToDevice, ctx->stream));
     if (int rc = stage_begin(ctx, kStagePagerank)) return rc;
@@ -1384,9 +1437,9 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   g->last_path = tol > 0.0 ? ANOMOD_PPR_PATH_READBACK : ANOMOD_PPR_PATH_GRAPH;
   if (fell_back) g->last_path |= ANOMOD_PPR_PATH_FALLBACK;
   if (int rc = stage_end(ctx, kStagePagerank)) return rc;
-  std::vector<double> xs((size_t)N * kb);
-  ANOMOD_HIP(ctx, hipMemcpyAsync(xs.data(), g->bx[done & 1], xs.size() * 8, hipMemcpyDeviceToHost,
-                                 ctx->stream));
+  const double* xs = g->h_bpin;
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_bpin, g->bx[done & 1], (size_t)N * kb * 8,
+                                 hipMemcpyDeviceToHost, ctx->stream));
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (uint32_t k = 0; k < K; ++k)
     for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];

@@ -165,8 +165,7 @@ def main() -> int:
         print(json.dumps(kernels, indent=1))
         hl = next((v for k, v in kernels.items() if k.startswith("headline")), None)
         if hl and ref:
-            d = dict(kernel="edge_agg_kernel", round=tag, n_spans=ref["config"]["spans_per_gpu"],
-                     correction=CORR, **hl)
+            d = dict(hl, round=tag, n_spans=ref["config"]["spans_per_gpu"], correction=CORR)
             (out / "edge_agg_pmc.json").write_text(json.dumps(d, indent=1) + "\n")
     # the headline kernel's own dispatches in the bench process's trace: the
     # first warmup call runs the form-unknown instantiation <1, 1, true, 1>;
