@@ -176,33 +176,35 @@ __device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], i
 constexpr uint32_t kFwd = ANOMOD_FWD, kBwd = ANOMOD_BWD;
 static_assert(kFwd % 2 == 0 && kBwd % 2 == 0 && kFwd + kBwd <= 16, "bidirectional step");
 
+template <uint32_t FW = kFwd, uint32_t BW = kBwd>
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,
                                                  uint32_t i, uint64_t pid) {
-  uint32_t f = a;             // next forward block [f, f + kFwd)
+  static_assert(FW % 2 == 0 && BW % 2 == 0 && FW + BW <= 16, "bidirectional step");
+  uint32_t f = a;             // next forward block [f, f + FW)
   int32_t g = (int32_t)i - 1;  // backward blocks end at g (inclusive)
   while (true) {
-    // backward block [gb, gb + kBwd) clamped to start at the trace start
-    const int32_t gb0 = g - (int32_t)kBwd + 1;
+    // backward block [gb, gb + BW) clamped to start at the trace start
+    const int32_t gb0 = g - (int32_t)BW + 1;
     const uint32_t gb = gb0 < (int32_t)a ? a : (uint32_t)gb0;
-    uint64_t v[kFwd], w[kBwd];
+    uint64_t v[FW], w[BW];
 #pragma unroll
-    for (uint32_t j = 0; j < kFwd; ++j) v[j] = lsid[f + j];
+    for (uint32_t j = 0; j < FW; ++j) v[j] = lsid[f + j];
 #pragma unroll
-    for (uint32_t j = 0; j < kBwd; ++j) w[j] = lsid[gb + j];
+    for (uint32_t j = 0; j < BW; ++j) w[j] = lsid[gb + j];
     uint32_t mf = 0, mb = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < kFwd; ++j) mf |= (v[j] == pid ? 1u : 0u) << j;
+    for (uint32_t j = 0; j < FW; ++j) mf |= (v[j] == pid ? 1u : 0u) << j;
 #pragma unroll
-    for (uint32_t j = 0; j < kBwd; ++j) mb |= (w[j] == pid ? 1u : 0u) << j;
-    const uint32_t hi = (b - f) < kFwd ? (b - f) : kFwd;  // >= 1 while f < b
+    for (uint32_t j = 0; j < BW; ++j) mb |= (w[j] == pid ? 1u : 0u) << j;
+    const uint32_t hi = (b - f) < FW ? (b - f) : FW;  // >= 1 while f < b
     mf &= (1u << hi) - 1u;
     // backward lanes past g (the clamp re-reads) or with g < a hold nothing new
     const int32_t nb = g - (int32_t)gb + 1;
     mb &= nb > 0 ? (1u << (uint32_t)nb) - 1u : 0u;
     if (mf) return (int)(f + __ffs(mf) - 1u);
     if (mb) return (int)(gb + 31u - __clz(mb));  // unique ids: any match is the match
-    f += kFwd;
-    g -= (int32_t)kBwd;
+    f += FW;
+    g -= (int32_t)BW;
     if (f >= b) return -1;
   }
 }

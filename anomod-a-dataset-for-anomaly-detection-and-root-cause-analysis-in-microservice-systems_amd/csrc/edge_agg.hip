@@ -115,7 +115,8 @@ constexpr int kOffWave = kOffCtl + 16;
 // away this many inserts stops: its waves hand their remaining traces to the
 // compact-form resume launch (edge_agg_kernel, kModeAuto / kModeResume).
 constexpr uint32_t kSatFails = 64;
-enum LaunchMode : uint32_t { kModeNormal = 0, kModeAuto = 1, kModeResume = 2 };
+// kModeWideScan: kModeNormal with the wide parent scan (process_chunk)
+enum LaunchMode : uint32_t { kModeNormal = 0, kModeAuto = 1, kModeResume = 2, kModeWideScan = 3 };
 enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2, kStWide = 3 };
 constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
 constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
@@ -433,7 +434,11 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
   return -1;
 }
 
-template <int HT, int ST, bool UNI>
+// Scan widths of the bidirectional parent scan: (kFwd, kBwd) = (6, 4) for
+// collector-ordered traces of tens of spans (SN / TrainTicket: 8 / 8 measured
+// 2-10 % slower there), (8, 8) for sets holding traces longer than a chunk
+// (LONG: random ancestors in 128- and 256-span traces, 7.52 vs 8.09 ms).
+template <int HT, int ST, bool UNI, bool WIDE = false>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
                                               const Chunk& c, const Regs& R, uint32_t S,
                                               const Table& tab) {
@@ -466,7 +471,8 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
         trace_bounds(Sm, r, lane, c.n, a, b);
-        const int q = UNI ? find_parent_bidir(lsid, a, b, i, R.pid[r])
+        const int q = UNI ? (WIDE ? find_parent_bidir<8, 8>(lsid, a, b, i, R.pid[r])
+                                  : find_parent_bidir(lsid, a, b, i, R.pid[r]))
                           : find_parent(lsid, a, b, R.pid[r]);
         if (q >= 0) p = lsvc[q];
       } else {  // ablation: a parent-like edge without the lookup (keeps key diversity)
@@ -1324,7 +1330,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       if (cur.k == 0) {  // a trace longer than kStage: listed for edge_big_kernel
         if (lane == 0) tab.big_list[atomicAdd(&tab.big[0], 1ull)] = tab.t_base + t_cur;
       } else {
-        process_chunk<HT, ST, UNI>(smem, wsm, lane, cur, R, S, tab);
+        process_chunk<HT, ST, UNI, MODE == kModeWideScan>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
@@ -1574,7 +1580,7 @@ struct Pick {
 
 // mode: kModeAuto only for the pair forms, kModeResume only for the compact
 // forms of the SN / TrainTicket widths (the instantiations that exist).
-Pick pick_kernel(uint32_t E, bool compact, bool uni, int mode = kModeNormal) {
+Pick pick_kernel(uint32_t E, bool compact, bool uni, int mode = kModeNormal, bool long_set = false) {
   const uint64_t keys = (uint64_t)E * kBins + 1;  // largest stored key
   const bool lds_hist = keys < (1ull << 31);  // >= 1 count bit above the key
 #define ANOMOD_PICK(H, S_, NAME)                                                               \
@@ -1589,6 +1595,9 @@ Pick pick_kernel(uint32_t E, bool compact, bool uni, int mode = kModeNormal) {
     ANOMOD_PICK_M(kHtCompact, kStWide, kModeResume, "edge_agg_kernel<lds_compact_hist,wide_stats,resume>");
   if (lds_hist && E > kLdsEdges && E <= kWideEdges && !compact && mode == kModeAuto)
     ANOMOD_PICK_M(kHtPair, kStWide, kModeAuto, "edge_agg_kernel<lds_hist,wide_stats,auto>");
+  if (lds_hist && E <= kLdsEdges && compact && uni && long_set && mode == kModeNormal)
+    return Pick{edge_agg_kernel<kHtCompact, kStDirect, true, kModeWideScan>, kHtCompact, kStDirect,
+                "edge_agg_kernel<lds_compact_hist,lds_stats,wide_scan>"};
   if (lds_hist && E <= kLdsEdges && compact)  // a set that overflowed the pair table
     ANOMOD_PICK(kHtCompact, kStDirect, "edge_agg_kernel<lds_compact_hist,lds_stats>");
   if (lds_hist && E <= kLdsEdges) ANOMOD_PICK(kHtPair, kStDirect, "edge_agg_kernel<lds_hist,lds_stats>");
@@ -1870,7 +1879,9 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   const int form = hist_form_of(spans);
   const bool uni = use_unique(spans);
   const bool autof = form < 0 && pick_kernel(E, false, uni).ht == kHtPair;
-  const Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal);
+  // (a set with traces longer than a chunk: LONG-like, the wide parent scan)
+  const bool long_set = spans->max_trace_len != ~0ull && spans->max_trace_len > (uint64_t)kBigMin;
+  const Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal, long_set);
   const Pick pr = autof ? pick_kernel(E, true, uni, kModeResume) : pk;  // the resume launch's form
   // As many workgroups as are resident at once (LDS / registers decide).
   int per_cu = 0, per_cu_r = 0;

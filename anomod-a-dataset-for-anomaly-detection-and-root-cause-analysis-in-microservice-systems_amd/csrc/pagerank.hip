@@ -626,7 +626,10 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
     const double* __restrict__ p, double alpha, double* x0, double* x1, unsigned long long* acc,
     uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit, double* ring,
     uint64_t slot) {
-  constexpr uint32_t kLdsE = 6144u;  // 48 KB of (col, w): 3 workgroups per CU
+  // 24 KB of (col, w) (~1 800 in-edges per 256-row block at N = 10^5; the
+  // rest from global memory) + the store staging: three workgroups per CU
+  // (the residency check admits per-CU occupancy minus one)
+  constexpr uint32_t kLdsE = 3072u;
   constexpr int S = kAccSlots * K;   // one accumulator block: K x kAccSlots
   constexpr int kNW = kPprThreads / 64;
   __shared__ uint32_t lcol[kLdsE];
@@ -830,6 +833,30 @@ PersistentFn persistent_fn(int sub, bool ring) {
                                                                : ppr_persistent_kernel<1, false>;
 }
 
+// A batch's personalizations: raw [K][N] -> normalised node-major [N][kb]
+// (padded vectors repeat vector 0), p / sum with the host's sum.
+struct BatchNorm {
+  double psum[16];
+};
+__global__ __launch_bounds__(kPprThreads) void ppr_batch_norm_kernel(const double* __restrict__ raw,
+                                                                     uint32_t N, uint32_t K,
+                                                                     uint32_t kb, BatchNorm bn,
+                                                                     double* __restrict__ bp) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    for (uint32_t k = 0; k < kb; ++k) {
+      const uint32_t src = k < K ? k : 0u;
+      bp[(uint64_t)i * kb + k] = raw[(uint64_t)src * N + i] / bn.psum[src];
+    }
+}
+// node-major [N][kb] -> [K][N]
+__global__ __launch_bounds__(kPprThreads) void ppr_batch_out_kernel(const double* __restrict__ x,
+                                                                    uint32_t N, uint32_t K,
+                                                                    uint32_t kb,
+                                                                    double* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    for (uint32_t k = 0; k < K; ++k) out[(uint64_t)k * N + i] = x[(uint64_t)i * kb + k];
+}
+
 using BatchFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*, const uint8_t*,
                         const double*, double, double*, double*, unsigned long long*, uint32_t,
                         double, unsigned int*, uint32_t, double*, uint64_t);
@@ -839,6 +866,20 @@ BatchFn batch_persistent_fn(uint32_t kb, bool ring) {
          : kb == 8 ? ppr_batch_persistent_kernel<8, true> : ppr_batch_persistent_kernel<16, true>;
   return kb == 2 ? ppr_batch_persistent_kernel<2, false> : kb == 4 ? ppr_batch_persistent_kernel<4, false>
        : kb == 8 ? ppr_batch_persistent_kernel<8, false> : ppr_batch_persistent_kernel<16, false>;
+}
+
+// The batch result x ([N][kb] on the device) -> X ([K][N] on the host)
+// through `tmp` (a free device vector buffer) and the pinned staging.
+hipError_t batch_out(anomod_ctx* ctx, anomod_graph* g, const double* x, double* tmp, uint32_t N,
+                     uint32_t K, uint32_t kb, double* X) {
+  hipLaunchKernelGGL(ppr_batch_out_kernel, dim3(std::min<uint32_t>((N + kPprThreads - 1) / kPprThreads, 2048)),
+                     dim3(kPprThreads), 0, ctx->stream, x, N, K, kb, tmp);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g->h_bpin, tmp, (size_t)N * K * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) memcpy(X, g->h_bpin, (size_t)N * K * 8);
+  return e;
 }
 
 void free_graph(anomod_graph* g) {
@@ -1270,17 +1311,8 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   const uint32_t N = g->N;
   const uint32_t kb = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16;  // padded with vector 0
   // node-major, normalised personalizations
-  std::vector<double> psums(kb);
-  for (uint32_t k = 0; k < kb; ++k) {
-    const double* pk = P + (size_t)(k < K ? k : 0) * N;
-    double s = 0.0;
-    const uint32_t bad = personalization_sum<false>(pk, N, nullptr, s);
-    ANOMOD_REQUIRE(ctx, bad == N, "personalization[%u][%u] invalid", k, bad);
-    ANOMOD_REQUIRE(ctx, s > 0.0, "personalization %u sums to zero", k);
-    psums[k] = s;
-  }
   if (int rc = bind(ctx)) return rc;
-  // pinned node-major staging of P in and X out (grow-only)
+  // pinned staging of P in and X out, [K][N] as the caller's (grow-only)
   if (g->h_bpin_n < (uint64_t)N * kb) {
     if (g->h_bpin) ANOMOD_HIP(ctx, hipHostFree(g->h_bpin));
     g->h_bpin = nullptr;
@@ -1289,10 +1321,16 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
                                   hipHostMallocDefault));
     g->h_bpin_n = (uint64_t)N * kb;
   }
-  double* pn = g->h_bpin;
-  for (uint32_t k = 0; k < kb; ++k) {
-    const double* pk = P + (size_t)(k < K ? k : 0) * N;
-    for (uint32_t i = 0; i < N; ++i) pn[(size_t)i * kb + k] = pk[i] / psums[k];
+  // the checking-and-summing pass copies each vector into the staging (the
+  // single solve's order); the device divides (the same IEEE division: the
+  // same bits) and transposes to node-major
+  BatchNorm bn{};
+  for (uint32_t k = 0; k < K; ++k) {
+    double s = 0.0;
+    const uint32_t bad = personalization_sum<true>(P + (size_t)k * N, N, g->h_bpin + (size_t)k * N, s);
+    ANOMOD_REQUIRE(ctx, bad == N, "personalization[%u][%u] invalid", k, bad);
+    ANOMOD_REQUIRE(ctx, s > 0.0, "personalization %u sums to zero", k);
+    bn.psum[k] = s;
   }
   if (g->kb < kb) {
     for (void* q : {(void*)g->bp, (void*)g->bx[0], (void*)g->bx[1], (void*)g->bacc})
@@ -1311,9 +1349,12 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
     g->host_bacc.assign(6ull * kb * kAccSlots, 0ull);
   }
   const int S = kAccSlots * (int)kb;  // one accumulator block = kb x kAccSlots
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bp, pn, (size_t)N * kb * 8, hipMemcpyHostToDevice,
+  // raw vectors through bx[1] (free until the first iteration writes it)
+  ANOMOD_HIP(ctx, hipMemcpyAsync(g->bx[1], g->h_bpin, (size_t)N * K * 8, hipMemcpyHostToDevice,
                                  ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the staging is reused for X
+  hipLaunchKernelGGL(ppr_batch_norm_kernel, dim3(std::min<uint32_t>((N + kPprThreads - 1) / kPprThreads, 2048)),
+                     dim3(kPprThreads), 0, ctx->stream, g->bx[1], N, K, kb, bn, g->bp);
+  ANOMOD_HIP(ctx, hipGetLastError());
   const uint32_t nx = N * kb;  // x0 = 1/N everywhere, on the device
   auto init_x0 = [&]() {
     hipLaunchKernelGGL(ppr_init_kernel, dim3(std::min<uint32_t>((nx + kPprThreads - 1) / kPprThreads, 2048)),
@@ -1398,12 +1439,7 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
     if (hb[1] == 0u) {
       done = hb[2];
       g->last_path = ANOMOD_PPR_PATH_PERSISTENT;
-      const double* xs = g->h_bpin;
-      ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_bpin, g->bx[0], (size_t)N * kb * 8, hipMemcpyDeviceToHost,
-                                     ctx->stream));
-      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      for (uint32_t k = 0; k < K; ++k)
-        for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];
+      ANOMOD_HIP(ctx, batch_out(ctx, g, g->bx[0], g->bx[1], N, K, kb, X));
       if (iters_done) *iters_done = done;
       return ANOMOD_OK;
     }
@@ -1437,12 +1473,7 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   g->last_path = tol > 0.0 ? ANOMOD_PPR_PATH_READBACK : ANOMOD_PPR_PATH_GRAPH;
   if (fell_back) g->last_path |= ANOMOD_PPR_PATH_FALLBACK;
   if (int rc = stage_end(ctx, kStagePagerank)) return rc;
-  const double* xs = g->h_bpin;
-  ANOMOD_HIP(ctx, hipMemcpyAsync(g->h_bpin, g->bx[done & 1], (size_t)N * kb * 8,
-                                 hipMemcpyDeviceToHost, ctx->stream));
-  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  for (uint32_t k = 0; k < K; ++k)
-    for (uint32_t i = 0; i < N; ++i) X[(size_t)k * N + i] = xs[(size_t)i * kb + k];
+  ANOMOD_HIP(ctx, batch_out(ctx, g, g->bx[done & 1], g->bx[(done & 1) ^ 1], N, K, kb, X));
   if (iters_done) *iters_done = done;
   return ANOMOD_OK;
 }

@@ -37,6 +37,7 @@ with anomod.Context(0) as ctx:
                 "us_per_iter": round(k_ms * 1e3 / done, 3), "wall_ms": round(wall, 3),
                 "vector_iters_per_s": round(K * done / (k_ms * 1e-3)),
                 "equal": bool(np.array_equal(X, ref)), "path": g.last_solve()[0]})
+        res["paths"] = sorted({x["path"] for v in res.values() if isinstance(v, list) for x in v})
         print(json.dumps(res), flush=True)
     os.environ.pop("ANOMOD_PPR_MODE", None)
     g.free()

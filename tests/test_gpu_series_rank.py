@@ -319,6 +319,16 @@ def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K):
     g.free()
 
 
+def test_pagerank_batch_bench_config_is_persistent(ctx):
+    """The bench's batch (config 5: N = 10^5, 8 vectors) fits one resident
+    grid (391 workgroups of 256 threads, three per CU on 256 CUs), so it runs
+    as one persistent launch."""
+    g = anomod.DeviceGraph(ctx, synthetic=(100000, 10, 11))
+    X, d = g.pagerank_batch(np.random.default_rng(3).random((8, g.N)), iters=5)
+    assert d == 5 and g.last_solve()[0] == "persistent"
+    g.free()
+
+
 @pytest.mark.parametrize("G", [1, 2, 3, 8, 500])
 def test_pagerank_row_sharded_equals_unsharded(ctx, monkeypatch, G):
     """Row-sharded solve rehearsed on one device (G row shards of whole 256-row
