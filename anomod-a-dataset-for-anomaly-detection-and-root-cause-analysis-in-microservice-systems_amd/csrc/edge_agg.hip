@@ -731,7 +731,10 @@ __device__ void big_one(unsigned char* smem, const uint64_t* __restrict__ span_i
 // ids of different traces never meet, and a workgroup pays the
 // load / insert / lookup round trips once per batch instead of once per
 // trace.  <= 2 spans per thread (sum L_i <= kBigWin = 2 x kBigThreads).
-constexpr int kGroup = 4;  // traces per ticket (one atomic, their entries and bounds loaded together)
+#ifndef ANOMOD_BIG_GROUP
+#define ANOMOD_BIG_GROUP 4
+#endif
+constexpr int kGroup = ANOMOD_BIG_GROUP;  // traces per ticket (one atomic, their entries and bounds loaded together)
 static_assert(kBigWin == 2 * kBigThreads, "a packed batch is two spans per thread");
 
 __device__ __forceinline__ uint32_t big_region_slot(uint64_t id, uint32_t size) {
@@ -928,8 +931,15 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
 // listed spans (16 traces per ticket, one load round trip per ticket) into
 // the chunk walk's tables.  Same first-match rule, same table forms.
 constexpr int kResThreads = 512;
-constexpr uint32_t kResWin = 2048;                 // ids per table window
-constexpr uint32_t kResSlots = 4096;               // load <= 1/2
+#ifndef ANOMOD_RES_WIN
+#define ANOMOD_RES_WIN 2048
+#endif
+constexpr uint32_t kResWin = ANOMOD_RES_WIN;       // ids per table window
+constexpr uint32_t kResSlots = 2 * kResWin;        // load <= 1/2
+static_assert((kResSlots & (kResSlots - 1)) == 0, "power-of-two table");
+__device__ __forceinline__ uint32_t res_slot(uint64_t id) {
+  return (uint32_t)((id * 0x9E3779B97F4A7C15ull) >> 32) & (kResSlots - 1u);
+}
 constexpr int kResPer = (int)kResWin / kResThreads;  // spans per thread in a packed window
 static_assert(kResWin % kResThreads == 0 && kResWin <= 65536, "window: whole rows, pos << 16 | svc");
 
@@ -967,7 +977,7 @@ __device__ void res_one(unsigned long long* bkey, uint32_t* bval,
         const uint64_t id = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
         if (id == 0ull) continue;
         const uint32_t sv = svcfl[lo + w0 + k] & 0xFFFFu;
-        for (uint32_t sl = big_slot(id);; sl = (sl + 1u) & (kResSlots - 1u)) {
+        for (uint32_t sl = res_slot(id);; sl = (sl + 1u) & (kResSlots - 1u)) {
           const unsigned long long prev = atomicCAS(&bkey[sl], 0ull, (unsigned long long)id);
           if (prev == 0ull || prev == id) {
             atomicMin(&bval[sl], (k << 16) | sv);  // the first position wins, with its service
@@ -980,7 +990,7 @@ __device__ void res_one(unsigned long long* bkey, uint32_t* bval,
 #pragma unroll
       for (int r = 0; r < kBigPer; ++r) {
         if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
-        for (uint32_t sl = big_slot(pid[r]);; sl = (sl + 1u) & (kResSlots - 1u)) {
+        for (uint32_t sl = res_slot(pid[r]);; sl = (sl + 1u) & (kResSlots - 1u)) {
           const unsigned long long key = bkey[sl];
           if (key == pid[r]) {
             psv[r] = bval[sl] & 0xFFFFu;
