@@ -75,6 +75,10 @@ constexpr uint32_t kBins = ANOMOD_HIST_BINS;
 #ifndef ANOMOD_ABL
 #define ANOMOD_ABL 0
 #endif
+#ifndef ANOMOD_LOAD16
+#define ANOMOD_LOAD16 0
+#endif
+static_assert(!ANOMOD_LOAD16 || (ANOMOD_ABL & 16), "16-B loads: stream-only timing builds");
 
 // LDS carve (bytes, every offset a multiple of 16).
 constexpr int kOffHt = 0;                      // u32 keys (pair) | u32 slots (compact); 0 = empty
@@ -398,6 +402,28 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
   const auto rpid = rsrc(col.parent + c.base, n * 8u);
   const auto rsf = rsrc(col.svcfl + c.base, n * 4u);
   const auto rdur = rsrc(col.dur + c.base, n * 4u);
+#if ANOMOD_LOAD16  // timing experiment (stream-only builds): 16 B per lane and load
+  static_assert(kPer == 4, "16-B loads: 4 rows");
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t i = (uint32_t)(j * 128 + 2 * lane);
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsid, (int)(i * 8u), 0, ANOMOD_LOAD_AUX);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rpid, (int)(i * 8u), 0, ANOMOD_LOAD_AUX);
+    R.sid[2 * j] = ((uint64_t)a[1] << 32) | a[0];
+    R.sid[2 * j + 1] = ((uint64_t)a[3] << 32) | a[2];
+    R.pid[2 * j] = ((uint64_t)b[1] << 32) | b[0];
+    R.pid[2 * j + 1] = ((uint64_t)b[3] << 32) | b[2];
+  }
+  {
+    const auto c = __builtin_amdgcn_raw_buffer_load_b128(rsf, (int)(lane * 16u), 0, ANOMOD_LOAD_AUX);
+    const auto d = __builtin_amdgcn_raw_buffer_load_b128(rdur, (int)(lane * 16u), 0, ANOMOD_LOAD_AUX);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      R.sf[r] = c[r];
+      R.dur[r] = d[r];
+    }
+  }
+#else
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = (uint32_t)lane + (uint32_t)(r * kWave);
@@ -406,6 +432,7 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
     R.sf[r] = bload32(rsf, i * 4u);
     R.dur[r] = bload32(rdur, i * 4u);
   }
+#endif
 }
 
 // First span of [a, b) whose id equals pid: kScan ids per step (ds_read2_b64
