@@ -46,7 +46,11 @@ using chunk::wave_sync;
 // Experiment-only builds (never set in the shipped library):
 //  2 = level A stores nothing, then the LSD path groups (timing of level A's
 //      loads and ranking only);
-//  4 = nontemporal record stores in level A.
+//  4 = nontemporal record stores in level A;
+//  8 = small bucket kernel: no record gathers (records made from the pairs);
+// 16 = small bucket kernel: no column / trace-start stores;
+// 32 = small bucket kernel: no in-LDS ranking (arrival order kept).
+// (8 / 16 / 32 give wrong groupings: timing only.)
 
 
 #ifndef ANOMOD_BK_ABL
@@ -792,28 +796,18 @@ __device__ void bucket_edges(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m
   }
 }
 
-// Bucket c = [a0, a0 + m) of the pairs `pin` (in arrival order inside the
-// bucket; every key shares its top T bits), its pairs k / v and — REG, the
-// small kernel — its records ra / rb already in registers (the big kernel
-// gathers the keys itself).  Split once more by the next 9 key bits (stable);
-// a sub-bucket holding one key is already in arrival order, a mixed one ranks
-// each pair by compares: rank = #{smaller pair} (a pair orders by (key bits,
-// position) and positions are arrival order).  The records come from `rec` by
-// position.  Writes the grouped columns of the bucket, its trace starts over
-// the bucket's own pairs (pin[a0 + ordinal], read before) and the trace count
-// dcnt[c] — or, EDGE, its edge records.
+// The bucket's final order in LDS (sfinal: arrival -> final position; sflag:
+// trace starts by final position).
 template <int W, int PER, bool EDGE, int R>
-__device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
-                            uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
-                            EdgeOut eo, int kshift, uint32_t* __restrict__ dcnt,
-                            const uint64_t (&k)[PER], const bool (&v)[PER], const uint4 (&ra)[R],
-                            const uint4 (&rb)[R]) {
+__device__ void bucket_rank(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m,
+                            const GRec* __restrict__ rec, int kshift, const uint64_t (&k)[PER],
+                            const bool (&v)[PER], const uint4 (&ra)[R], const uint4 (&rb)[R]) {
   constexpr int kCap = W * PER, kNW = W / kWv;
-  static_assert(W >= kSub, "one thread per sub-digit");
   constexpr bool REG = R == PER;
   auto& P = L.u.pre;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   (void)kCap;
+  (void)a0;
   uint64_t fk[PER];
   uint32_t e[PER], off[PER];
   if constexpr (!REG) {
@@ -938,6 +932,7 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
     const uint32_t f = (uint32_t)(tid + j * W);
     clash |= f > 0 && f < m && !P.sflag[f] && P.skey[f] != P.skey[f - 1];
   }
+  if constexpr ((ANOMOD_BK_ABL & 8) != 0) clash = false;  // timing: keys are not the records'
   if (__syncthreads_or(clash)) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -962,10 +957,20 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
     __syncthreads();
   }
 
-  if constexpr (EDGE) {
-    bucket_edges(L, a0, m, k, v, ra, rb, rec, eo);
-    return;
-  }
+}
+
+// The bucket in final order out: its grouped columns (records by final
+// position), its trace starts over the bucket's own pairs (pin[a0 +
+// ordinal], read before) and its trace count dcnt[c].
+template <int W, int PER, bool EDGE, int R>
+__device__ void bucket_emit(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
+                            uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+                            uint32_t* __restrict__ dcnt, const uint64_t (&k)[PER],
+                            const bool (&v)[PER], const uint4 (&ra)[R], const uint4 (&rb)[R]) {
+  constexpr int kNW = W / kWv;
+  constexpr bool REG = R == PER;
+  auto& P = L.u.pre;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   // trace starts: ordinals in final order (written last: over the bucket's
   // own pairs, read until then)
   uint32_t cnt = 0;
@@ -999,6 +1004,10 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
         x1 = q[1];
       }
       const uint32_t i = L.sfinal[p];
+      if constexpr ((ANOMOD_BK_ABL & 16) != 0) {  // timing: no stores
+        if (x0.x == 0x12345678u && x1.w == 0x9ABCDEF0u) out.sf[a0 + i] = i;
+        continue;
+      }
       if (out.h) out.h[a0 + i] = ((uint64_t)x0.y << 32) | x0.x;  // (aggregate-only calls: none)
       out.sid[a0 + i] = ((uint64_t)x0.w << 32) | x0.z;
       out.pid[a0 + i] = ((uint64_t)x1.y << 32) | x1.x;
@@ -1012,6 +1021,49 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
     if ((fl >> j) & 1u) pin[a0 + ord++] = (uint64_t)a0 + (uint32_t)(tid * PER + j);
   if (tid == 0) dcnt[c] = nt;
 }
+
+// Bucket c = [a0, a0 + m) of the pairs `pin` (in arrival order inside the
+// bucket; every key shares its top T bits), its pairs k / v and — REG, the
+// small kernel — its records ra / rb already in registers (the big kernel
+// gathers the keys itself).  Split once more by the next 9 key bits (stable);
+// a sub-bucket holding one key is already in arrival order, a mixed one ranks
+// each pair by compares: rank = #{smaller pair} (a pair orders by (key bits,
+// position) and positions are arrival order).  The records come from `rec` by
+// position.  Writes the grouped columns of the bucket, its trace starts over
+// the bucket's own pairs (pin[a0 + ordinal], read before) and the trace count
+// dcnt[c] — or, EDGE, its edge records.
+template <int W, int PER, bool EDGE, int R>
+__device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
+                            uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
+                            EdgeOut eo, int kshift, uint32_t* __restrict__ dcnt,
+                            const uint64_t (&k)[PER], const bool (&v)[PER], const uint4 (&ra)[R],
+                            const uint4 (&rb)[R]) {
+  constexpr int kCap = W * PER, kNW = W / kWv;
+  static_assert(W >= kSub, "one thread per sub-digit");
+  constexpr bool REG = R == PER;
+  auto& P = L.u.pre;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  (void)kCap;
+  if constexpr ((ANOMOD_BK_ABL & 32) != 0 && REG) {  // timing: arrival order, every span a trace
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+      if (v[j]) {
+        L.sfinal[p] = (uint16_t)p;
+        L.u.pre.sflag[p] = 1;
+      }
+    }
+    __syncthreads();
+  } else {
+  bucket_rank<W, PER, EDGE, R>(L, a0, m, rec, kshift, k, v, ra, rb);
+  }
+  if constexpr (EDGE) {
+    bucket_edges(L, a0, m, k, v, ra, rb, rec, eo);
+    return;
+  }
+  bucket_emit<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, dcnt, k, v, ra, rb);
+}
+
 
 
 // One bucket by one workgroup: the size checks (over-size buckets listed for
@@ -1063,6 +1115,11 @@ __device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t
   if constexpr (REG) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {  // the gathers: issued together, after every pair load
+      if constexpr ((ANOMOD_BK_ABL & 8) != 0) {
+        ra[j] = make_uint4((uint32_t)k[j], (uint32_t)(k[j] >> 32), (uint32_t)k[j], 0u);
+        rb[j] = make_uint4((uint32_t)(k[j] >> 32), 0u, 0u, 0u);
+        continue;
+      }
       const uint4* q = reinterpret_cast<const uint4*>(rec + (uint32_t)k[j]);
       ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
       rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
