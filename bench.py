@@ -389,8 +389,8 @@ def load_traffic(n_spans: int) -> float | None:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--traces-per-gpu", type=int, default=1 << 27)
     ap.add_argument("--seed", type=int, default=20251103)
     ap.add_argument("--cpu-traces", type=int, default=1 << 21)
