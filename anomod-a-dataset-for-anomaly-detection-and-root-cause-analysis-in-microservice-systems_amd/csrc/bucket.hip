@@ -81,6 +81,10 @@ constexpr int kSub = 1 << kSubBits;
 #endif
 constexpr int kSmallW = 512, kSmallPer = ANOMOD_BK_SPER;  // per-bucket kernel: 2048 spans
 constexpr int kBigW = 1024, kBigPer = 8;       // oversized buckets: 8192 spans
+#ifndef ANOMOD_BK_RANK
+#define ANOMOD_BK_RANK 0  // small bucket kernel: 0 = stable split, 1 = atomic slots + compare rank
+#endif
+constexpr bool kRankAtomic = ANOMOD_BK_RANK != 0;
 constexpr int kDChunk = 4096;                  // entries per partial sum of the trace-count scan
 
 // Exclusive scan of one value per thread across a workgroup of NW waves;
@@ -796,6 +800,38 @@ __device__ void bucket_edges(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m
   }
 }
 
+// Two traces of a bucket whose keys agree in every bit the pairs carry: the
+// bucket ranked by (full key, arrival) instead (rare: O(m^2) compares by
+// every thread).  Every thread calls it (barriers).
+template <int W, int PER, bool EDGE>
+__device__ void bucket_rerank_exact(BucketLds<W, PER, EDGE>& L, uint32_t m,
+                                    const uint64_t (&fk)[PER], const bool (&v)[PER]) {
+  auto& P = L.u.pre;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  (void)tid;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if (v[j]) P.skey[p] = fk[j];  // full keys by arrival position
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    if (v[j]) {
+      uint32_t rank = 0, first = 1;
+      for (uint32_t q = 0; q < m; ++q) {
+        const uint64_t kq = P.skey[q];
+        rank += (kq < fk[j] || (kq == fk[j] && q < p)) ? 1u : 0u;
+        first &= (kq == fk[j] && q < p) ? 0u : 1u;
+      }
+      L.sfinal[p] = (uint16_t)rank;
+      P.sflag[rank] = (uint8_t)first;
+    }
+  }
+  __syncthreads();
+}
+
 // The bucket's final order in LDS (sfinal: arrival -> final position; sflag:
 // trace starts by final position).
 template <int W, int PER, bool EDGE, int R>
@@ -933,30 +969,99 @@ __device__ void bucket_rank(BucketLds<W, PER, EDGE>& L, uint32_t a0, uint32_t m,
     clash |= f > 0 && f < m && !P.sflag[f] && P.skey[f] != P.skey[f - 1];
   }
   if constexpr ((ANOMOD_BK_ABL & 8) != 0) clash = false;  // timing: keys are not the records'
-  if (__syncthreads_or(clash)) {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-      if (v[j]) P.skey[p] = fk[j];  // full keys by arrival position
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint32_t p = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-      if (v[j]) {
-        uint32_t rank = 0, first = 1;
-        for (uint32_t q = 0; q < m; ++q) {
-          const uint64_t kq = P.skey[q];
-          rank += (kq < fk[j] || (kq == fk[j] && q < p)) ? 1u : 0u;
-          first &= (kq == fk[j] && q < p) ? 0u : 1u;
-        }
-        L.sfinal[p] = (uint16_t)rank;
-        P.sflag[rank] = (uint8_t)first;
-      }
-    }
-    __syncthreads();
-  }
+  if (__syncthreads_or(clash)) bucket_rerank_exact<W, PER, EDGE>(L, m, fk, v);
 
+}
+
+// Small-kernel ranking without the stable split (ANOMOD_BK_RANK=1): each span
+// takes a slot in its sub-bucket with one LDS atomic (any order), the
+// sub-bucket starts come from one block scan, and a span's final position is
+// a + #{pairs of its sub-bucket below its own} — pairs are distinct and order
+// by (key bits, arrival), so this is the stable order however the slots were
+// taken.  The compare loop is O(s) per span, so a bucket holding a sub-bucket
+// of more than kLongSub spans (a long trace) returns false and goes to the
+// large kernel's stable split.  The full-key check rides along: spans with
+// equal pair keys must have equal low 32 bits of k (the bucket and the pair
+// fix the other da + 32 >= 33), else the bucket is re-ranked exactly.
+constexpr uint32_t kLongSub = 128;
+template <int W, int PER, bool EDGE, int R>
+__device__ bool bucket_rank_atomic(BucketLds<W, PER, EDGE>& L, uint32_t m, int kshift,
+                                   const uint64_t (&k)[PER], const bool (&v)[PER],
+                                   const uint4 (&ra)[R]) {
+  static_assert(R == PER, "records in registers");
+  constexpr int kCap = W * PER, kNW = W / kWv;
+  static_assert(kNW * kSub * 2 >= kCap * 4, "low key words fit over the wave counters");
+  static_assert(W == kSub, "one thread per sub-digit");
+  auto& P = L.u.pre;
+  uint32_t* cnt = P.mixed;                                      // [kSub] spans per sub-bucket
+  uint32_t* sfk = reinterpret_cast<uint32_t*>(&P.wcnt[0][0]);  // [kCap] low key word, staged
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  uint64_t fk[PER];
+  uint32_t e[PER], o[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    fk[j] = mix64(((uint64_t)ra[j].y << 32) | ra[j].x);
+    e[j] = (uint32_t)(k[j] >> kshift) & (kSub - 1);
+  }
+  cnt[tid] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) o[j] = v[j] ? atomicAdd(&cnt[e[j]], 1u) : 0u;
+  __syncthreads();
+  const uint32_t tot = cnt[tid];
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kNW>(tot, L.wsum, &all);
+  P.tstart[tid] = pre;
+  if (tid == 0) P.tstart[kSub] = m;
+  if (__syncthreads_or(tot > kLongSub)) return false;  // (also orders tstart)
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (v[j]) {
+      const uint32_t sp = P.tstart[e[j]] + o[j];
+      P.skey[sp] = k[j];
+      sfk[sp] = (uint32_t)fk[j];
+      P.sorig[sp] = (uint16_t)(w * (PER * kWv) + j * kWv + lane);
+    }
+  }
+  __syncthreads();
+  bool clash = false;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t sp = (uint32_t)(tid + j * W);
+    if (sp < m) {
+      const uint64_t kp = P.skey[sp];
+      const uint32_t fp = sfk[sp];
+      const uint32_t ee = (uint32_t)(kp >> kshift) & (kSub - 1);
+      const uint32_t a = P.tstart[ee], b = P.tstart[ee + 1];
+      uint32_t rank = 0, first = 1;
+      if (b - a > 1u) {
+        for (uint32_t q0 = a; q0 < b; q0 += 4) {  // 4 pairs per step: one LDS round trip
+          uint64_t kq[4];
+          uint32_t fq[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint32_t q = q0 + t < b ? q0 + t : a;
+            kq[t] = P.skey[q];
+            fq[t] = sfk[q];
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const bool in = q0 + t < b;
+            const bool below = in && kq[t] < kp;  // pairs are distinct
+            const bool same = in && (kq[t] >> 32) == (kp >> 32);
+            rank += below ? 1u : 0u;
+            first &= (below && same) ? 0u : 1u;
+            clash |= same && fq[t] != fp;
+          }
+        }
+      }
+      const uint32_t f = a + rank;
+      P.sflag[f] = (uint8_t)first;
+      L.sfinal[P.sorig[sp]] = (uint16_t)f;
+    }
+  }
+  if (__syncthreads_or(clash)) bucket_rerank_exact<W, PER, EDGE>(L, m, fk, v);
+  return true;
 }
 
 // The bucket in final order out: its grouped columns (records by final
@@ -1032,18 +1137,18 @@ __device__ void bucket_emit(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
 // position.  Writes the grouped columns of the bucket, its trace starts over
 // the bucket's own pairs (pin[a0 + ordinal], read before) and the trace count
 // dcnt[c] — or, EDGE, its edge records.
-template <int W, int PER, bool EDGE, int R>
-__device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
+template <int W, int PER, bool EDGE, int R, bool ATOMIC = false>
+__device__ bool bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0, uint32_t m,
                             uint64_t* __restrict__ pin, const GRec* __restrict__ rec, SoaOut out,
                             EdgeOut eo, int kshift, uint32_t* __restrict__ dcnt,
                             const uint64_t (&k)[PER], const bool (&v)[PER], const uint4 (&ra)[R],
                             const uint4 (&rb)[R]) {
-  constexpr int kCap = W * PER, kNW = W / kWv;
   static_assert(W >= kSub, "one thread per sub-digit");
   constexpr bool REG = R == PER;
-  auto& P = L.u.pre;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  (void)kCap;
+  (void)tid;
+  (void)lane;
+  (void)w;
   if constexpr ((ANOMOD_BK_ABL & 32) != 0 && REG) {  // timing: arrival order, every span a trace
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -1054,14 +1159,17 @@ __device__ void bucket_body(BucketLds<W, PER, EDGE>& L, uint32_t c, uint32_t a0,
       }
     }
     __syncthreads();
+  } else if constexpr (ATOMIC) {
+    if (!bucket_rank_atomic<W, PER, EDGE, R>(L, m, kshift, k, v, ra)) return false;
   } else {
-  bucket_rank<W, PER, EDGE, R>(L, a0, m, rec, kshift, k, v, ra, rb);
+    bucket_rank<W, PER, EDGE, R>(L, a0, m, rec, kshift, k, v, ra, rb);
   }
   if constexpr (EDGE) {
     bucket_edges(L, a0, m, k, v, ra, rb, rec, eo);
-    return;
+    return true;
   }
   bucket_emit<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, dcnt, k, v, ra, rb);
+  return true;
 }
 
 
@@ -1125,7 +1233,17 @@ __device__ void bucket_sort_one(BucketLds<W, PER, EDGE>& L, uint32_t c, uint64_t
       rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
     }
   }
-  bucket_body<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, eo, kshift, dcnt, k, v, ra, rb);
+  if constexpr (W == kSmallW && kRankAtomic) {
+    if (!bucket_body<W, PER, EDGE, R, true>(L, c, a0, m, pin, rec, out, eo, kshift, dcnt, k, v, ra,
+                                            rb) &&
+        tid == 0) {  // a sub-bucket too long for the compare rank: the large kernel
+      const unsigned long long i = atomicAdd(over_n, 1ull);
+      if (i < over_cap) over[i] = c;
+      else atomicAdd(too_big, 1ull);
+    }
+  } else {
+    bucket_body<W, PER, EDGE, R>(L, c, a0, m, pin, rec, out, eo, kshift, dcnt, k, v, ra, rb);
+  }
 }
 
 #ifndef ANOMOD_BK_MINW
