@@ -401,3 +401,37 @@ def test_duplicate_ids_are_not_declared_unique(ctx):
     assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(sp))
     gen = ctx.generate(anomod.SynthSpec("SN", seed=3), 1000)
     assert gen.unique_ids and gen.download().check_unique_ids()
+
+
+@pytest.mark.parametrize("alias", [False, True])
+def test_long_set_wide_scan(ctx, monkeypatch, alias):
+    """Sets holding a trace longer than a chunk take the long-trace kernel
+    instantiation (8 / 8 bidirectional scan, compact form).  Traces of
+    49..256 spans with random ancestors, unique ids per trace; alias: every
+    trace reuses the same id values, so a chunk holds equal ids of different
+    traces (the scan stays inside the span's own trace).  Orphans, roots, a
+    300-span trace for the long-trace pass.  Equal to the oracle."""
+    monkeypatch.setenv("ANOMOD_HIST_FORM", "compact")
+    rng = np.random.default_rng(71 + alias)
+    lens = np.r_[rng.integers(49, 257, 600), rng.integers(1, 40, 400), [300]]
+    rng.shuffle(lens)
+    sp = _random_spanset(rng, 12, 0, 0, lens=lens)
+    if alias:  # ids 1..L inside each trace, parents remapped to them
+        ptr = sp.trace_ptr.astype(np.int64)
+        sid = np.empty(sp.n_spans, np.uint64)
+        remap = {}
+        for t in range(len(lens)):
+            a, b = ptr[t], ptr[t + 1]
+            new = np.arange(1, b - a + 1, dtype=np.uint64)
+            remap.update(zip(sp.span_id[a:b].tolist(), new.tolist()))
+            sid[a:b] = new
+        pid = np.array([remap.get(int(p), 10**12 + int(p) % 997) if p else 0
+                        for p in sp.parent_span_id], np.uint64)
+        sp = anomod.SpanSet(sp.services, sp.trace_ptr, sid.copy(), sid, pid, sp.svc, sp.flags,
+                            sp.dur_us)
+    assert sp.check_unique_ids()
+    ref = native.edge_aggregate(sp)
+    dev = ctx.upload(sp)
+    for _ in range(2):
+        assert_table_equal(ctx.edge_aggregate(dev), ref)
+    dev.free()
