@@ -661,10 +661,13 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
     rb = in_ptr[r];
     re = in_ptr[r + 1];
     dg = dangling[r] != 0;
+    // x0 = 1/N everywhere (the host fills it so): the row's previous value
+    // without a plain load of a buffer later iterations rewrite
+    const double x0v = 1.0 / (double)N;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       pr[k] = p[(uint64_t)r * K + k];
-      xr[k] = x0[(uint64_t)r * K + k];
+      xr[k] = x0v;
     }
   }
   if (threadIdx.x == 0) s_conv = 0u;
