@@ -1203,7 +1203,10 @@ __global__ __launch_bounds__(kResThreads, ANOMOD_RES_MINB) void edge_big_resolve
 // The listed spans into the tables, kRecGroup traces per ticket (wave 0 keeps
 // the next ticket's entries and bounds in flight).
 constexpr int kRecGroup = 16;
-constexpr int kRecPer = 4;
+#ifndef ANOMOD_REC_PER
+#define ANOMOD_REC_PER 4
+#endif
+constexpr int kRecPer = ANOMOD_REC_PER;  // listed spans per thread loaded together
 template <int HT, int ST>
 __global__ __launch_bounds__(kBigThreads) void edge_big_record_kernel(
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
