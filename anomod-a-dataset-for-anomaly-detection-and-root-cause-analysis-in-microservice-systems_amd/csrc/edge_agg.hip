@@ -1252,6 +1252,11 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_record_kernel(
     __syncthreads();
     const uint32_t tot = s_off[kRecGroup];
     if (tot == 0) break;  // tickets exhausted (listed traces are never empty)
+    // the ticket's trace offsets in scalar registers (uniform; read once, not
+    // per span)
+    uint32_t off[kRecGroup];
+#pragma unroll
+    for (int i = 0; i < kRecGroup; ++i) off[i] = __builtin_amdgcn_readfirstlane(s_off[i]);
     // kRecPer spans per thread loaded together, then recorded (the records'
     // LDS / HBM atomics would otherwise keep the next loads behind them)
     for (uint32_t q0 = tid; q0 < tot; q0 += kRecPer * kBigThreads) {
@@ -1260,9 +1265,14 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_record_kernel(
       for (int j = 0; j < kRecPer; ++j) {
         const uint32_t q = q0 + (uint32_t)j * kBigThreads;
         int t = 0;
+        uint32_t base = 0;
 #pragma unroll
-        for (int i = 1; i < kRecGroup; ++i) t = q >= s_off[i] ? i : t;
-        const uint64_t g = s_lo[t] + (q - s_off[t]);
+        for (int i = 1; i < kRecGroup; ++i) {
+          const bool in = q >= off[i];
+          t = in ? i : t;
+          base = in ? off[i] : base;
+        }
+        const uint64_t g = s_lo[t] + (q - base);
         const bool v = q < tot;
         sf[j] = v ? svcfl[g] : 0u;
         dr[j] = v ? dur[g] : 0u;
