@@ -176,9 +176,12 @@ __device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], i
 constexpr uint32_t kFwd = ANOMOD_FWD, kBwd = ANOMOD_BWD;
 static_assert(kFwd % 2 == 0 && kBwd % 2 == 0 && kFwd + kBwd <= 16, "bidirectional step");
 
-template <uint32_t FW = kFwd, uint32_t BW = kBwd>
+// MAXS > 0: give up after that many steps and return -2 (not found yet; the
+// caller completes the lookup cooperatively).
+template <uint32_t FW = kFwd, uint32_t BW = kBwd, int MAXS = 0>
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,
                                                  uint32_t i, uint64_t pid) {
+  int steps = 0;
   static_assert(FW % 2 == 0 && BW % 2 == 0 && FW + BW <= 16, "bidirectional step");
   uint32_t f = a;             // next forward block [f, f + FW)
   int32_t g = (int32_t)i - 1;  // backward blocks end at g (inclusive)
@@ -206,6 +209,32 @@ __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t 
     f += FW;
     g -= (int32_t)BW;
     if (f >= b) return -1;
+    if (MAXS > 0 && ++steps >= MAXS) return -2;
+  }
+}
+
+// The first span of [a_j, b_j) whose id is pid_j for each lane j of `pend`
+// (wave-uniform mask), the whole wave scanning 64 ids per step with a ballot:
+// the lookups the per-lane scans left after their first steps (a row would
+// otherwise wait for its slowest lane).  First match in trace order.
+__device__ __forceinline__ void coop_parent(const uint64_t* lsid, uint64_t pend, int lane,
+                                            uint64_t pid, uint32_t a, uint32_t b, int& q) {
+  while (pend) {
+    const int j = __ffsll((unsigned long long)pend) - 1;
+    const uint64_t pj = readlane64(pid, j);
+    const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)a, j);
+    const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)b, j);
+    int qj = -1;
+    for (uint32_t s0 = aj; s0 < bj; s0 += kWave) {
+      const uint32_t sp = s0 + (uint32_t)lane;
+      const uint64_t hit = __ballot(sp < bj && lsid[sp < bj ? sp : aj] == pj);
+      if (hit) {
+        qj = (int)(s0 + (uint32_t)__ffsll((unsigned long long)hit) - 1u);
+        break;
+      }
+    }
+    if (lane == j) q = qj;
+    pend &= pend - 1ull;
   }
 }
 

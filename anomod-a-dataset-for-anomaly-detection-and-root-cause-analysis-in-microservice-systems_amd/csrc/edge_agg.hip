@@ -443,11 +443,20 @@ __device__ __forceinline__ void load_regs(const Cols& col, const Chunk& c, int l
 #define ANOMOD_SCAN_IDS 10
 #endif
 constexpr uint32_t kScan = ANOMOD_SCAN_IDS;  // ids compared per step (kScan / 2 x ds_read2_b64)
+// Per-lane scan steps before a row's remaining lookups go to the whole wave
+// (coop_parent); 0 = every lane scans to the end.
+#ifndef ANOMOD_COOP_STEPS
+#define ANOMOD_COOP_STEPS 0
+#endif
+constexpr int kCoopSteps = ANOMOD_COOP_STEPS;
 static_assert(kScan % 2 == 0 && kScan <= 16, "scan step");
 
+template <int MAXS = 0>  // > 0: -2 after that many steps (completed cooperatively)
 __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uint32_t b,
                                            uint64_t pid) {
+  int steps = 0;
   for (uint32_t q0 = a; q0 < b; q0 += kScan) {
+    if (MAXS > 0 && steps++ >= MAXS) return -2;
     uint64_t v[kScan];
 #pragma unroll
     for (uint32_t j = 0; j < kScan; ++j) v[j] = lsid[q0 + j];
@@ -493,7 +502,21 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
     uint32_t p = S;  // ROOT
-    if (i < c.n && R.pid[r] != 0ull) {
+    if constexpr (kCoopSteps > 0 && !(ANOMOD_ABL & 4)) {
+      // kCoopSteps scan steps per lane, then the row's remaining lookups by
+      // the whole wave (coop_parent)
+      const bool has = i < c.n && R.pid[r] != 0ull;
+      uint32_t a, b;
+      trace_bounds(Sm, r, lane, c.n, a, b);
+      int q = -1;
+      if (has) {
+        q = UNI ? (WIDE ? find_parent_bidir<8, 8, kCoopSteps>(lsid, a, b, i, R.pid[r])
+                        : find_parent_bidir<kFwd, kBwd, kCoopSteps>(lsid, a, b, i, R.pid[r]))
+                : find_parent<kCoopSteps>(lsid, a, b, R.pid[r]);
+      }
+      coop_parent(lsid, __ballot(q == -2), lane, R.pid[r], a, b, q);
+      if (has) p = q >= 0 ? lsvc[q] : S + 1u;  // ORPHAN unless found in the trace
+    } else if (i < c.n && R.pid[r] != 0ull) {
       p = S + 1u;  // ORPHAN unless found in the trace
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
