@@ -258,9 +258,20 @@ constexpr uint32_t kSpinLimit = 1u << 22;
 #endif
 constexpr int kBarGroups = 8;  // 16 / 32 groups measured slower
 constexpr int kBarStride = 32;  // u32 words between counters (128 B)
+// ANOMOD_PPR_REPL copies of the top counter (0: one, bar[0]); block b polls copy
+// b mod ANOMOD_PPR_REPL
+#ifndef ANOMOD_PPR_REPL
+#define ANOMOD_PPR_REPL 8
+#endif
+#ifndef ANOMOD_PPR_SLEEP
+#define ANOMOD_PPR_SLEEP 1
+#endif
+constexpr int kBarCopies = ANOMOD_PPR_REPL;
+static_assert(kBarCopies >= 0 && kBarCopies <= 64, "top-counter copies");
 // bar[0] top counter, bar[1] timeout flag, bar[2] iterations done,
-// bar[kBarStride * (1 + g)] group counters
-constexpr int kBarWords = kBarStride * (1 + kBarGroups);
+// bar[kBarStride * (1 + g)] group counters, bar[kBarStride * (1 + kBarGroups + c)]
+// copy c of the top counter
+constexpr int kBarWords = kBarStride * (1 + kBarGroups + kBarCopies);
 
 __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int* s_flag,
                                              uint32_t spin_limit) {
@@ -316,13 +327,25 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
     const uint32_t gsize = (nb - g + ng - 1) / ng;  // blocks with index = g (mod ng)
     const uint32_t old = __hip_atomic_fetch_add(&bar[kBarStride * (1 + g)], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
+#if ANOMOD_PPR_REPL
+    // the group's last arriver bumps every copy of the top counter and each
+    // block polls one copy: a line takes ~1/kBarCopies of the polls (one
+    // polled line: 8.3 vs 7.9 us per iteration at N = 1e5)
+    if (old + 1u == gsize * (k + 1u))
+      for (uint32_t j = 0; j < (uint32_t)kBarCopies; ++j)
+        __hip_atomic_fetch_add(&bar[kBarStride * (1 + kBarGroups + j)], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int* const top = &bar[kBarStride * (1 + kBarGroups + blockIdx.x % kBarCopies)];
+#else
     if (old + 1u == gsize * (k + 1u))
       __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int* const top = &bar[0];
+#endif
     const uint32_t target = ng * (k + 1u);
     uint32_t spins = 0;
     int fail = 0;
-    while (__hip_atomic_load(&bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
+    while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (ANOMOD_PPR_SLEEP) __builtin_amdgcn_s_sleep(ANOMOD_PPR_SLEEP);
       if (++spins > spin_limit) {
         atomicOr(&bar[1], 1u);
         fail = 1;

@@ -668,11 +668,13 @@ def main() -> int:
         kb = 8
         Pb = np.random.default_rng(100 + rank).random((kb, g.N))
         g.pagerank_batch(Pb, iters=args.ppr_iters)
-        bt = []
+        bt, bw = [], []
         barrier()
         t0 = time.perf_counter()
         for _ in range(3):
+            t1 = time.perf_counter()
             g.pagerank_batch(Pb, iters=args.ppr_iters)
+            bw.append(round((time.perf_counter() - t1) * 1e3, 3))
             bt.append(ctx.stage_ms(L.STAGE_PAGERANK))
         bwall = allmax(time.perf_counter() - t0)
         b_ms = float(np.mean(bt))
@@ -682,6 +684,7 @@ def main() -> int:
             "vector_iters_per_s_per_gpu": kb * args.ppr_iters / (b_ms * 1e-3),
             "iters_per_s_per_gpu": args.ppr_iters / (b_ms * 1e-3),
             "us_per_batched_iter": b_ms * 1e3 / args.ppr_iters,
+            "wall_ms_per_batch": bw, "last_solve": list(g.last_solve()),
             "what": "solved vector-iterations/s (wall, all ranks) of 8-vector batches; per-GPU "
                     "device rates from the kernel time"}
         g.free()
