@@ -197,12 +197,14 @@ class Context:
         return v.value
 
     def group_info(self) -> dict:
-        """How the last grouping ran: path ("bucket" / "lsd"), scatter levels
-        or radix passes, and the key bits they sorted on."""
+        """How the last grouping ran: path ("bucket" / "join": the bucket
+        scatters then the ungrouped aggregation's per-bucket hash join / "lsd"),
+        scatter levels or radix passes, and the key bits they sorted on."""
         p, lv, b = C.c_int(), C.c_int(), C.c_int()
         self._check(self._lib.anomod_ctx_group_info(self.handle, C.byref(p), C.byref(lv),
                                                     C.byref(b)))
-        return {"path": "bucket" if p.value == 1 else "lsd", "levels": lv.value, "bits": b.value}
+        return {"path": {1: "bucket", 2: "join"}.get(p.value, "lsd"), "levels": lv.value,
+                "bits": b.value}
 
     # -- multi-GPU
     @staticmethod

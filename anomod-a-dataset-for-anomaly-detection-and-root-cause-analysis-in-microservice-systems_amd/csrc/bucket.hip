@@ -1339,6 +1339,148 @@ __global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_k
   }
 }
 
+// The fused ungrouped aggregation without the sort (the fused path's default;
+// ANOMOD_FUSED_JOIN=0: the sorting kernel below).  A bucket holds every span of
+// its traces, so a span's parent is found by an LDS hash join on (trace hash,
+// span id) over the bucket in arrival order: no ranking, no trace bounds.  The
+// table keeps the first arrival of a repeated (trace, id); arrival order inside
+// a trace is its input order (levels A and B are stable), so this is the
+// first-match rule (jaeger_to_csv.py:34-38 / trace_collector.py:424-443).
+// Records go out by arrival position (the edge table is order-free).
+constexpr int kJoinCap = kSmallW * kSmallPer;
+constexpr uint32_t kJoinSlots = 2u * kJoinCap;  // load factor <= 1/2
+static_assert((kJoinSlots & (kJoinSlots - 1u)) == 0u, "join table size");
+struct JoinLds {
+  uint64_t h[kJoinCap];
+  uint64_t sid[kJoinCap];
+  uint32_t tab[kJoinSlots];  // arrival position + 1; 0 = empty
+  uint16_t svc[kJoinCap];
+};
+
+__device__ __forceinline__ uint32_t join_slot(uint64_t h, uint64_t id) {
+  return (uint32_t)(mix64(h ^ (id * 0x9E3779B97F4A7C15ull)) >> 32) & (kJoinSlots - 1u);
+}
+
+__global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
+    const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
+    unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ JoinLds L;
+  constexpr int PER = kSmallPer;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const uint32_t c = blockIdx.x;
+  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
+  if (m > (uint32_t)kJoinCap) {  // the large (sorting) kernel's list
+    if (tid == 0) {
+      const unsigned long long i = atomicAdd(over_n, 1ull);
+      if (i < over_cap) over[i] = c;
+      else atomicAdd(too_big, 1ull);
+    }
+    return;
+  }
+  if (m == 0) return;
+  uint32_t p[PER];
+  bool v[PER];
+  uint32_t idx[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    v[j] = p[j] < m;
+    idx[j] = v[j] ? (uint32_t)pin[a0 + p[j]] : 0u;
+  }
+  uint4 ra[PER], rb[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
+    const uint4* q = reinterpret_cast<const uint4*>(rec + idx[j]);
+    ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+    rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t i = tid; i < kJoinSlots / 4u; i += kSmallW)
+    reinterpret_cast<uint4*>(L.tab)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (v[j]) {
+      L.h[p[j]] = ((uint64_t)ra[j].y << 32) | ra[j].x;
+      L.sid[p[j]] = ((uint64_t)ra[j].w << 32) | ra[j].z;
+      L.svc[p[j]] = (uint16_t)rb[j].z;
+    }
+  __syncthreads();
+  // inserts: every span's first CAS issued together; a taken slot (another
+  // key, or the same (trace, id) again) continues in the probe loop
+  uint32_t sl[PER], cur[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
+    const uint64_t id = ((uint64_t)ra[j].w << 32) | ra[j].z;
+    sl[j] = join_slot(hh, id);
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) cur[j] = v[j] ? atomicCAS(&L.tab[sl[j]], 0u, p[j] + 1u) : 0u;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (cur[j] == 0u) continue;
+    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
+    const uint64_t id = ((uint64_t)ra[j].w << 32) | ra[j].z;
+    uint32_t s = sl[j], c = cur[j];
+    while (true) {
+      const uint32_t q = c - 1u;
+      if (L.h[q] == hh && L.sid[q] == id) {  // a repeated (trace, id): keep the first
+        atomicMin(&L.tab[s], p[j] + 1u);
+        break;
+      }
+      s = (s + 1u) & (kJoinSlots - 1u);
+      c = L.tab[s];
+      if (c == 0u) {
+        c = atomicCAS(&L.tab[s], 0u, p[j] + 1u);
+        if (c == 0u) break;
+      }
+    }
+  }
+  __syncthreads();
+  // lookups: first probes, their candidates' keys, then the services, each
+  // round issued for every span together; a miss on an occupied slot probes on
+  uint32_t e[PER], prow[PER];
+  uint64_t pid[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
+    pid[j] = ((uint64_t)rb[j].y << 32) | rb[j].x;
+    sl[j] = join_slot(hh, pid[j]);
+    e[j] = v[j] && pid[j] != 0ull ? L.tab[sl[j]] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
+    prow[j] = pid[j] == 0ull ? eo.S : eo.S + 1u;  // ROOT / ORPHAN unless the trace holds it
+    if (e[j] == 0u) continue;
+    const uint32_t q = e[j] - 1u;
+    if (L.h[q] == hh && L.sid[q] == pid[j]) {
+      e[j] = q + 1u;  // found: its service below
+      continue;
+    }
+    uint32_t s = sl[j];
+    e[j] = 0u;
+    while (true) {
+      s = (s + 1u) & (kJoinSlots - 1u);
+      const uint32_t c = L.tab[s];
+      if (c == 0u) break;
+      if (L.h[c - 1u] == hh && L.sid[c - 1u] == pid[j]) {
+        e[j] = c;
+        break;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (!v[j]) continue;
+    if (e[j] != 0u) prow[j] = L.svc[e[j] - 1u];
+    const uint32_t svc = rb[j].z & 0xFFFFu, fl = rb[j].z >> 16;
+    eo.rec[a0 + p[j]] = ((uint64_t)(prow[j] * eo.S + svc) << 33) |
+                        ((uint64_t)((fl & ANOMOD_FLAG_ERROR) ? 1u : 0u) << 32) | rb[j].w;
+  }
+}
+
 // The fused ungrouped aggregation's bucket kernels: the same sort, then
 // edge records instead of grouped columns.
 __global__ __launch_bounds__(kSmallW) void bk_bucket_edge_kernel(
@@ -1628,7 +1770,11 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
                                                  (uint64_t)std::max(per_cu, 1));
   };
   if (eo) {  // the fused ungrouped aggregation: edge records, no columns, no trace_ptr
-    if (pipe)
+    if (env_int("ANOMOD_FUSED_JOIN", 1))
+      hipLaunchKernelGGL(bk_bucket_join_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
+                         recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                         ws->misc + kMiscTooBig);
+    else if (pipe)
       hipLaunchKernelGGL(bk_bucket_pipe_kernel<true>,
                          dim3(pipe_grid(reinterpret_cast<const void*>(bk_bucket_pipe_kernel<true>))),
                          dim3(kSmallW), 0, st, pin, recs, SoaOut{}, *eo, bstart, (uint32_t)nbk,

@@ -909,17 +909,18 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   }
   GroupResult g;
   if (rc == ANOMOD_OK) rc = bind(ctx);
-  // Fused path (bucket grouping only): the buckets write one 8-B edge record
-  // per span instead of the grouped columns, and the edge table is taken from
-  // those records — no grouped columns, no trace_ptr, no walk over them.
-  // Opt-in (ANOMOD_UNGROUPED_FUSED=1): measured slower than grouping then
-  // aggregating (71.0 + 2.1 vs 63.7 + 5.7 ms at 2^27 SN traces,
-  // gpurun_out/r4c_pipe_f*.log: the edge scan in LDS costs the bucket kernel
-  // more than the columns' write and re-read).  A set whose buckets hold
-  // traces of thousands of spans side by side takes the unfused path below.
+  // Fused path (bucket grouping only; the default, ANOMOD_UNGROUPED_FUSED=0
+  // turns it off): the buckets write one 8-B edge record per span instead of
+  // the grouped columns, and the edge table is taken from those records — no
+  // grouped columns, no trace_ptr, no walk over them.  Each bucket finds the
+  // parents by an LDS hash join (bk_bucket_join_kernel, no sort): 52.6 + 2.1
+  // vs 57.8 + 5.7 ms unfused at 2^27 SN traces (gpurun_out/r4u_ab.log; with
+  // the sorting bucket kernel's in-trace scan, ANOMOD_FUSED_JOIN=0, it was
+  // 71.0 + 2.1).  A set whose buckets hold traces of thousands of spans side
+  // by side takes the unfused path below.
   const char* fz = std::getenv("ANOMOD_UNGROUPED_FUSED");
   const uint64_t n = spans->n_spans;
-  if (rc == ANOMOD_OK && n > 0 && !force_lsd() && fz && fz[0] == '1' && n_services >= 1 &&
+  if (rc == ANOMOD_OK && n > 0 && !force_lsd() && !(fz && fz[0] == '0') && n_services >= 1 &&
       n_services <= 4096 && spans->max_svc < n_services && n <= 0xFFFFFFFFull - 4096) {
     rc = ensure_group_ws(ctx, n);
     bool fallback = true;
@@ -929,7 +930,7 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
       rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
       if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
       if (rc == ANOMOD_OK && !fallback) {
-        ctx->group_path = 1;
+        ctx->group_path = 2;
         ctx->group_levels = g.passes;
         ctx->group_bits = g.bits;
         return edge_aggregate_records(ctx, erec, n, n_services, &spans->hist_form, out);

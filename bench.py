@@ -334,6 +334,16 @@ def group_bytes(info: dict, n: int, n_traces: int) -> int:
         if two:
             b += 8 * n + 16 * n + 5 * 4 * (-(-n // 16384)) * (1 << db)
         return b + 72 * n + 24 * n_traces
+    if info["path"] == "join":
+        # the same scatters; the join kernel reads the pairs (8 B), gathers
+        # the records (32 B) and writes one 8-B edge record per span
+        T, two = info["bits"], info["levels"] == 2
+        da = min(11, T) if not two else max(T - 11, min((T + 1) // 2, 9))
+        db = T - da if two else 0
+        b = 8 * n + 72 * n + 5 * 4 * tiles * (1 << da)
+        if two:
+            b += 8 * n + 16 * n + 5 * 4 * (-(-n // 16384)) * (1 << db)
+        return b + 48 * n
     # csrc/group.hip (LSD): the first pass's tile counts read trace_hash, later
     # passes' the 1-B digits the previous pass wrote (written + read: 2 B);
     # each radix pass reads and writes 32 B (records, the last one the SoA
@@ -361,7 +371,9 @@ def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
     gbytes = group_bytes(info, n, n_traces)
     g_ms, e_ms = float(np.mean(g)), float(np.mean(e))
     return {"what": "SN spans of every 4096 consecutive traces interleaved (ES start_time "
-                    "order); step = device grouping + edge aggregation",
+                    "order); step = device grouping + edge aggregation (group_path join: "
+                    "bucket scatters + per-bucket parent hash join writing edge records, "
+                    "group_ms; the table from the records, edge_ms)",
             "spans": n, "traces": n_traces, "group_path": info,
             "spans_per_s": allsum(n / float(np.mean(wall))), "step_ms": float(np.mean(wall)) * 1e3,
             "group_ms": g_ms, "edge_ms": e_ms,

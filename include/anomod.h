@@ -181,8 +181,9 @@ int anomod_spans_grouped(const anomod_spans* spans, int* grouped);
 int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* ungrouped, anomod_spans** grouped);
 /* How the ctx's last grouping ran (csrc/group.hip, csrc/bucket.hip):
  * *path = 1 bucket path (two stable MSD scatters over the top *bits bits of
- * mix64(trace_hash), then one workgroup per bucket), 0 LSD path (8-bit radix
- * passes + bucket fix-up); *levels = scatter levels / radix passes run;
+ * mix64(trace_hash), then one workgroup per bucket), 2 the same scatters then
+ * the per-bucket hash join of anomod_edge_aggregate_ungrouped (edge records,
+ * no grouped columns), 0 LSD path (8-bit radix passes + bucket fix-up); *levels = scatter levels / radix passes run;
  * *bits = bucket bits (bucket path) or 8 * passes.  All 0 before any grouping. */
 int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits);
 /* Rearranged copies of a grouped set (synthetic arrival orders for tests
@@ -294,8 +295,13 @@ int anomod_metrics_free(anomod_metrics* m);
  * (RCCL all-reduce) before quantiles are taken.                            */
 int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
                                 anomod_edge_table* out);
-/* Edge table of an ungrouped set: group (anomod_spans_group, into a
- * workspace the ctx keeps) then aggregate; a grouped set is aggregated as is. */
+/* Edge table of an ungrouped set; a grouped set is aggregated as is.  By
+ * default the set is bucketed by trace (the grouping's two scatter levels) and
+ * each bucket finds its spans' parents by an LDS hash join on (trace, span id),
+ * writing one edge record per span that the table is taken from (no grouped
+ * columns).  A set whose buckets hold several traces of thousands of spans,
+ * or ANOMOD_UNGROUPED_FUSED=0, takes group (anomod_spans_group, into a
+ * workspace the ctx keeps) then aggregate.  Same table either way. */
 int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
                                     uint32_t n_services, anomod_edge_table* out);
 /* Exact per-edge order statistics (SURVEY.md §8a a11 cross-check mode): the

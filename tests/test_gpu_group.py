@@ -274,15 +274,19 @@ def test_group_pair_key_collisions(ctx, env_knob, avg):
     assert ctx.group_info()["levels"] == (2 if avg else 1)
 
 
+@pytest.mark.parametrize("join", ["1", "0"])
 @pytest.mark.parametrize("S,max_len,form", [(12, 24, None), (46, 60, None), (20, 40, None),
                                             (12, 24, "pair"), (100, 30, None)])
-def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, form):
-    """anomod_edge_aggregate_ungrouped's fused path (opt-in,
-    ANOMOD_UNGROUPED_FUSED=1: the buckets write one edge record per span, the
-    table is taken from those records) against the default unfused one
-    (grouped columns, then the chunk walk) and the oracle: SN / TrainTicket
+def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, form, join):
+    """anomod_edge_aggregate_ungrouped's fused path (the default: the buckets
+    write one edge record per span, the table is taken from those records)
+    against the unfused one (ANOMOD_UNGROUPED_FUSED=0: grouped columns, then
+    the chunk walk) and the oracle: SN / TrainTicket
     widths (direct, wide, slot stats), wide latencies (a compact-form run that
-    learns the set's form), duplicate ids, orphans, interleaved arrival."""
+    learns the set's form), duplicate ids, orphans, interleaved arrival.  join
+    "1": the buckets' LDS hash join on (trace, id) (the fused default); "0":
+    the sorting bucket kernel's in-trace scan."""
+    env_knob("ANOMOD_FUSED_JOIN", join)
     if form:
         env_knob("ANOMOD_HIST_FORM", form)
     rng = np.random.default_rng(S * 3 + max_len)
@@ -293,9 +297,9 @@ def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, 
     dev = ctx.upload_ungrouped(flat)
     monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "1")
     fused = ctx.edge_aggregate(dev)
-    assert ctx.group_info()["path"] == "bucket"
+    assert ctx.group_info()["path"] == "join"
     assert_table_equal(fused, ref)
-    monkeypatch.delenv("ANOMOD_UNGROUPED_FUSED")
+    monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "0")
     assert_table_equal(ctx.edge_aggregate(dev), ref)
     if form is None:  # learned from the compact run (wide latencies: far too many keys)
         assert dev.hints[1] in ((1,) if S == 20 else (0, 1))
