@@ -126,6 +126,8 @@ def main() -> int:
                          slice(None)),
                         ("fused ungrouped: buckets -> edge records", "bk_bucket_edge_kernel",
                          48 * nu, slice(None)),
+                        ("ungrouped: join buckets -> edge records (pairs, gathers, records)",
+                         "bk_bucket_join_kernel", 48 * nu, slice(None)),
                         ("fused ungrouped: edge records -> table", "edge_rec_kernel", 8 * nu,
                          slice(None))]
     kernels = {}
