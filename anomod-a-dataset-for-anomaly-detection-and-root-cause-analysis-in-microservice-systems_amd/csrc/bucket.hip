@@ -1347,8 +1347,13 @@ __global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_k
 // a trace is its input order (levels A and B are stable), so this is the
 // first-match rule (jaeger_to_csv.py:34-38 / trace_collector.py:424-443).
 // Records go out by arrival position (the edge table is order-free).
-constexpr int kJoinCap = kSmallW * kSmallPer;
-constexpr uint32_t kJoinSlots = 2u * kJoinCap;  // load factor <= 1/2
+#ifndef ANOMOD_JOIN_PER
+#define ANOMOD_JOIN_PER 4
+#endif
+constexpr int kJoinPer = ANOMOD_JOIN_PER;  // spans per lane of the join kernel
+constexpr int kJoinCap = kSmallW * kJoinPer;
+// load factor <= 1/2 (PER 3: <= 3/4, ~0.54 at the SN mean of ~1 100 spans)
+constexpr uint32_t kJoinSlots = kJoinPer == 3 ? 2048u : 2u * kJoinCap;
 static_assert((kJoinSlots & (kJoinSlots - 1u)) == 0u, "join table size");
 struct JoinLds {
   uint64_t h[kJoinCap];
@@ -1367,7 +1372,7 @@ __global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
     unsigned long long* __restrict__ over_n, uint32_t over_cap,
     unsigned long long* __restrict__ too_big) {
   __shared__ JoinLds L;
-  constexpr int PER = kSmallPer;
+  constexpr int PER = kJoinPer;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
   const uint32_t c = blockIdx.x;
   const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
