@@ -109,11 +109,24 @@ def main():
                 tot += max(fn(i, nf, nb) for i in range(r0, min(r0 + 64, b)))
         return tot / len(chunks)
 
+    def cost_queue(nf, nb):
+        """each lane works through its own spans of the chunk (positions l,
+        l + 64, ...) one lookup after another; the wave steps until every
+        lane's queue is empty: max over lanes of the lane's summed steps"""
+        tot = 0
+        for t0, t1 in chunks:
+            a, b = ptr[t0], ptr[t1]
+            tot += max(sum(steps(i, nf, nb) for i in range(a + l, b, 64)) for l in range(64))
+        return tot / len(chunks)
+
     print(f"{topo}: {n / nt:.2f} spans/trace, {len(chunks)} chunks")
     import os
     splits = [tuple(int(x) for x in t.split("+")) for t in os.environ.get("SPLITS", "10+0 6+4").split()]
     for nf, nb in splits:
         print(f"  {'fwd' if nb == 0 else 'bidir'} {nf}+{nb}: {cost(nf, nb):.2f} row-steps/chunk")
+    if os.environ.get("QUEUE"):
+        for nf, nb in splits:
+            print(f"  per-lane queue {nf}+{nb}: {cost_queue(nf, nb):.2f} row-steps/chunk")
     if os.environ.get("SIM_ALL"):
         for nf, nb in ((6, 4), (8, 2)):
             print(f"  bidir-meet {nf}+{nb}: {cost(nf, nb, steps_meet):.2f} row-steps/chunk")
