@@ -321,3 +321,44 @@ def test_ungrouped_fused_long_traces_fall_back(ctx, monkeypatch):
     dev = ctx.upload_ungrouped(flat)
     monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "1")
     assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(_oracle_grouped(flat)))
+
+
+def test_ungrouped_join_shared_ids_and_big_buckets(ctx):
+    """The join path's edge cases, against the oracle on the stably grouped
+    spans: forty traces in ONE bucket (mixed keys sharing their top 40 bits)
+    whose span ids and parent ids are identical — the (trace, id) join must
+    tell them apart by the trace hash, and each trace's duplicate ids resolve
+    to its own first match — and three 900-span traces in one bucket (2 700
+    spans: over the join kernel's 2 048, so the sorting large kernel's edge
+    form takes it), beside ordinary random traces."""
+    rng = np.random.default_rng(77)
+    S = 12
+
+    def same_ids(k, L):
+        sid = rng.integers(1, 2**63, L, dtype=np.uint64)
+        sid[5] = sid[2]  # a repeated id inside the trace: the first match wins
+        pid = np.zeros(L, np.uint64)
+        pid[1:] = sid[(rng.random(L - 1) * np.arange(1, L)).astype(np.int64)]
+        pid[7] = np.uint64(12345)  # an orphan reference
+        ptr = np.arange(k + 1, dtype=np.uint64) * np.uint64(L)
+        n = k * L
+        return anomod.SpanSet([f"svc{i:03d}" for i in range(S)], ptr, np.zeros(n, np.uint64),
+                              np.tile(sid, k), np.tile(pid, k),
+                              rng.integers(0, S, n).astype(np.uint16),
+                              (rng.random(n) < 0.1).astype(np.uint16),
+                              rng.integers(50, 5000, n).astype(np.uint32))
+
+    def one_bucket(sp):
+        base = rng.integers(0, 2**64, 1, dtype=np.uint64)[0] & np.uint64(0xFFFFFFFFFF000000)
+        low = rng.choice(2**24, sp.n_traces, replace=False).astype(np.uint64)
+        return _with_trace_hashes(sp, rng, _unmix64((base | low).astype(np.uint64)))
+
+    shared = one_bucket(same_ids(40, 20))
+    big = one_bucket(_random_spanset(rng, S, 0, 0, dup=0.02, lens=[900, 900, 900]))
+    rest = _with_trace_hashes(_random_spanset(rng, S, 20000, 16, dup=0.02), rng)
+    flat = _interleave(anomod.SpanSet.concat([rest, shared, big]), rng, "random")
+    dev = ctx.upload_ungrouped(flat)
+    got = ctx.edge_aggregate(dev)
+    assert ctx.group_info()["path"] == "join"
+    assert_table_equal(got, native.edge_aggregate(_oracle_grouped(flat)))
+    dev.free()
