@@ -261,6 +261,27 @@ def stage_tt_files(root: str) -> list:
         return pool.map(_stage_tt_experiment, work)
 
 
+def _evict_page_cache(paths) -> int:
+    """Drop the page-cache pages of these files (fsync, then
+    posix_fadvise(DONTNEED); best effort: a tmpfs keeps them).  Returns the
+    files handled."""
+    done = 0
+    for p in paths:
+        try:
+            fd = os.open(p, os.O_RDONLY)
+        except OSError:
+            continue
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            done += 1
+        except OSError:
+            pass
+        finally:
+            os.close(fd)
+    return done
+
+
 def tt_config2_files(ctx, staged: list) -> dict:
     """BASELINE config 2 from files: each experiment's trace payload and long
     metric CSV go through load_experiment (native decoders) -> features() ->
@@ -286,6 +307,17 @@ def tt_config2_files(ctx, staged: list) -> dict:
         spans += e.spans.n_spans
         samples += e.metrics.S * e.metrics.T
     el = time.perf_counter() - t0
+    # the same experiments again, each experiment's files dropped from the page
+    # cache first (a collector's fresh files would be in it; a dataset read
+    # back later would not)
+    cold_dec, cold_tot, evicted = 0.0, 0.0, 0
+    for d, mc, fault in staged:
+        evicted += _evict_page_cache([str(x) for x in Path(d).rglob("*") if x.is_file()] + [mc])
+        a = time.perf_counter()
+        e = one(d, mc)
+        cold_dec += time.perf_counter() - a
+        anomod.features(e, ctx, baseline=base)
+        cold_tot += time.perf_counter() - a
     sizes = [next(Path(d).glob("*.json")).stat().st_size for d, _, _ in staged]
     csv_sizes = [Path(mc).stat().st_size for _, mc, _ in staged]
     return {"experiments": len(staged), "spans": spans, "samples": samples, "seconds": el,
@@ -293,6 +325,12 @@ def tt_config2_files(ctx, staged: list) -> dict:
             "trace_json_mb_mean": float(np.mean(sizes)) / 1e6,
             "metric_csv_mb_mean": float(np.mean(csv_sizes)) / 1e6,
             "top3_hit_rate": float(np.mean(hits)),
+            "cold_files": {"ms_per_experiment": cold_tot / len(staged) * 1e3,
+                           "decode_ms_per_experiment": cold_dec / len(staged) * 1e3,
+                           "files_evicted": evicted,
+                           "what": "load_experiment + features per experiment after "
+                                   "fsync + posix_fadvise(DONTNEED) on its files (best effort: "
+                                   "no effect on a tmpfs)"},
             "note": "files in the dataset layout (collector payload JSON indent=2 + long metric "
                     "CSV) -> load_experiment (native decoders) -> features -> rank"}
 
