@@ -1366,41 +1366,16 @@ __device__ __forceinline__ uint32_t join_slot(uint64_t h, uint64_t id) {
   return (uint32_t)(mix64(h ^ (id * 0x9E3779B97F4A7C15ull)) >> 32) & (kJoinSlots - 1u);
 }
 
-__global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
-    const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
-    const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
-    unsigned long long* __restrict__ over_n, uint32_t over_cap,
-    unsigned long long* __restrict__ too_big) {
-  __shared__ JoinLds L;
+// One bucket's join (its records already gathered into ra / rb): stage, insert,
+// look up, write the edge records.  Every thread of the workgroup calls it.
+__device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool (&v)[kJoinPer],
+                                            const uint4 (&ra)[kJoinPer],
+                                            const uint4 (&rb)[kJoinPer], EdgeOut eo) {
   constexpr int PER = kJoinPer;
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  const uint32_t c = blockIdx.x;
-  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
-  if (m > (uint32_t)kJoinCap) {  // the large (sorting) kernel's list
-    if (tid == 0) {
-      const unsigned long long i = atomicAdd(over_n, 1ull);
-      if (i < over_cap) over[i] = c;
-      else atomicAdd(too_big, 1ull);
-    }
-    return;
-  }
-  if (m == 0) return;
   uint32_t p[PER];
-  bool v[PER];
-  uint32_t idx[PER];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-    v[j] = p[j] < m;
-    idx[j] = v[j] ? (uint32_t)pin[a0 + p[j]] : 0u;
-  }
-  uint4 ra[PER], rb[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
-    const uint4* q = reinterpret_cast<const uint4*>(rec + idx[j]);
-    ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
-    rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
-  }
+  for (int j = 0; j < PER; ++j) p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
   for (uint32_t i = tid; i < kJoinSlots / 4u; i += kSmallW)
     reinterpret_cast<uint4*>(L.tab)[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -1484,6 +1459,44 @@ __global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
     eo.rec[a0 + p[j]] = ((uint64_t)(prow[j] * eo.S + svc) << 33) |
                         ((uint64_t)((fl & ANOMOD_FLAG_ERROR) ? 1u : 0u) << 32) | rb[j].w;
   }
+}
+
+__global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
+    const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
+    unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  __shared__ JoinLds L;
+  constexpr int PER = kJoinPer;
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const uint32_t c = blockIdx.x;
+  const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
+  if (m > (uint32_t)kJoinCap) {  // the large (sorting) kernel's list
+    if (tid == 0) {
+      const unsigned long long i = atomicAdd(over_n, 1ull);
+      if (i < over_cap) over[i] = c;
+      else atomicAdd(too_big, 1ull);
+    }
+    return;
+  }
+  if (m == 0) return;
+  uint32_t p[PER];
+  bool v[PER];
+  uint32_t idx[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    v[j] = p[j] < m;
+    idx[j] = v[j] ? (uint32_t)pin[a0 + p[j]] : 0u;
+  }
+  uint4 ra[PER], rb[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
+    const uint4* q = reinterpret_cast<const uint4*>(rec + idx[j]);
+    ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+    rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+  }
+  join_bucket(L, a0, v, ra, rb, eo);
 }
 
 // The fused ungrouped aggregation's bucket kernels: the same sort, then
