@@ -1351,7 +1351,11 @@ __global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_k
 #define ANOMOD_JOIN_PER 4
 #endif
 constexpr int kJoinPer = ANOMOD_JOIN_PER;  // spans per lane of the join kernel
-constexpr int kJoinCap = kSmallW * kJoinPer;
+#ifndef ANOMOD_JOIN_W
+#define ANOMOD_JOIN_W 512
+#endif
+constexpr int kJoinW = ANOMOD_JOIN_W;  // threads of a join workgroup
+constexpr int kJoinCap = kJoinW * kJoinPer;
 // load factor <= 1/2 (PER 3: <= 3/4, ~0.54 at the SN mean of ~1 100 spans)
 constexpr uint32_t kJoinSlots = kJoinPer == 3 ? 2048u : 2u * kJoinCap;
 static_assert((kJoinSlots & (kJoinSlots - 1u)) == 0u, "join table size");
@@ -1376,7 +1380,7 @@ __device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool 
   uint32_t p[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-  for (uint32_t i = tid; i < kJoinSlots / 4u; i += kSmallW)
+  for (uint32_t i = tid; i < kJoinSlots / 4u; i += kJoinW)
     reinterpret_cast<uint4*>(L.tab)[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (int j = 0; j < PER; ++j)
@@ -1461,7 +1465,7 @@ __device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool 
   }
 }
 
-__global__ __launch_bounds__(kSmallW) void bk_bucket_join_kernel(
+__global__ __launch_bounds__(kJoinW) void bk_bucket_join_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
     unsigned long long* __restrict__ over_n, uint32_t over_cap,
@@ -1789,7 +1793,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   };
   if (eo) {  // the fused ungrouped aggregation: edge records, no columns, no trace_ptr
     if (env_int("ANOMOD_FUSED_JOIN", 1))
-      hipLaunchKernelGGL(bk_bucket_join_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
+      hipLaunchKernelGGL(bk_bucket_join_kernel, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
                          recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                          ws->misc + kMiscTooBig);
     else if (pipe)
