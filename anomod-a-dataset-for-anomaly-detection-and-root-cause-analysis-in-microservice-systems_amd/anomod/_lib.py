@@ -171,6 +171,8 @@ _SIGS = {
     "anomod_synth_generate_host": (_i32, [_P(SynthSpec), _u64, _u64, _P(SpanSoA), _P(_u64)]),
     "anomod_spans_generate": (_i32, [_vp, _P(SynthSpec), _u64, _u64, _P(_vp)]),
     "anomod_edge_aggregate_spans": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
+    "anomod_edge_aggregate_host": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _u32, _i32,
+                                          _P(_i32), _P(_i32), _P(EdgeTableC)]),
     "anomod_edge_aggregate": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(EdgeTableC)]),
     "anomod_trace_structure_spans": (_i32, [_vp, _vp, _P(TraceStructC)]),
     "anomod_trace_structure": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(TraceStructC)]),

@@ -198,12 +198,14 @@ class Context:
 
     def group_info(self) -> dict:
         """How the last grouping ran: path ("bucket" / "join": the bucket
-        scatters then the ungrouped aggregation's per-bucket hash join / "lsd"),
+        scatters then the ungrouped aggregation's per-bucket hash join /
+        "fused-sort": the same scatters then the sorting bucket kernels' edge
+        records (ANOMOD_FUSED_JOIN=0) / "lsd"),
         scatter levels or radix passes, and the key bits they sorted on."""
         p, lv, b = C.c_int(), C.c_int(), C.c_int()
         self._check(self._lib.anomod_ctx_group_info(self.handle, C.byref(p), C.byref(lv),
                                                     C.byref(b)))
-        return {"path": {1: "bucket", 2: "join"}.get(p.value, "lsd"), "levels": lv.value,
+        return {"path": {1: "bucket", 2: "join", 3: "fused-sort"}.get(p.value, "lsd"), "levels": lv.value,
                 "bits": b.value}
 
     # -- multi-GPU
@@ -314,12 +316,24 @@ class Context:
         return DeviceSpans(self, h, spec.services())
 
     def edge_aggregate(self, spans: DeviceSpans | SpanSet, with_hist: bool = True) -> EdgeTable:
-        """Edge table of a span set (uploading it first if it is on the host;
-        the hints learned on the device go back onto the host set)."""
-        tmp = host = None
+        """Edge table of a span set.  A host set goes through
+        anomod_edge_aggregate_host (pinned staging pipeline into a device set
+        the context keeps; the hints learned on the device go back onto the
+        host set)."""
         if isinstance(spans, SpanSet):
-            host = spans
-            tmp = spans = self.upload(spans)
+            table = EdgeTable.empty(spans.services, with_hist)
+            cs = table.c_struct()
+            soa = spans.soa()
+            order, form = C.c_int(spans.scan_order), C.c_int(spans.hist_form)
+            self._check(self._lib.anomod_edge_aggregate_host(
+                self.handle, C.byref(soa), spans.n_spans, L.ptr(spans.trace_ptr, C.c_uint64),
+                spans.n_traces, len(spans.services), 1 if spans.unique_ids else 0,
+                C.byref(order), C.byref(form), C.byref(cs)))
+            if table.hist is not None:
+                table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
+            spans.scan_order, spans.hist_form = order.value, form.value
+            return table
+        tmp = host = None
         try:
             table = EdgeTable.empty(spans.services, with_hist)
             cs = table.c_struct()

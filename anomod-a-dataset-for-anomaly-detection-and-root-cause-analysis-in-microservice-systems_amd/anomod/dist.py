@@ -91,6 +91,16 @@ def _reduce(parts: list[np.ndarray], op: int) -> np.ndarray:
     raise ValueError(f"unknown reduction op {op}")
 
 
+def _link_options(sock: socket.socket, timeout_s: float) -> None:
+    """A formed peer link: every recv bounded by timeout_s, TCP keepalive on
+    (probes after 30 s idle, every 10 s, 6 unanswered = dead link)."""
+    sock.settimeout(timeout_s)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE, 1)
+    for name, v in (("TCP_KEEPIDLE", 30), ("TCP_KEEPINTVL", 10), ("TCP_KEEPCNT", 6)):
+        if hasattr(socket, name):
+            sock.setsockopt(socket.IPPROTO_TCP, getattr(socket, name), v)
+
+
 class HostGroup:
     """A star-shaped TCP process group over the ranks of one node.
 
@@ -104,17 +114,23 @@ class HostGroup:
                  coll_timeout_s: float | None = None):
         """timeout_s bounds the rendezvous (ANOMOD_RCCL_TIMEOUT_S, 300 s);
         once the group is formed a collective waits coll_timeout_s for a peer
-        (ANOMOD_HOSTGROUP_TIMEOUT_S; default: as long as it takes — a barrier
-        behind a slow rank must not fail, and a rank that dies closes its
-        socket, which every peer sees at once)."""
+        (ANOMOD_HOSTGROUP_TIMEOUT_S; default 10 x timeout_s, so a barrier
+        behind a slow rank still passes) and then raises TimeoutError.  A rank
+        that exits closes its socket, which every peer sees at once; a rank
+        stuck in a GPU call or a lost host sends nothing, which the timeout
+        and TCP keepalive on every peer link turn into an error instead of a
+        wait without end."""
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"bad rank {rank} of world {world}")
         self.rank, self.world = rank, world
         self.timeout_s = float(timeout_s if timeout_s is not None
                                else os.environ.get("ANOMOD_RCCL_TIMEOUT_S", "300"))
-        if coll_timeout_s is None and os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S"):
-            coll_timeout_s = float(os.environ["ANOMOD_HOSTGROUP_TIMEOUT_S"])
-        self.coll_timeout_s = coll_timeout_s
+        if coll_timeout_s is None:
+            env = os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S")
+            coll_timeout_s = float(env) if env else 10.0 * self.timeout_s
+        if not coll_timeout_s > 0:
+            raise ValueError(f"collective timeout must be > 0 s, got {coll_timeout_s}")
+        self.coll_timeout_s = float(coll_timeout_s)
         self._peers: list[socket.socket] = []  # rank 0: ranks 1..world-1 in order
         self._sock: socket.socket | None = None  # other ranks: the link to rank 0
         self._file: Path | None = None
@@ -166,7 +182,7 @@ class HostGroup:
                 srv.close()
             self._peers = [peers[r] for r in range(1, world)]
             for c in self._peers:
-                c.settimeout(self.coll_timeout_s)
+                _link_options(c, self.coll_timeout_s)
                 _send(c, b"ok")
         else:
             while True:
@@ -178,7 +194,7 @@ class HostGroup:
                     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     _send(s, _MAGIC + struct.pack("<ii", rank, world))
                     if _recv(s) == b"ok":
-                        s.settimeout(self.coll_timeout_s)
+                        _link_options(s, self.coll_timeout_s)
                         self._sock, s = s, None
                         break
                 except (OSError, ValueError, KeyError, ConnectionError, struct.error):
@@ -202,13 +218,18 @@ class HostGroup:
         to every rank."""
         if self.world == 1:
             return combine([payload])
-        if self.rank == 0:
-            out = combine([payload] + [_recv(c) for c in self._peers])
-            for c in self._peers:
-                _send(c, out)
-            return out
-        _send(self._sock, payload)
-        return _recv(self._sock)
+        try:
+            if self.rank == 0:
+                out = combine([payload] + [_recv(c) for c in self._peers])
+                for c in self._peers:
+                    _send(c, out)
+                return out
+            _send(self._sock, payload)
+            return _recv(self._sock)
+        except socket.timeout:
+            raise TimeoutError(f"anomod host group: rank {self.rank} of {self.world} waited "
+                               f"{self.coll_timeout_s:.0f} s for a peer in a collective "
+                               f"(ANOMOD_HOSTGROUP_TIMEOUT_S)") from None
 
     def broadcast(self, data: bytes | None, src: int = 0) -> bytes:
         """src's bytes on every rank."""

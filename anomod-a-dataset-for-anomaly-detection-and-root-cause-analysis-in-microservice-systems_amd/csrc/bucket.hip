@@ -561,6 +561,72 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_b_kernel(
   }
 }
 
+// ---- level B for the join: the same scatter, ranks from LDS atomics -----------
+// The ungrouped aggregation's join resolves a repeated (trace, id) by the
+// pairs' level-A positions (arrival order: level A is stable), not by the
+// order inside a bucket, so level B need not be stable there.  A pair's rank
+// inside its digit is one returning LDS add instead of db wave ballots per
+// row; the digit totals are the counters themselves (one scan, no per-wave
+// counter matrix).  Same tile map, counts and output bucket starts as the
+// stable kernel.
+__global__ __launch_bounds__(kBThreads) void bk_scatter_b_fast_kernel(
+    const uint64_t* __restrict__ pin, uint64_t* __restrict__ pout, int db,
+    const uint32_t* __restrict__ toff, const uint32_t* __restrict__ bsA,
+    const uint32_t* __restrict__ btile, const uint32_t* __restrict__ tmap, int na, uint32_t nx) {
+  __shared__ uint64_t stage[kPTile];      // 128 KiB: the tile's pairs in digit order
+  __shared__ uint32_t lcnt[kNDMax];       // digit counts, then the tile's digit starts
+  __shared__ uint32_t delta[kNDMax];      // global start - tile start, per digit
+  __shared__ uint32_t wsum[kBWaves];
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const int nd = 1 << db, shift = 64 - db;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x, nx);
+  uint64_t base, nvalid;
+  if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
+  uint64_t x[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane);
+    x[k] = loc < nvalid ? pin[base + loc] : 0ull;
+  }
+  for (int dd = tid; dd < nd; dd += kBThreads) lcnt[dd] = 0u;
+  __syncthreads();
+  uint32_t off[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane);
+    off[k] = loc < nvalid ? atomicAdd(&lcnt[(uint32_t)(x[k] >> shift)], 1u) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const int dpt = nd > kBThreads ? nd / kBThreads : 1;
+  uint32_t c[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd < nd) c[i] = lcnt[dd];
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kBWaves>(c[0] + c[1], wsum, &all);
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd >= nd) continue;
+    const uint32_t ts = pre + (i ? c[0] : 0u);
+    lcnt[dd] = ts;
+    delta[dd] = toff[tile * nd + dd] - ts;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k)
+    if (off[k] != 0xFFFFFFFFu) stage[lcnt[(uint32_t)(x[k] >> shift)] + off[k]] = x[k];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPPer; ++j) {
+    const uint32_t cc = (uint32_t)(tid + j * kBThreads);
+    if (cc < nvalid) {
+      const uint64_t y = stage[cc];
+      pout[(uint64_t)(uint32_t)(delta[(uint32_t)(y >> shift)] + cc)] = y;
+    }
+  }
+}
+
 // ---- one bucket in (k, arrival) order ---------------------------------------
 template <int W, int PER, bool EDGE = false>
 struct BucketLds {
@@ -1340,85 +1406,130 @@ __global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_k
 }
 
 // The fused ungrouped aggregation without the sort (the fused path's default;
-// ANOMOD_FUSED_JOIN=0: the sorting kernel below).  A bucket holds every span of
-// its traces, so a span's parent is found by an LDS hash join on (trace hash,
-// span id) over the bucket in arrival order: no ranking, no trace bounds.  The
-// table keeps the first arrival of a repeated (trace, id); arrival order inside
-// a trace is its input order (levels A and B are stable), so this is the
-// first-match rule (jaeger_to_csv.py:34-38 / trace_collector.py:424-443).
-// Records go out by arrival position (the edge table is order-free).
-#ifndef ANOMOD_JOIN_PER
-#define ANOMOD_JOIN_PER 4
-#endif
-constexpr int kJoinPer = ANOMOD_JOIN_PER;  // spans per lane of the join kernel
-#ifndef ANOMOD_JOIN_W
-#define ANOMOD_JOIN_W 512
-#endif
-constexpr int kJoinW = ANOMOD_JOIN_W;  // threads of a join workgroup
-constexpr int kJoinCap = kJoinW * kJoinPer;
-// load factor <= 1/2 (PER 3: <= 3/4, ~0.54 at the SN mean of ~1 100 spans)
-constexpr uint32_t kJoinSlots = kJoinPer == 3 ? 2048u : 2u * kJoinCap;
-static_assert((kJoinSlots & (kJoinSlots - 1u)) == 0u, "join table size");
-struct JoinLds {
-  uint64_t h[kJoinCap];
-  uint64_t sid[kJoinCap];
-  uint32_t tab[kJoinSlots];  // arrival position + 1; 0 = empty
-  uint16_t svc[kJoinCap];
+// ANOMOD_FUSED_JOIN=0: the sorting kernels below).  A bucket holds every span
+// of its traces, so a span's parent is found by an LDS hash join on (trace,
+// span id) over the bucket: no ranking, no trace bounds.  A repeated (trace,
+// id) resolves to its earliest arrival — the smallest level-A position, since
+// level A is stable (level B is not: bk_scatter_b_fast_kernel), read from the
+// bucket's pairs — which is the first-match rule (jaeger_to_csv.py:34-38 /
+// trace_collector.py:424-443).  Records go out by bucket position (the edge
+// table is order-free).
+//
+// LDS per span: the trace key, the span id and half a u16 table slot (load
+// <= 1/2).  PACK (T >= 12 bucket bits: every k of a bucket shares its top 12
+// bits, and a service index is < 4096) keeps the service in those 12 bits of
+// the key word: 20 B per span, so the 2 048-span kernel takes 40 KiB and four
+// workgroups share a CU (the r04 form, 26 B per span, fit three).
+constexpr uint64_t kKeyLow = (1ull << 52) - 1ull;  // the k bits a PACK key word compares
+
+template <int W, int PER, bool PACK>
+struct JoinGeom {
+  static constexpr int kCap = W * PER;
+  static constexpr uint32_t kSlots = 2u * (uint32_t)kCap;  // u16 slots, two per word
+  static constexpr size_t kOffSid = 8ull * kCap, kOffTab = 16ull * kCap, kOffSvc = 20ull * kCap;
+  static constexpr size_t kBytes = PACK ? 20ull * kCap : 22ull * kCap;
+  static_assert((kSlots & (kSlots - 1u)) == 0u, "join table size");
+  static_assert(kCap <= 65535, "u16 slots hold arrival + 1");
 };
 
-__device__ __forceinline__ uint32_t join_slot(uint64_t h, uint64_t id) {
-  return (uint32_t)(mix64(h ^ (id * 0x9E3779B97F4A7C15ull)) >> 32) & (kJoinSlots - 1u);
+__device__ __forceinline__ uint32_t join_slot(uint64_t k, uint64_t id, uint32_t slots) {
+  return (uint32_t)(mix64(k ^ (id * 0x9E3779B97F4A7C15ull)) >> 32) & (slots - 1u);
 }
 
-// One bucket's join (its records already gathered into ra / rb): stage, insert,
-// look up, write the edge records.  Every thread of the workgroup calls it.
-__device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool (&v)[kJoinPer],
-                                            const uint4 (&ra)[kJoinPer],
-                                            const uint4 (&rb)[kJoinPer], EdgeOut eo) {
-  constexpr int PER = kJoinPer;
+__device__ __forceinline__ uint32_t slot_get(const uint32_t* tab, uint32_t s) {
+  return (tab[s >> 1] >> ((s & 1u) * 16u)) & 0xFFFFu;
+}
+
+// Compare-and-swap of u16 slot s (a 32-bit CAS on its word, retried while only
+// the other half changes): the slot's value before, == expect when swapped.
+__device__ __forceinline__ uint32_t slot_cas(uint32_t* tab, uint32_t s, uint32_t expect,
+                                             uint32_t desired) {
+  uint32_t* wp = &tab[s >> 1];
+  const uint32_t sh = (s & 1u) * 16u, mask = 0xFFFFu << sh;
+  uint32_t w = (expect << sh) | (*wp & ~mask);
+  while (true) {
+    const uint32_t old = atomicCAS(wp, w, (w & ~mask) | (desired << sh));
+    if (old == w) return expect;
+    const uint32_t cur = (old >> sh) & 0xFFFFu;
+    if (cur != expect) return cur;
+    w = old;
+  }
+}
+
+// One bucket [a0, a0 + m) of the level-B pairs `pin` joined in LDS; every
+// thread of the workgroup calls it.  The records come from `rec` by the pairs'
+// level-A positions.
+template <int W, int PER, bool PACK>
+__device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uint32_t m,
+                                            const uint64_t* __restrict__ pin,
+                                            const GRec* __restrict__ rec, EdgeOut eo) {
+  using G = JoinGeom<W, PER, PACK>;
+  constexpr uint32_t kSlots = G::kSlots;
+  uint64_t* lkx = reinterpret_cast<uint64_t*>(lds);
+  uint64_t* lsid = reinterpret_cast<uint64_t*>(lds + G::kOffSid);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + G::kOffTab);
+  uint16_t* lsvc = reinterpret_cast<uint16_t*>(lds + G::kOffSvc);  // !PACK only
   const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
-  uint32_t p[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-  for (uint32_t i = tid; i < kJoinSlots / 4u; i += kJoinW)
-    reinterpret_cast<uint4*>(L.tab)[i] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int j = 0; j < PER; ++j)
-    if (v[j]) {
-      L.h[p[j]] = ((uint64_t)ra[j].y << 32) | ra[j].x;
-      L.sid[p[j]] = ((uint64_t)ra[j].w << 32) | ra[j].z;
-      L.svc[p[j]] = (uint16_t)rb[j].z;
-    }
-  __syncthreads();
-  // inserts: every span's first CAS issued together; a taken slot (another
-  // key, or the same (trace, id) again) continues in the probe loop
-  uint32_t sl[PER], cur[PER];
+  uint32_t p[PER], ap[PER];
+  bool v[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
-    const uint64_t id = ((uint64_t)ra[j].w << 32) | ra[j].z;
-    sl[j] = join_slot(hh, id);
+    p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
+    v[j] = p[j] < m;
+    ap[j] = v[j] ? (uint32_t)pin[a0 + p[j]] : 0u;  // level-A position
   }
+  uint4 ra[PER], rb[PER];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) cur[j] = v[j] ? atomicCAS(&L.tab[sl[j]], 0u, p[j] + 1u) : 0u;
+  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
+    const uint4* q = reinterpret_cast<const uint4*>(rec + ap[j]);
+    ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
+    rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t i = tid; i < kSlots / 8u; i += W)
+    reinterpret_cast<uint4*>(tab)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t k = mix64(((uint64_t)ra[j].y << 32) | ra[j].x);
+    if (v[j]) {
+      lkx[p[j]] = PACK ? (((uint64_t)(rb[j].z & 0xFFFu) << 52) | (k & kKeyLow)) : k;
+      lsid[p[j]] = ((uint64_t)ra[j].w << 32) | ra[j].z;
+      if constexpr (!PACK) lsvc[p[j]] = (uint16_t)rb[j].z;
+    }
+  }
+  __syncthreads();
+  auto same_trace = [](uint64_t a, uint64_t b) {
+    return PACK ? ((a ^ b) & kKeyLow) == 0ull : a == b;
+  };
+  // inserts: every span's first CAS issued together; a taken slot (another
+  // key, or the same (trace, id) again) continues in the probe loop
+  // (keys and span ids are read back from LDS: the records' first halves are
+  // dead after the staging, which keeps the kernel at four workgroups per CU)
+  uint32_t sl[PER], cur[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    sl[j] = v[j] ? join_slot(lkx[p[j]] & (PACK ? kKeyLow : ~0ull), lsid[p[j]], kSlots) : 0u;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) cur[j] = v[j] ? slot_cas(tab, sl[j], 0u, p[j] + 1u) : 0u;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     if (cur[j] == 0u) continue;
-    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
-    const uint64_t id = ((uint64_t)ra[j].w << 32) | ra[j].z;
+    const uint64_t id = lsid[p[j]], kj = lkx[p[j]];
     uint32_t s = sl[j], c = cur[j];
     while (true) {
-      const uint32_t q = c - 1u;
-      if (L.h[q] == hh && L.sid[q] == id) {  // a repeated (trace, id): keep the first
-        atomicMin(&L.tab[s], p[j] + 1u);
+      uint32_t q = c - 1u;
+      if (same_trace(lkx[q], kj) && lsid[q] == id) {
+        // a repeated (trace, id): the smallest level-A position keeps the slot
+        const uint32_t mine = (uint32_t)pin[a0 + p[j]];
+        while ((uint32_t)pin[a0 + q] > mine) {
+          const uint32_t old = slot_cas(tab, s, q + 1u, p[j] + 1u);
+          if (old == q + 1u) break;
+          q = old - 1u;  // another copy took it first: compare with that one
+        }
         break;
       }
-      s = (s + 1u) & (kJoinSlots - 1u);
-      c = L.tab[s];
-      if (c == 0u) {
-        c = atomicCAS(&L.tab[s], 0u, p[j] + 1u);
-        if (c == 0u) break;
-      }
+      s = (s + 1u) & (kSlots - 1u);
+      c = slot_cas(tab, s, 0u, p[j] + 1u);
+      if (c == 0u) break;
     }
   }
   __syncthreads();
@@ -1428,28 +1539,24 @@ __device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool 
   uint64_t pid[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
     pid[j] = ((uint64_t)rb[j].y << 32) | rb[j].x;
-    sl[j] = join_slot(hh, pid[j]);
-    e[j] = v[j] && pid[j] != 0ull ? L.tab[sl[j]] : 0u;
+    sl[j] = v[j] ? join_slot(lkx[p[j]] & (PACK ? kKeyLow : ~0ull), pid[j], kSlots) : 0u;
+    e[j] = v[j] && pid[j] != 0ull ? slot_get(tab, sl[j]) : 0u;
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const uint64_t hh = ((uint64_t)ra[j].y << 32) | ra[j].x;
     prow[j] = pid[j] == 0ull ? eo.S : eo.S + 1u;  // ROOT / ORPHAN unless the trace holds it
     if (e[j] == 0u) continue;
     const uint32_t q = e[j] - 1u;
-    if (L.h[q] == hh && L.sid[q] == pid[j]) {
-      e[j] = q + 1u;  // found: its service below
-      continue;
-    }
+    const uint64_t kj = lkx[p[j]];
+    if (same_trace(lkx[q], kj) && lsid[q] == pid[j]) continue;  // found: its service below
     uint32_t s = sl[j];
     e[j] = 0u;
     while (true) {
-      s = (s + 1u) & (kJoinSlots - 1u);
-      const uint32_t c = L.tab[s];
+      s = (s + 1u) & (kSlots - 1u);
+      const uint32_t c = slot_get(tab, s);
       if (c == 0u) break;
-      if (L.h[c - 1u] == hh && L.sid[c - 1u] == pid[j]) {
+      if (same_trace(lkx[c - 1u], kj) && lsid[c - 1u] == pid[j]) {
         e[j] = c;
         break;
       }
@@ -1458,25 +1565,36 @@ __device__ __forceinline__ void join_bucket(JoinLds& L, uint32_t a0, const bool 
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     if (!v[j]) continue;
-    if (e[j] != 0u) prow[j] = L.svc[e[j] - 1u];
+    if (e[j] != 0u) prow[j] = PACK ? (uint32_t)(lkx[e[j] - 1u] >> 52) : lsvc[e[j] - 1u];
     const uint32_t svc = rb[j].z & 0xFFFFu, fl = rb[j].z >> 16;
     eo.rec[a0 + p[j]] = ((uint64_t)(prow[j] * eo.S + svc) << 33) |
                         ((uint64_t)((fl & ANOMOD_FLAG_ERROR) ? 1u : 0u) << 32) | rb[j].w;
   }
 }
 
-__global__ __launch_bounds__(kJoinW) void bk_bucket_join_kernel(
+constexpr int kJoinW = 512, kJoinPer = 4;           // 2 048 spans per bucket
+// Waves per SIMD the small join kernel's registers must allow: 8 = four
+// workgroups per CU (64 VGPRs, a few dwords spilled); 6 = three (72 VGPRs).
+#ifndef ANOMOD_JOIN_MINW
+#define ANOMOD_JOIN_MINW 8
+#endif
+constexpr int kJoinBigW = 1024;                     // buckets over 2 048 spans
+constexpr int join_big_per(bool pack) { return pack ? 8 : 4; }  // 8 192 / 4 096 spans
+
+// One workgroup per bucket; a bucket over 2 048 spans is listed for the big
+// kernel (a list overflow: the unfused path).
+template <bool PACK, int MINW = PACK ? ANOMOD_JOIN_MINW : 6>
+__global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
     unsigned long long* __restrict__ over_n, uint32_t over_cap,
     unsigned long long* __restrict__ too_big) {
-  __shared__ JoinLds L;
-  constexpr int PER = kJoinPer;
-  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  using G = JoinGeom<kJoinW, kJoinPer, PACK>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[G::kBytes];
   const uint32_t c = blockIdx.x;
   const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
-  if (m > (uint32_t)kJoinCap) {  // the large (sorting) kernel's list
-    if (tid == 0) {
+  if (m > (uint32_t)G::kCap) {
+    if (threadIdx.x == 0) {
       const unsigned long long i = atomicAdd(over_n, 1ull);
       if (i < over_cap) over[i] = c;
       else atomicAdd(too_big, 1ull);
@@ -1484,23 +1602,32 @@ __global__ __launch_bounds__(kJoinW) void bk_bucket_join_kernel(
     return;
   }
   if (m == 0) return;
-  uint32_t p[PER];
-  bool v[PER];
-  uint32_t idx[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    p[j] = (uint32_t)(w * (PER * kWv) + j * kWv + lane);
-    v[j] = p[j] < m;
-    idx[j] = v[j] ? (uint32_t)pin[a0 + p[j]] : 0u;
+  join_bucket<kJoinW, kJoinPer, PACK>(lds, a0, m, pin, rec, eo);
+}
+
+// The listed buckets, one workgroup each in turn; one over this kernel's
+// capacity (traces of thousands of spans side by side) sends the set to the
+// unfused path (too_big).
+template <bool PACK>
+__global__ __launch_bounds__(kJoinBigW) void bk_join_big_kernel(
+    const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
+    const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ over,
+    const unsigned long long* __restrict__ over_n, uint32_t over_cap,
+    unsigned long long* __restrict__ too_big) {
+  constexpr int PER = join_big_per(PACK);
+  using G = JoinGeom<kJoinBigW, PER, PACK>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[G::kBytes];
+  const uint64_t cnt = *over_n < over_cap ? *over_n : over_cap;
+  for (uint64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const uint32_t c = over[i];
+    const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
+    if (m > (uint32_t)G::kCap) {
+      if (threadIdx.x == 0) atomicAdd(too_big, 1ull);
+      continue;
+    }
+    join_bucket<kJoinBigW, PER, PACK>(lds, a0, m, pin, rec, eo);
+    __syncthreads();  // the next bucket reuses the LDS
   }
-  uint4 ra[PER], rb[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
-    const uint4* q = reinterpret_cast<const uint4*>(rec + idx[j]);
-    ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
-    rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
-  }
-  join_bucket(L, a0, v, ra, rb, eo);
 }
 
 // The fused ungrouped aggregation's bucket kernels: the same sort, then
@@ -1705,6 +1832,9 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   GRec* recs = ws->aos[0];                    // level-A records (gathered by the buckets)
   SoaOut cols = soa_of(ws->aos[1]);           // the grouped columns
   if (!want_h) cols.h = nullptr;              // an aggregation reads no trace_hash column
+  // the fused aggregation's per-bucket hash join (ANOMOD_FUSED_JOIN=0: the
+  // sorting bucket kernels' edge form)
+  const bool join = eo && env_int("ANOMOD_FUSED_JOIN", 1) != 0;
   uint64_t* pa = ws->pairs[0];                // level-A pairs
   uint64_t* pb = ws->pairs[1];                // level-B pairs
   hipStream_t st = ctx->stream;
@@ -1756,8 +1886,14 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       g.DB = kDMax;  // long traces side by side: split finer
       g.T = g.DA + g.DB;
     }
-    hipLaunchKernelGGL(bk_scatter_b_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st, pa,
-                       pb, g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap, na, nxB);
+    // the join resolves repeated ids by level-A position: level B need not be
+    // stable there (ANOMOD_BK_STABLE_B=1 keeps the stable scatter for A/B)
+    if (join && !env_int("ANOMOD_BK_STABLE_B", 0))
+      hipLaunchKernelGGL(bk_scatter_b_fast_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st,
+                         pa, pb, g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap, na, nxB);
+    else
+      hipLaunchKernelGGL(bk_scatter_b_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st, pa,
+                         pb, g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap, na, nxB);
     pin = pb;
     bstart = ws->bstart;
   } else {
@@ -1792,11 +1928,29 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
                                                  (uint64_t)std::max(per_cu, 1));
   };
   if (eo) {  // the fused ungrouped aggregation: edge records, no columns, no trace_ptr
-    if (env_int("ANOMOD_FUSED_JOIN", 1))
-      hipLaunchKernelGGL(bk_bucket_join_kernel, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
-                         recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
-                         ws->misc + kMiscTooBig);
-    else if (pipe)
+    if (join) {
+      // PACK: the service rides in the 12 key bits every k of a bucket shares
+      // (ANOMOD_JOIN_PACK=0 forces the separate service array: tests)
+      const bool pack = g.T >= 12 && env_int("ANOMOD_JOIN_PACK", 1) != 0;
+      const unsigned big_grid = (unsigned)std::max(ctx->num_cus, 1);
+      if (pack) {
+        // ANOMOD_JOIN_W6=1: the 3-workgroups-per-CU form (no spills; A/B)
+        auto fn = env_int("ANOMOD_JOIN_W6", 0) ? bk_join_kernel<true, 6> : bk_join_kernel<true>;
+        hipLaunchKernelGGL(fn, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
+                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                           ws->misc + kMiscTooBig);
+        hipLaunchKernelGGL(bk_join_big_kernel<true>, dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
+                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                           ws->misc + kMiscTooBig);
+      } else {
+        hipLaunchKernelGGL(bk_join_kernel<false>, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
+                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                           ws->misc + kMiscTooBig);
+        hipLaunchKernelGGL(bk_join_big_kernel<false>, dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
+                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                           ws->misc + kMiscTooBig);
+      }
+    } else if (pipe)
       hipLaunchKernelGGL(bk_bucket_pipe_kernel<true>,
                          dim3(pipe_grid(reinterpret_cast<const void*>(bk_bucket_pipe_kernel<true>))),
                          dim3(kSmallW), 0, st, pin, recs, SoaOut{}, *eo, bstart, (uint32_t)nbk,
@@ -1806,9 +1960,10 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       hipLaunchKernelGGL(bk_bucket_edge_kernel, dim3((unsigned)nbk), dim3(kSmallW), 0, st, pin,
                          recs, *eo, bstart, kshift, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                          ws->misc + kMiscTooBig);
-    hipLaunchKernelGGL(bk_bucket_edge_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
-                       dim3(kBigW), 0, st, pin, recs, *eo, bstart, kshift, ws->over,
-                       ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
+    if (!join)
+      hipLaunchKernelGGL(bk_bucket_edge_big_kernel, dim3((unsigned)std::max(ctx->num_cus, 1)),
+                         dim3(kBigW), 0, st, pin, recs, *eo, bstart, kshift, ws->over,
+                         ws->misc + kMiscBigN, (uint32_t)nbk, ws->misc + kMiscTooBig);
     ANOMOD_HIP(ctx, hipGetLastError());
     ANOMOD_HIP(ctx, hipMemcpyAsync(ws->h_misc + kMiscRead, ws->misc + kMiscRead,
                                    (kMiscWords - kMiscRead) * 8, hipMemcpyDeviceToHost, st));
@@ -1817,6 +1972,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
     res->passes = g.DB ? 2 : 1;
     res->bits = g.T;
     res->bucket = true;
+    res->join = join;
     return ANOMOD_OK;
   }
   if (pipe)

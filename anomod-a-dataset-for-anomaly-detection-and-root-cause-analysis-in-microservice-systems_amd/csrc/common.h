@@ -17,7 +17,19 @@ namespace anomod {
 // otherwise (anomod_last_error).
 void set_error(anomod_ctx* ctx, const char* fmt, ...);
 
-struct GroupWs;  // group.hip
+struct GroupWs;   // group.hip
+struct Uploader;  // upload.hip
+
+// One host -> device copy of the upload pipeline (upload.hip): kind 0 copies
+// n bytes from a; kind 1 packs n elements of svc (u16, a) | flags (u16, b) << 16
+// into u32 words.
+struct UpItem {
+  void* dst;
+  const void* a;
+  const void* b;
+  uint64_t n;
+  int kind;
+};
 
 enum Stage { kStageEdgeAgg = 0, kStageEdgeFinal = 1, kStageEdgeReduce = 2, kStageEwma = 3,
              kStagePagerank = 4, kStageTraceStruct = 5, kStageSegments = 6, kStageSummary = 7,
@@ -57,6 +69,11 @@ struct anomod_ctx {
   // Pinned host staging for the edge table's small per-edge vectors (one D2H).
   void* h_stage = nullptr;
   size_t stage_bytes = 0;
+  // Upload pipeline (worker threads, their streams and pinned buffers) and
+  // the grow-only device span set anomod_edge_aggregate_host fills.
+  anomod::Uploader* uploader = nullptr;
+  anomod_spans* host_set = nullptr;
+  uint64_t host_set_spans = 0, host_set_traces = 0;  // its capacity
 };
 
 struct anomod_spans {
@@ -177,6 +194,11 @@ int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_
 void free_spans(anomod_spans* s);
 // Trace-grouping workspace (group.hip), released with the ctx.
 void free_group_ws(anomod_ctx* ctx);
+// Host -> device copies through the pinned staging pipeline (upload.hip);
+// *max_svc = the largest service index a kind-1 item packed.  Returns after
+// every copy landed.  free_uploader releases the pipeline with the ctx.
+int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* max_svc);
+void free_uploader(anomod_ctx* ctx);
 // Edge table of n per-span edge records (the fused ungrouped aggregation:
 // (parent row * S + service) << 33 | error << 32 | duration, csrc/bucket.hip)
 // into `out`, merged over an attached communicator; *hist_form is the set's

@@ -347,6 +347,8 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   anomod::free_group_ws(ctx);
+  anomod::free_uploader(ctx);
+  if (ctx->host_set) anomod::free_spans(ctx->host_set);
   if (ctx->d_status) (void)hipFree(ctx->d_status);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->d_table) (void)hipFree(ctx->d_table);

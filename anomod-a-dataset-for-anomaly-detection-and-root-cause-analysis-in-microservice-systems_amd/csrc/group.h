@@ -90,6 +90,7 @@ struct GroupResult {
   int passes = 0;   // LSD: radix passes; bucket path: scatter levels
   int bits = 0;     // key bits the passes / levels sorted on
   bool bucket = false;
+  bool join = false;  // fused aggregation: the per-bucket hash join ran (else the sorting kernels)
 };
 
 // Bucket path geometry for n spans (bucket.hip).

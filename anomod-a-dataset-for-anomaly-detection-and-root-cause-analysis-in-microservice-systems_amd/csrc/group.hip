@@ -930,7 +930,7 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
       rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
       if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
       if (rc == ANOMOD_OK && !fallback) {
-        ctx->group_path = 2;
+        ctx->group_path = g.join ? 2 : 3;  // join / fused-sort
         ctx->group_levels = g.passes;
         ctx->group_bits = g.bits;
         return edge_aggregate_records(ctx, erec, n, n_services, &spans->hist_form, out);

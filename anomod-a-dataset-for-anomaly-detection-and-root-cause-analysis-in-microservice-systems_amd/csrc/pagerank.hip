@@ -55,6 +55,7 @@ struct anomod_graph {
   int bcoop_blocks = -1; // the same for the persistent batch kernel of width bcoop_kb
   uint32_t bcoop_kb = 0;
   bool bcoop_ring = false;
+  uint32_t bcoop_sub = 0;
   uint32_t last_path = 0;   // ANOMOD_PPR_PATH_* of the last single-vector solve
   uint32_t fallbacks = 0;   // persistent solves rerun per launch (barrier timed out)
   double* h_pin = nullptr;  // pinned [N] staging of p in / x out (single-vector solve)
@@ -642,8 +643,12 @@ __device__ __forceinline__ void store16_wt(void* p, v4u32 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
 }
 
-template <int K, bool RING>
-__global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
+// SUB: a workgroup holds SUB consecutive 256-row blocks (SUB * 256 threads);
+// each block keeps its rows, edge order, reduction tree and fixed-point slot,
+// only the number of workgroups meeting at the grid barrier shrinks — K = 16
+// (216 VGPRs) at SUB = 2 puts N = 10^5's 391 blocks in 196 resident workgroups.
+template <int K, bool RING, int SUB = 1>
+__global__ __launch_bounds__(kPprThreads * SUB) void ppr_batch_persistent_kernel(
     uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
     const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
     const double* __restrict__ p, double alpha, double* x0, double* x1, unsigned long long* acc,
@@ -652,23 +657,26 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
   // 24 KB of (col, w) (~1 800 in-edges per 256-row block at N = 10^5; the
   // rest from global memory) + the store staging: three workgroups per CU
   // (the residency check admits per-CU occupancy minus one)
-  constexpr uint32_t kLdsE = 3072u;
+  constexpr uint32_t kLdsE = 3072u * SUB;
   constexpr int S = kAccSlots * K;   // one accumulator block: K x kAccSlots
-  constexpr int kNW = kPprThreads / 64;
+  constexpr int kNW = kPprThreads / 64;  // waves per 256-row block
+  constexpr int kWaves = kNW * SUB;
   __shared__ uint32_t lcol[kLdsE];
   __shared__ float lw[kLdsE];
-  __shared__ double red[2 * K * kNW];
+  __shared__ double red[SUB * 2 * K * kNW];
   __shared__ double s_dsum[K];
-  __shared__ v4u32 stg[kNW * 64 * (K / 2 + 1)];  // per wave: 64 rows of K doubles (+ a pad piece)
+  __shared__ v4u32 stg[kWaves * 64 * (K / 2 + 1)];  // per wave: 64 rows of K doubles (+ a pad piece)
   __shared__ uint32_t s_conv;
   __shared__ int s_flag;
-  const uint32_t r = blockIdx.x * kRowsPerBlock + threadIdx.x;
-  const uint32_t r0 = blockIdx.x * kRowsPerBlock;
+  const uint32_t sub = threadIdx.x / kPprThreads, lt = threadIdx.x % kPprThreads;
+  const uint32_t gb = blockIdx.x * SUB + sub;  // the 256-row block of this thread
+  const uint32_t r = blockIdx.x * SUB * kRowsPerBlock + threadIdx.x;
+  const uint32_t r0 = blockIdx.x * SUB * kRowsPerBlock;
   const uint32_t r0e = r0 < N ? r0 : N;
-  const uint32_t r1 = r0 + kRowsPerBlock < N ? r0 + kRowsPerBlock : N;
+  const uint32_t r1 = r0 + SUB * kRowsPerBlock < N ? r0 + SUB * kRowsPerBlock : N;
   const uint32_t e0 = in_ptr[r0e], e1 = in_ptr[r1];
   const uint32_t nc = e1 - e0 < kLdsE ? e1 - e0 : kLdsE;
-  for (uint32_t i = threadIdx.x; i < nc; i += kPprThreads) {
+  for (uint32_t i = threadIdx.x; i < nc; i += kPprThreads * SUB) {
     lcol[i] = in_col[e0 + i];
     lw[i] = in_w[e0 + i];
   }
@@ -706,7 +714,7 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
     // the previous iteration's per-vector slots: dangling mass, and (tolerance
     // mode) L1 change -> the vectors converged by then
     const bool check = ntol > 0.0 && it > 0;
-    for (int k = wid; k < K; k += kNW) {
+    for (int k = wid; k < K; k += kWaves) {
       unsigned long long dv = __hip_atomic_load(&acc[rr * S + k * kAccSlots + lane],
                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned long long ev = check ? __hip_atomic_load(&acc[(3 + rr) * S + k * kAccSlots + lane],
@@ -805,26 +813,26 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_persistent_kernel(
         eacc[k] += __shfl_xor(eacc[k], off);
       }
       if (lane == 0) {
-        red[(2 * k) * kNW + wid] = dacc[k];
-        red[(2 * k + 1) * kNW + wid] = eacc[k];
+        red[sub * 2 * K * kNW + (2 * k) * kNW + (wid % kNW)] = dacc[k];
+        red[sub * 2 * K * kNW + (2 * k + 1) * kNW + (wid % kNW)] = eacc[k];
       }
     }
     __syncthreads();
     // block_sum's order: thread 0 of the per-launch kernel adds the 4 wave
     // partials from 0.0 in wave order; here thread k does it for vector k
-    if (threadIdx.x < K) {
-      const int k = threadIdx.x;
+    if (lt < (uint32_t)K) {
+      const int k = (int)lt;
       double ds = 0.0, es = 0.0;
       for (int q = 0; q < kNW; ++q) {
-        ds += red[(2 * k) * kNW + q];
-        es += red[(2 * k + 1) * kNW + q];
+        ds += red[sub * 2 * K * kNW + (2 * k) * kNW + q];
+        es += red[sub * 2 * K * kNW + (2 * k + 1) * kNW + q];
       }
-      const int sl = k * kAccSlots + (blockIdx.x & (kAccSlots - 1));
+      const int sl = k * kAccSlots + (int)(gb & (kAccSlots - 1));
       atomicAdd(&acc[w * S + sl], __double2ull_rn(ds * kDScale));
       atomicAdd(&acc[(3 + w) * S + sl], __double2ull_rn(es * kEScale));
     }
     if (blockIdx.x == 0)
-      for (int i = threadIdx.x; i < S; i += kPprThreads) {
+      for (int i = threadIdx.x; i < S; i += kPprThreads * SUB) {
         __hip_atomic_store(&acc[z * S + i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&acc[(3 + z) * S + i], 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -886,7 +894,23 @@ __global__ __launch_bounds__(kPprThreads) void ppr_batch_out_kernel(const double
 using BatchFn = void (*)(uint32_t, const uint32_t*, const uint32_t*, const float*, const uint8_t*,
                         const double*, double, double*, double*, unsigned long long*, uint32_t,
                         double, unsigned int*, uint32_t, double*, uint64_t);
-BatchFn batch_persistent_fn(uint32_t kb, bool ring) {
+// 256-row blocks per workgroup of the batched persistent solve: K = 16 takes
+// 2 (216 VGPRs: one block per workgroup left N = 10^5's 391 blocks
+// non-resident, the batch ran per launch); ANOMOD_PPR_BSUB overrides (1 / 2).
+uint32_t batch_sub(uint32_t kb) {
+  const char* e = getenv("ANOMOD_PPR_BSUB");
+  if (e && *e) return atoi(e) >= 2 ? 2u : 1u;
+  return kb >= 16 ? 2u : 1u;
+}
+
+BatchFn batch_persistent_fn(uint32_t kb, bool ring, uint32_t sub = 1) {
+  if (sub >= 2) {
+    if (ring)
+      return kb == 2 ? ppr_batch_persistent_kernel<2, true, 2> : kb == 4 ? ppr_batch_persistent_kernel<4, true, 2>
+           : kb == 8 ? ppr_batch_persistent_kernel<8, true, 2> : ppr_batch_persistent_kernel<16, true, 2>;
+    return kb == 2 ? ppr_batch_persistent_kernel<2, false, 2> : kb == 4 ? ppr_batch_persistent_kernel<4, false, 2>
+         : kb == 8 ? ppr_batch_persistent_kernel<8, false, 2> : ppr_batch_persistent_kernel<16, false, 2>;
+  }
   if (ring)
     return kb == 2 ? ppr_batch_persistent_kernel<2, true> : kb == 4 ? ppr_batch_persistent_kernel<4, true>
          : kb == 8 ? ppr_batch_persistent_kernel<8, true> : ppr_batch_persistent_kernel<16, true>;
@@ -1424,26 +1448,29 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   const uint64_t slot = (uint64_t)g->grid * kRowsPerBlock * kb;  // doubles per ring slot
   const char* ring_env = getenv("ANOMOD_PPR_RING");
   bool ring = !(ring_env && ring_env[0] == '0') && (uint64_t)iters * slot * 8 <= kRingBytes;
-  const BatchFn bfn = batch_persistent_fn(kb, ring);
-  if (g->bcoop_kb != kb || g->bcoop_ring != ring) {
+  const uint32_t bsub = batch_sub(kb);
+  const uint32_t bgrid = (g->grid + bsub - 1) / bsub;  // persistent workgroups
+  const BatchFn bfn = batch_persistent_fn(kb, ring, bsub);
+  if (g->bcoop_kb != kb || g->bcoop_ring != ring || g->bcoop_sub != bsub) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfn, kPprThreads, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfn, kPprThreads * bsub, 0) != hipSuccess)
       per_cu = 0;
     (void)hipGetLastError();
     g->bcoop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
     g->bcoop_kb = kb;
     g->bcoop_ring = ring;
+    g->bcoop_sub = bsub;
   }
-  bool persistent = mode != 1 && (int)g->grid <= g->bcoop_blocks;
+  bool persistent = mode != 1 && (int)bgrid <= g->bcoop_blocks;
   if (persistent && ring) {
     ring = ensure_ring(ctx, g, (uint64_t)iters * slot * 8);
     if (!ring) {  // no ring: the two-buffer instantiation (its own residency)
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, batch_persistent_fn(kb, false),
-                                                       kPprThreads, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, batch_persistent_fn(kb, false, bsub),
+                                                       kPprThreads * bsub, 0) != hipSuccess)
         per_cu = 0;
       (void)hipGetLastError();
-      persistent = (int)g->grid <= (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
+      persistent = (int)bgrid <= (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
     }
   }
   if (persistent) ANOMOD_HIP(ctx, hipMemsetAsync(g->bar, 0, kBarWords * sizeof(unsigned int),
@@ -1453,7 +1480,7 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   bool fell_back = false;
   if (persistent) {
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
-    hipLaunchKernelGGL(batch_persistent_fn(kb, ring), dim3(g->grid), dim3(kPprThreads), 0,
+    hipLaunchKernelGGL(batch_persistent_fn(kb, ring, bsub), dim3(bgrid), dim3(kPprThreads * bsub), 0,
                        ctx->stream, N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->bp, alpha,
                        g->bx[0], g->bx[1], g->bacc, iters, ntol, g->bar, spin,
                        ring ? g->ring : nullptr, slot);

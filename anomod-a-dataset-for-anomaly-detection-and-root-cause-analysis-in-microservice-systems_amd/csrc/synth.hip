@@ -656,61 +656,114 @@ int anomod_spans_unique_ids(const anomod_spans* spans, int* unique) {
   return ANOMOD_OK;
 }
 
-int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
-                        const uint64_t* trace_ptr, uint64_t n_traces, anomod_spans** out) {
-  ANOMOD_REQUIRE(nullptr, ctx && soa && out, "anomod_spans_upload: NULL argument");
-  *out = nullptr;
+namespace {
+
+// Validates an upload's arguments (kernels index by these values) and returns
+// the longest trace in *max_len.
+int check_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                 const uint64_t* trace_ptr, uint64_t n_traces, uint64_t* max_len) {
   ANOMOD_REQUIRE(ctx, n_traces == 0 || trace_ptr, "trace_ptr is NULL");
   ANOMOD_REQUIRE(ctx, n_spans == 0 || (soa->span_id && soa->parent_span_id && soa->svc &&
                                        soa->flags && soa->dur_us),
                  "span arrays must be non-NULL");
   ANOMOD_REQUIRE(ctx, n_traces < (1ull << 36), "n_traces too large");
-  // Host-side validation: kernels index by these values.
-  uint64_t max_len = 0;
+  uint64_t ml = 0;
   for (uint64_t t = 0; t < n_traces; ++t) {
     ANOMOD_REQUIRE(ctx, trace_ptr[t] <= trace_ptr[t + 1],
                    "trace_ptr is not non-decreasing at trace %llu", (unsigned long long)t);
-    max_len = std::max<uint64_t>(max_len, trace_ptr[t + 1] - trace_ptr[t]);
+    ml = std::max<uint64_t>(ml, trace_ptr[t + 1] - trace_ptr[t]);
   }
   if (n_traces) {
     ANOMOD_REQUIRE(ctx, trace_ptr[n_traces] <= n_spans,
                    "trace_ptr[n_traces]=%llu exceeds n_spans=%llu",
                    (unsigned long long)trace_ptr[n_traces], (unsigned long long)n_spans);
   }
-  uint32_t max_svc = 0;
-  for (uint64_t i = 0; i < n_spans; ++i) max_svc = std::max<uint32_t>(max_svc, soa->svc[i]);
+  *max_len = ml;
+  return ANOMOD_OK;
+}
+
+// The columns of soa (trace_hash only when with_hash and given) and trace_ptr
+// into s through the staging pipeline; s->max_svc from the packing pass.
+int fill_set(anomod_ctx* ctx, anomod_spans* s, const anomod_span_soa* soa, uint64_t n_spans,
+             const uint64_t* trace_ptr, uint64_t n_traces, bool with_hash) {
+  UpItem it[7];
+  int k = 0;
+  if (n_traces) it[k++] = {s->trace_ptr, trace_ptr, nullptr, (n_traces + 1) * 8, 0};
+  else ANOMOD_HIP(ctx, hipMemsetAsync(s->trace_ptr, 0, 8, ctx->stream));
+  if (with_hash && soa->trace_hash && s->trace_hash)
+    it[k++] = {s->trace_hash, soa->trace_hash, nullptr, n_spans * 8, 0};
+  it[k++] = {s->span_id, soa->span_id, nullptr, n_spans * 8, 0};
+  it[k++] = {s->parent_span_id, soa->parent_span_id, nullptr, n_spans * 8, 0};
+  it[k++] = {s->svc_flags, soa->svc, soa->flags, n_spans, 1};
+  it[k++] = {s->dur_us, soa->dur_us, nullptr, n_spans * 4, 0};
+  uint32_t mx = 0;
+  if (int rc = upload_items(ctx, it, k, &mx)) return rc;
+  s->max_svc = mx;
+  return ANOMOD_OK;
+}
+
+}  // namespace
+
+int anomod_spans_upload(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                        const uint64_t* trace_ptr, uint64_t n_traces, anomod_spans** out) {
+  ANOMOD_REQUIRE(nullptr, ctx && soa && out, "anomod_spans_upload: NULL argument");
+  *out = nullptr;
+  uint64_t max_len = 0;
+  if (int rc = check_upload(ctx, soa, n_spans, trace_ptr, n_traces, &max_len)) return rc;
   if (int rc = bind(ctx)) return rc;
   anomod_spans* s = nullptr;
   if (int rc = alloc_spans(ctx, n_spans, n_traces, soa->trace_hash != nullptr, &s)) return rc;
-  s->max_svc = max_svc;
   // (no trace_ptr: an ungrouped set, its trace lengths unknown until grouped)
   s->max_trace_len = n_traces || !n_spans ? max_len : ~0ull;
-  hipError_t e = hipSuccess;
-  auto cp = [&](void* dst, const void* src, size_t bytes) {
-    if (e == hipSuccess && bytes)
-      e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
-  };
-  if (n_traces) {
-    cp(s->trace_ptr, trace_ptr, (n_traces + 1) * 8);
-  } else if (e == hipSuccess) {
-    e = hipMemsetAsync(s->trace_ptr, 0, 8, ctx->stream);
-  }
-  if (soa->trace_hash) cp(s->trace_hash, soa->trace_hash, n_spans * 8);
-  cp(s->span_id, soa->span_id, n_spans * 8);
-  cp(s->parent_span_id, soa->parent_span_id, n_spans * 8);
-  std::vector<uint32_t> packed(n_spans);
-  for (uint64_t i = 0; i < n_spans; ++i)
-    packed[i] = (uint32_t)soa->svc[i] | ((uint32_t)soa->flags[i] << 16);
-  cp(s->svc_flags, packed.data(), n_spans * 4);
-  cp(s->dur_us, soa->dur_us, n_spans * 4);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  if (e != hipSuccess) {
+  if (int rc = fill_set(ctx, s, soa, n_spans, trace_ptr, n_traces, true)) {
     free_spans(s);
-    set_error(ctx, "span upload failed: %s", hipGetErrorString(e));
-    return ANOMOD_EHIP;
+    return rc;
   }
   *out = s;
   return ANOMOD_OK;
+}
+
+int anomod_edge_aggregate_host(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                               const uint64_t* trace_ptr, uint64_t n_traces, uint32_t n_services,
+                               int unique_ids, int* scan_order, int* hist_form,
+                               anomod_edge_table* out) {
+  ANOMOD_REQUIRE(nullptr, ctx && soa && out && scan_order && hist_form,
+                 "anomod_edge_aggregate_host: NULL argument");
+  ANOMOD_REQUIRE(ctx, *scan_order >= -1 && *scan_order <= 1 && *hist_form >= -1 && *hist_form <= 1,
+                 "scan_order=%d / hist_form=%d outside [-1, 1]", *scan_order, *hist_form);
+  uint64_t max_len = 0;
+  int local = check_upload(ctx, soa, n_spans, trace_ptr, n_traces, &max_len);
+  if (local == ANOMOD_OK) local = bind(ctx);
+  // the ctx's grow-only set: no trace_hash (a grouped aggregation reads none)
+  if (local == ANOMOD_OK &&
+      (!ctx->host_set || ctx->host_set_spans < n_spans || ctx->host_set_traces < n_traces)) {
+    if (ctx->host_set) {
+      (void)hipStreamSynchronize(ctx->stream);
+      free_spans(ctx->host_set);
+      ctx->host_set = nullptr;
+    }
+    const uint64_t cs = std::max<uint64_t>(n_spans, ctx->host_set_spans);
+    const uint64_t ct = std::max<uint64_t>(n_traces, ctx->host_set_traces);
+    local = alloc_spans(ctx, cs, ct, false, &ctx->host_set);
+    ctx->host_set_spans = local == ANOMOD_OK ? cs : 0;
+    ctx->host_set_traces = local == ANOMOD_OK ? ct : 0;
+  }
+  anomod_spans* s = ctx->host_set;
+  if (local == ANOMOD_OK) {
+    s->n_spans = n_spans;
+    s->n_traces = n_traces;
+    s->grouped = true;
+    s->unique_ids = unique_ids != 0;
+    s->order = (int8_t)*scan_order;
+    s->hist_form = (int8_t)*hist_form;
+    s->max_trace_len = max_len;
+    local = fill_set(ctx, s, soa, n_spans, trace_ptr, n_traces, false);
+  }
+  if (local != ANOMOD_OK) return comm_agree(ctx, local);  // peers learn of it before their reduce
+  const int rc = anomod_edge_aggregate_spans(ctx, s, n_services, out);
+  *scan_order = s->order;
+  *hist_form = s->hist_form;
+  return rc;
 }
 
 int anomod_spans_info(const anomod_spans* spans, uint64_t* n_spans, uint64_t* n_traces) {

@@ -1,0 +1,187 @@
+// Host -> device span upload through a pinned staging pipeline (the product
+// path's one conversion per experiment: collect_trace.sh:70 converts each
+// dump once, then every feature is computed from it).
+//
+// r04 uploaded with pageable hipMemcpyAsync calls after two serial host passes
+// (the max-service scan and a fresh svc|flags packing vector): 108.9 ms for
+// 55.6 M spans, 98 % of it host work.  Here the columns
+// are cut into 8-MiB pieces dealt round-robin to W worker threads; each
+// worker copies (or packs svc|flags, taking the largest service on the way)
+// its piece into one of its two pinned buffers and hands it to the DMA on its
+// own stream, so host copies, packing and PCIe transfers overlap and the
+// DMA sees W streams at once.  The workers, their streams and pinned
+// buffers live with the ctx.
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "common.h"
+
+namespace anomod {
+
+struct Uploader {
+  static constexpr size_t kPiece = size_t(8) << 20;  // bytes of device data per piece
+  struct Piece {
+    int item;
+    uint64_t off, len;  // in the item's units (bytes, or packed elements)
+  };
+  int device = 0, nw = 0;
+  std::vector<std::thread> th;
+  std::vector<hipStream_t> st;
+  std::vector<void*> pin;       // two per worker
+  std::vector<hipEvent_t> ev;   // two per worker
+  std::mutex m;
+  std::condition_variable cv_go, cv_done;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool quit = false;
+  const UpItem* items = nullptr;
+  std::vector<Piece> pieces;
+  std::vector<uint32_t> wmax;
+  std::vector<hipError_t> werr;
+
+  void work(int w) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv_go.wait(lk, [&] { return quit || gen != seen; });
+        if (quit) return;
+        seen = gen;
+      }
+      hipError_t err = hipSetDevice(device);
+      uint32_t mx = 0;
+      int slot = 0;
+      for (size_t i = (size_t)w; err == hipSuccess && i < pieces.size(); i += (size_t)nw) {
+        const Piece& P = pieces[i];
+        const UpItem& it = items[P.item];
+        void* buf = pin[2 * w + slot];
+        err = hipEventSynchronize(ev[2 * w + slot]);  // the DMA out of this buffer is done
+        if (err != hipSuccess) break;
+        size_t bytes;
+        char* dst;
+        if (it.kind == 1) {  // svc (u16) | flags (u16) << 16 -> u32
+          const uint16_t* svc = static_cast<const uint16_t*>(it.a) + P.off;
+          const uint16_t* fl = static_cast<const uint16_t*>(it.b) + P.off;
+          uint32_t* o = static_cast<uint32_t*>(buf);
+          for (uint64_t j = 0; j < P.len; ++j) {
+            o[j] = (uint32_t)svc[j] | ((uint32_t)fl[j] << 16);
+            mx = svc[j] > mx ? svc[j] : mx;
+          }
+          bytes = P.len * 4;
+          dst = static_cast<char*>(it.dst) + P.off * 4;
+        } else {
+          std::memcpy(buf, static_cast<const char*>(it.a) + P.off, P.len);
+          bytes = P.len;
+          dst = static_cast<char*>(it.dst) + P.off;
+        }
+        err = hipMemcpyAsync(dst, buf, bytes, hipMemcpyHostToDevice, st[w]);
+        if (err == hipSuccess) err = hipEventRecord(ev[2 * w + slot], st[w]);
+        slot ^= 1;
+      }
+      const hipError_t e2 = hipStreamSynchronize(st[w]);
+      if (err == hipSuccess) err = e2;
+      std::lock_guard<std::mutex> lk(m);
+      wmax[w] = mx;
+      werr[w] = err;
+      if (--pending == 0) cv_done.notify_one();
+    }
+  }
+};
+
+namespace {
+
+int make_uploader(anomod_ctx* ctx) {
+  if (ctx->uploader) return ANOMOD_OK;
+  auto* u = new Uploader();
+  u->device = ctx->device;
+  const char* e = std::getenv("ANOMOD_UPLOAD_THREADS");
+  int nw = e && *e ? std::atoi(e) : 8;
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw) nw = std::min<int>(nw, (int)hw);
+  nw = std::max(1, std::min(nw, 32));
+  u->nw = nw;
+  u->st.assign(nw, nullptr);
+  u->pin.assign(2 * nw, nullptr);
+  u->ev.assign(2 * nw, nullptr);
+  u->wmax.assign(nw, 0u);
+  u->werr.assign(nw, hipSuccess);
+  bool ok = true;
+  for (int w = 0; ok && w < nw; ++w) {
+    ok = hipStreamCreateWithFlags(&u->st[w], hipStreamNonBlocking) == hipSuccess;
+    for (int s = 0; ok && s < 2; ++s) {
+      ok = hipHostMalloc(&u->pin[2 * w + s], Uploader::kPiece, hipHostMallocDefault) == hipSuccess &&
+           hipEventCreateWithFlags(&u->ev[2 * w + s], hipEventDisableTiming) == hipSuccess;
+    }
+  }
+  ctx->uploader = u;  // (freed by free_uploader on failure too)
+  if (!ok) {
+    free_uploader(ctx);
+    set_error(ctx, "creating the upload pipeline (%d pinned 2 x 8-MiB buffers) failed", nw);
+    return ANOMOD_ENOMEM;
+  }
+  for (int w = 0; w < nw; ++w) u->th.emplace_back([u, w] { u->work(w); });
+  return ANOMOD_OK;
+}
+
+}  // namespace
+
+void free_uploader(anomod_ctx* ctx) {
+  Uploader* u = ctx->uploader;
+  if (!u) return;
+  {
+    std::lock_guard<std::mutex> lk(u->m);
+    u->quit = true;
+  }
+  u->cv_go.notify_all();
+  for (auto& t : u->th) t.join();
+  for (auto s : u->st)
+    if (s) (void)hipStreamDestroy(s);
+  for (auto p : u->pin)
+    if (p) (void)hipHostFree(p);
+  for (auto e : u->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete u;
+  ctx->uploader = nullptr;
+}
+
+int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* max_svc) {
+  if (max_svc) *max_svc = 0;
+  uint64_t total = 0;
+  for (int i = 0; i < n_items; ++i) total += items[i].n;
+  if (total == 0) return ANOMOD_OK;
+  if (int rc = make_uploader(ctx)) return rc;
+  Uploader* u = ctx->uploader;
+  // the ctx stream's earlier work on these buffers (a previous call's kernels
+  // reading a reused set) must be done before the worker streams write them
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  u->pieces.clear();
+  for (int i = 0; i < n_items; ++i) {
+    const uint64_t unit = items[i].kind == 1 ? Uploader::kPiece / 4 : Uploader::kPiece;
+    for (uint64_t off = 0; off < items[i].n; off += unit)
+      u->pieces.push_back({i, off, std::min<uint64_t>(unit, items[i].n - off)});
+  }
+  {
+    std::unique_lock<std::mutex> lk(u->m);
+    u->items = items;
+    u->pending = u->nw;
+    ++u->gen;
+    u->cv_go.notify_all();
+    u->cv_done.wait(lk, [&] { return u->pending == 0; });
+  }
+  uint32_t mx = 0;
+  for (int w = 0; w < u->nw; ++w) {
+    if (u->werr[w] != hipSuccess) {
+      set_error(ctx, "span upload failed: %s", hipGetErrorString(u->werr[w]));
+      return ANOMOD_EHIP;
+    }
+    mx = std::max(mx, u->wmax[w]);
+  }
+  if (max_svc) *max_svc = mx;
+  return ANOMOD_OK;
+}
+
+}  // namespace anomod

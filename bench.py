@@ -134,28 +134,61 @@ def cpu_trace_structure(spec, n_traces: int, min_seconds: float) -> dict:
 
 
 def cpu_group(spec, n_traces: int, min_seconds: float) -> dict:
-    """The oracle's grouping (oracle/spec.py group_by_trace: numpy stable
-    argsort of mix64(trace_hash)) + the gather of the 5 span columns, on an
-    interleaved host sample: the CPU side of the ungrouped leg's grouping."""
-    from oracle import spec as ospec
+    """The ungrouped step on the CPU, every usable core: the C oracle's
+    grouping (oracle_group_by_trace: a parallel two-level radix partition of
+    mix64(trace_hash), spans of a trace in arrival order — spec.group_by_trace
+    restated), the gather of the span columns (oracle_take_spans, one row range
+    per thread) and the edge table over the grouped spans (oracle_edge_aggregate,
+    one trace range per thread, tables summed) — the CPU side of the GPU leg's
+    group + join + table step, on an interleaved host sample of the same
+    workload."""
+    from types import SimpleNamespace
+
+    from oracle import native
 
     sample = anomod.synth_generate_host(spec, n_traces)
-    rng = np.random.default_rng(1)
-    perm = rng.permutation(sample.n_spans)
-    cols = {k: getattr(sample, k)[perm] for k in ("trace_hash", "span_id", "parent_span_id", "svc",
-                                                   "flags", "dur_us")}
+    S = len(sample.services)
+    perm = np.random.default_rng(1).permutation(sample.n_spans)
+    src = [np.ascontiguousarray(getattr(sample, k)[perm]) for k in
+           ("trace_hash", "span_id", "parent_span_id", "svc", "flags", "dur_us")]
+    dst = [np.empty_like(a) for a in src]
+    threads = host_cores()["usable"]
+    n = sample.n_spans
+    rows = [(n * i // threads, n * (i + 1) // threads) for i in range(threads)]
+    lib = native.lib()
+
+    def step():
+        order, tptr = native.group_by_trace(src[0], threads)
+        o = np.ascontiguousarray(order, np.uint64)
+        _threads_run(lambda i: lib.oracle_take_spans(
+            native._p(o), rows[i][0], rows[i][1], *[native._p(a) for a in src],
+            *[native._p(a) for a in dst]), threads, 0.0)
+        g = SimpleNamespace(services=sample.services, span_id=dst[1], parent_span_id=dst[2],
+                            svc=dst[3], flags=dst[4], dur_us=dst[5], trace_ptr=tptr,
+                            n_traces=tptr.shape[0] - 1)
+        tb = np.linspace(0, g.n_traces, threads + 1).astype(np.int64)
+        tabs = [None] * threads
+
+        def agg(i):
+            tabs[i] = native.edge_aggregate(g, S, int(tb[i]), int(tb[i + 1]))
+
+        _threads_run(agg, threads, 0.0)
+        return sum(t["count"] for t in tabs)
+
+    cnt = step()  # load + warm; every span lands in the table once
+    if int(cnt.sum()) != n:
+        raise RuntimeError("cpu ungrouped step lost spans")
     r, t0 = 0, time.perf_counter()
     while True:
-        order, _ = ospec.group_by_trace(cols["trace_hash"])
-        for v in cols.values():
-            v.take(order)
+        step()
         r += 1
         el = time.perf_counter() - t0
         if el >= min_seconds:
             break
-    return {"value": sample.n_spans * r / el, "unit": "spans/s", "cores": 1, "kind": "port",
-            "sample": f"{sample.n_spans} interleaved synthetic SN spans x {r} groupings in "
-                      f"{el:.1f} s (numpy stable argsort of mix64 + column gathers, one core)"}
+    return {"value": n * r / el, "unit": "spans/s", "cores": threads, "kind": "port",
+            "sample": f"{n} interleaved synthetic SN spans x {r} ungrouped steps in {el:.1f} s "
+                      f"(C oracle: oracle_group_by_trace radix partition + oracle_take_spans + "
+                      f"oracle_edge_aggregate, {threads} threads each)"}
 
 
 def cpu_ewma(T: int, S_slice: int, W: int, min_seconds: float) -> dict:
@@ -714,29 +747,30 @@ def main() -> int:
             "mode": "row-sharded, per-iteration launches + RCCL all-reduce/all-gather"
                     if world > 1 else "row-sharded path, 1 shard (per-iteration launches)"}
         # batched personalizations (one per fault hypothesis)
-        # (one persistent launch per batch: K vectors per grid barrier)
-        kb = 8
-        Pb = np.random.default_rng(100 + rank).random((kb, g.N))
-        g.pagerank_batch(Pb, iters=args.ppr_iters)
-        bt, bw = [], []
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(3):
-            t1 = time.perf_counter()
+        # (one persistent launch per batch: K vectors per grid barrier; K = 16
+        # in workgroups of two 256-row blocks)
+        for kb, key in ((8, "batched"), (16, "batched_k16")):
+            Pb = np.random.default_rng(100 + rank + kb).random((kb, g.N))
             g.pagerank_batch(Pb, iters=args.ppr_iters)
-            bw.append(round((time.perf_counter() - t1) * 1e3, 3))
-            bt.append(ctx.stage_ms(L.STAGE_PAGERANK))
-        bwall = allmax(time.perf_counter() - t0)
-        b_ms = float(np.mean(bt))
-        result["pagerank"]["batched"] = {
-            "vectors": kb, "path": g.last_solve()[0],
-            "vector_iters_per_s": world * 3 * kb * args.ppr_iters / bwall,
-            "vector_iters_per_s_per_gpu": kb * args.ppr_iters / (b_ms * 1e-3),
-            "iters_per_s_per_gpu": args.ppr_iters / (b_ms * 1e-3),
-            "us_per_batched_iter": b_ms * 1e3 / args.ppr_iters,
-            "wall_ms_per_batch": bw, "last_solve": list(g.last_solve()),
-            "what": "solved vector-iterations/s (wall, all ranks) of 8-vector batches; per-GPU "
-                    "device rates from the kernel time"}
+            bt, bw = [], []
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                t1 = time.perf_counter()
+                g.pagerank_batch(Pb, iters=args.ppr_iters)
+                bw.append(round((time.perf_counter() - t1) * 1e3, 3))
+                bt.append(ctx.stage_ms(L.STAGE_PAGERANK))
+            bwall = allmax(time.perf_counter() - t0)
+            b_ms = float(np.mean(bt))
+            result["pagerank"][key] = {
+                "vectors": kb, "path": g.last_solve()[0],
+                "vector_iters_per_s": world * 3 * kb * args.ppr_iters / bwall,
+                "vector_iters_per_s_per_gpu": kb * args.ppr_iters / (b_ms * 1e-3),
+                "iters_per_s_per_gpu": args.ppr_iters / (b_ms * 1e-3),
+                "us_per_batched_iter": b_ms * 1e3 / args.ppr_iters,
+                "wall_ms_per_batch": bw, "last_solve": list(g.last_solve()),
+                "what": f"solved vector-iterations/s (wall, all ranks) of {kb}-vector batches; "
+                        f"per-GPU device rates from the kernel time"}
         g.free()
     if "ewma" in legs:
         # --- EWMA/z, BASELINE config 4 at its size: S = 10^5 series x ~10^6

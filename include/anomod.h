@@ -183,7 +183,8 @@ int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* ungrouped, anomod_sp
  * *path = 1 bucket path (two stable MSD scatters over the top *bits bits of
  * mix64(trace_hash), then one workgroup per bucket), 2 the same scatters then
  * the per-bucket hash join of anomod_edge_aggregate_ungrouped (edge records,
- * no grouped columns), 0 LSD path (8-bit radix passes + bucket fix-up); *levels = scatter levels / radix passes run;
+ * no grouped columns), 3 the same scatters then the sorting bucket kernels'
+ * edge records (the fused aggregation with ANOMOD_FUSED_JOIN=0), 0 LSD path (8-bit radix passes + bucket fix-up); *levels = scatter levels / radix passes run;
  * *bits = bucket bits (bucket path) or 8 * passes.  All 0 before any grouping. */
 int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits);
 /* Rearranged copies of a grouped set (synthetic arrival orders for tests
@@ -295,6 +296,20 @@ int anomod_metrics_free(anomod_metrics* m);
  * (RCCL all-reduce) before quantiles are taken.                            */
 int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint32_t n_services,
                                 anomod_edge_table* out);
+/* Edge table of a host span set grouped by trace (trace_ptr), in one call:
+ * the columns go to a device set the ctx keeps and regrows only when a
+ * larger set comes (no trace_hash: the aggregation reads none) through the
+ * pinned staging pipeline (worker threads pack svc|flags into pinned
+ * buffers, several DMA streams), then anomod_edge_aggregate_spans.  The
+ * set's hints (anomod_spans_hints) go in through *scan_order / *hist_form
+ * and come back with what the call learned; unique_ids as
+ * anomod_spans_set_unique_ids.  The product path's one conversion per
+ * experiment (collect_trace.sh:70: each dump is converted once, then every
+ * feature comes from it).                                                  */
+int anomod_edge_aggregate_host(anomod_ctx* ctx, const anomod_span_soa* soa, uint64_t n_spans,
+                               const uint64_t* trace_ptr, uint64_t n_traces, uint32_t n_services,
+                               int unique_ids, int* scan_order, int* hist_form,
+                               anomod_edge_table* out);
 /* Edge table of an ungrouped set; a grouped set is aggregated as is.  By
  * default the set is bucketed by trace (the grouping's two scatter levels) and
  * each bucket finds its spans' parents by an LDS hash join on (trace, span id),

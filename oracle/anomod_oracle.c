@@ -295,3 +295,211 @@ void oracle_trace_structure(const uint64_t* span_id, const uint64_t* parent, con
     n_roots[t] = roots;
   }
 }
+
+/* ---- grouping of spans that arrive interleaved (north_star (2)) ----------
+ * The CPU side of anomod_edge_aggregate_ungrouped / anomod_spans_group: the
+ * Elasticsearch path pulls sw_segment-* hits sorted by start_time over all
+ * traces (enhanced_trace_collector.py:80-90), so a trace's spans are known
+ * only by trace_hash.  Output: order[] such that spans taken in that order are
+ * grouped — traces by k = mix64(trace_hash) ascending, the spans of a trace in
+ * arrival order (stable) — and trace_ptr over them; the same result as
+ * oracle/spec.py group_by_trace (a numpy stable argsort), here as a parallel
+ * two-level MSD radix partition (pthreads) so that bench.py can time the
+ * ungrouped step on every usable host core.  Level 1 scatters (k, arrival)
+ * pairs stably by the top 11 bits of k (per-thread chunk counts, one prefix);
+ * level 2 counting-sorts each level-1 bucket by the next 11 bits, then a
+ * stable insertion sort by k finishes each (tiny) sub-bucket. */
+#include <pthread.h>
+
+typedef struct {
+  uint64_t k, i;
+} or_pair;
+
+static uint64_t or_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+#define OR_G_BITS 11u
+#define OR_G_DIG (1u << OR_G_BITS)
+
+typedef struct {
+  const uint64_t* h;
+  uint64_t n;
+  uint32_t threads;
+  or_pair* a; /* pairs in arrival order, then the result */
+  or_pair* b; /* level-1 output */
+  uint64_t* cnt; /* [threads][OR_G_DIG] chunk counts, then scatter cursors */
+  uint64_t* bs;  /* [OR_G_DIG + 1] level-1 bucket starts */
+  uint64_t next; /* level-2 bucket ticket */
+  uint64_t* chg; /* [threads] trace starts per chunk, then their prefix */
+  uint64_t* order;
+  uint64_t* tptr;
+  int phase;
+} or_group;
+
+typedef struct {
+  or_group* g;
+  uint32_t t;
+} or_job;
+
+static void or_chunk(const or_group* g, uint32_t t, uint64_t* lo, uint64_t* hi) {
+  *lo = g->n * t / g->threads;
+  *hi = g->n * (t + 1) / g->threads;
+}
+
+static void* or_group_worker(void* arg) {
+  or_job* j = (or_job*)arg;
+  or_group* g = j->g;
+  const uint32_t t = j->t;
+  uint64_t lo, hi;
+  or_chunk(g, t, &lo, &hi);
+  if (g->phase == 0) { /* keys + chunk counts of the top bits */
+    uint64_t* c = g->cnt + (uint64_t)t * OR_G_DIG;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const uint64_t k = or_mix64(g->h[i]);
+      g->a[i].k = k;
+      g->a[i].i = i;
+      c[k >> (64u - OR_G_BITS)]++;
+    }
+  } else if (g->phase == 1) { /* stable level-1 scatter */
+    uint64_t* c = g->cnt + (uint64_t)t * OR_G_DIG;
+    for (uint64_t i = lo; i < hi; ++i) g->b[c[g->a[i].k >> (64u - OR_G_BITS)]++] = g->a[i];
+  } else if (g->phase == 2) { /* level 2 per bucket, then insertion sort */
+    uint64_t sc[OR_G_DIG];
+    for (;;) {
+      const uint64_t d = __atomic_fetch_add(&g->next, 1ull, __ATOMIC_RELAXED);
+      if (d >= OR_G_DIG) break;
+      const uint64_t s = g->bs[d], e = g->bs[d + 1];
+      if (e - s <= 1) {
+        if (e > s) g->a[s] = g->b[s];
+        continue;
+      }
+      memset(sc, 0, sizeof(sc));
+      for (uint64_t i = s; i < e; ++i) sc[(g->b[i].k >> (64u - 2u * OR_G_BITS)) & (OR_G_DIG - 1u)]++;
+      uint64_t run = s;
+      for (uint32_t x = 0; x < OR_G_DIG; ++x) {
+        const uint64_t c = sc[x];
+        sc[x] = run;
+        run += c;
+      }
+      for (uint64_t i = s; i < e; ++i)
+        g->a[sc[(g->b[i].k >> (64u - 2u * OR_G_BITS)) & (OR_G_DIG - 1u)]++] = g->b[i];
+      /* sub-bucket x now ends at sc[x]: stable insertion sort by k */
+      uint64_t ss = s;
+      for (uint32_t x = 0; x < OR_G_DIG; ++x) {
+        const uint64_t se = sc[x];
+        for (uint64_t i = ss + 1; i < se; ++i) {
+          const or_pair v = g->a[i];
+          uint64_t q = i;
+          while (q > ss && g->a[q - 1].k > v.k) {
+            g->a[q] = g->a[q - 1];
+            --q;
+          }
+          g->a[q] = v;
+        }
+        ss = se;
+      }
+    }
+  } else if (g->phase == 3) { /* order, trace starts per chunk */
+    uint64_t c = 0;
+    for (uint64_t i = lo; i < hi; ++i) {
+      g->order[i] = g->a[i].i;
+      c += (i == 0 || g->a[i].k != g->a[i - 1].k) ? 1u : 0u;
+    }
+    g->chg[t] = c;
+  } else { /* trace_ptr */
+    uint64_t w = g->chg[t];
+    for (uint64_t i = lo; i < hi; ++i)
+      if (i == 0 || g->a[i].k != g->a[i - 1].k) g->tptr[w++] = i;
+  }
+  return NULL;
+}
+
+static int or_run(or_group* g, int phase) {
+  pthread_t th[256];
+  or_job jobs[256];
+  g->phase = phase;
+  for (uint32_t t = 0; t < g->threads; ++t) {
+    jobs[t].g = g;
+    jobs[t].t = t;
+    if (pthread_create(&th[t], NULL, or_group_worker, &jobs[t]) != 0) {
+      for (uint32_t q = 0; q < t; ++q) pthread_join(th[q], NULL);
+      return -1;
+    }
+  }
+  for (uint32_t t = 0; t < g->threads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
+/* order[n], tptr[n + 1] (caller-sized); returns the trace count, or -1. */
+int64_t oracle_group_by_trace(const uint64_t* trace_hash, uint64_t n, uint32_t threads,
+                              uint64_t* order, uint64_t* tptr) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  if (n == 0) {
+    tptr[0] = 0;
+    return 0;
+  }
+  or_group g;
+  memset(&g, 0, sizeof(g));
+  g.h = trace_hash;
+  g.n = n;
+  g.threads = threads;
+  g.order = order;
+  g.tptr = tptr;
+  g.a = (or_pair*)malloc(n * sizeof(or_pair));
+  g.b = (or_pair*)malloc(n * sizeof(or_pair));
+  g.cnt = (uint64_t*)calloc((size_t)threads * OR_G_DIG, sizeof(uint64_t));
+  g.bs = (uint64_t*)malloc((OR_G_DIG + 1) * sizeof(uint64_t));
+  g.chg = (uint64_t*)malloc((threads + 1) * sizeof(uint64_t));
+  int64_t rc = -1;
+  if (g.a && g.b && g.cnt && g.bs && g.chg && or_run(&g, 0) == 0) {
+    uint64_t run = 0;
+    for (uint32_t d = 0; d < OR_G_DIG; ++d) { /* digit-major, thread-minor: stable */
+      g.bs[d] = run;
+      for (uint32_t t = 0; t < threads; ++t) {
+        const uint64_t c = g.cnt[(uint64_t)t * OR_G_DIG + d];
+        g.cnt[(uint64_t)t * OR_G_DIG + d] = run;
+        run += c;
+      }
+    }
+    g.bs[OR_G_DIG] = run;
+    if (or_run(&g, 1) == 0 && or_run(&g, 2) == 0 && or_run(&g, 3) == 0) {
+      uint64_t tot = 0;
+      for (uint32_t t = 0; t < threads; ++t) {
+        const uint64_t c = g.chg[t];
+        g.chg[t] = tot;
+        tot += c;
+      }
+      if (or_run(&g, 4) == 0) {
+        tptr[tot] = n;
+        rc = (int64_t)tot;
+      }
+    }
+  }
+  free(g.a);
+  free(g.b);
+  free(g.cnt);
+  free(g.bs);
+  free(g.chg);
+  return rc;
+}
+
+/* The span columns taken in `order` (rows [lo, hi) of the output), for one
+ * thread's share of the gather after oracle_group_by_trace. */
+void oracle_take_spans(const uint64_t* order, uint64_t lo, uint64_t hi, const uint64_t* h,
+                       const uint64_t* sid, const uint64_t* pid, const uint16_t* svc,
+                       const uint16_t* flags, const uint32_t* dur, uint64_t* oh, uint64_t* osid,
+                       uint64_t* opid, uint16_t* osvc, uint16_t* oflags, uint32_t* odur) {
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t s = order[i];
+    oh[i] = h[s];
+    osid[i] = sid[s];
+    opid[i] = pid[s];
+    osvc[i] = svc[s];
+    oflags[i] = flags[s];
+    odur[i] = dur[s];
+  }
+}

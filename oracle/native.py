@@ -37,6 +37,10 @@ def lib():
                                        C.c_uint32, C.c_double, C.c_void_p]
         _lib.oracle_trace_structure.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_uint64,
                                                                     C.c_uint32] + [C.c_void_p] * 6
+        _lib.oracle_group_by_trace.restype = C.c_int64
+        _lib.oracle_group_by_trace.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
+                                               C.c_void_p]
+        _lib.oracle_take_spans.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64] + [C.c_void_p] * 12
         _lib.oracle_pagerank.restype = C.c_uint32
         _lib.oracle_pagerank.argtypes = [C.c_void_p] * 3 + [C.c_uint32, C.c_void_p, C.c_double,
                                                             C.c_uint32, C.c_double, C.c_void_p]
@@ -151,3 +155,18 @@ def pagerank(row_ptr, col, w, p, alpha=0.85, iters=100, tol=1e-10):
         col, w = np.zeros(1, np.uint32), np.zeros(1, np.float32)
     it = lib().oracle_pagerank(_p(row_ptr), _p(col), _p(w), N, _p(p), alpha, iters, tol, _p(x))
     return x, it
+
+
+def group_by_trace(trace_hash: np.ndarray, threads: int = 1) -> tuple[np.ndarray, np.ndarray]:
+    """(order, trace_ptr) of oracle_group_by_trace: spans taken in `order` are
+    grouped (traces by mix64(trace_hash) ascending, spans of a trace in
+    arrival order) — spec.group_by_trace as a parallel C radix partition."""
+    h = np.ascontiguousarray(trace_hash, np.uint64)
+    n = h.shape[0]
+    order = np.empty(n, np.uint64)
+    tptr = np.empty(n + 1, np.uint64)
+    nt = lib().oracle_group_by_trace(_p(h), n, threads, _p(order), _p(tptr))
+    if nt < 0:
+        raise MemoryError("oracle_group_by_trace failed")
+    return order.astype(np.int64), tptr[:nt + 1].copy()
+

@@ -159,3 +159,48 @@ def test_rendezvous_survives_stray_clients(tmp_path):
     s.close()
     assert not errs, errs
     assert res == {0: 3.0, 1: 3.0}
+
+
+def test_silent_peer_times_out(tmp_path):
+    """A rank that stops answering without closing its socket (stuck in a GPU
+    call, a lost host) makes the others raise TimeoutError after the
+    collective timeout instead of waiting forever; keepalive is on every
+    peer link (threads of one process here; rank 1 forms the group, then
+    never enters the barrier)."""
+    import socket
+    import threading
+
+    from anomod import dist
+
+    key, errs, formed, release = f"silent{os.getpid()}", {}, threading.Event(), threading.Event()
+    groups = {}
+
+    def rank(r):
+        try:
+            g = dist.HostGroup(r, 2, key=key, rdzv_dir=str(tmp_path), timeout_s=30,
+                               coll_timeout_s=1.5)
+            groups[r] = g
+            if r == 1:
+                formed.set()
+                release.wait(30)  # silent: socket open, no collective
+            else:
+                formed.wait(30)
+                g.barrier()
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    ts[0].join(30)
+    release.set()
+    ts[1].join(30)
+    assert isinstance(errs.get(0), TimeoutError), errs
+    assert 1 not in errs
+    link = groups[0]._peers[0]
+    assert link.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
+    assert groups[0].coll_timeout_s == 1.5
+    for g in groups.values():
+        g.close()
+    assert dist.HostGroup(0, 1).coll_timeout_s == 10 * 300.0 or os.environ.get(
+        "ANOMOD_HOSTGROUP_TIMEOUT_S") or os.environ.get("ANOMOD_RCCL_TIMEOUT_S")

@@ -212,17 +212,24 @@ def test_shards_sum_to_whole(ctx):
 
 @pytest.mark.slow
 def test_large_synthetic_full_parity(ctx):
-    """~72 M spans generated in HBM: full oracle parity + conservation."""
+    """~72 M spans generated in HBM: full oracle parity + conservation of the
+    first call (auto form) and of the second — the instantiation bench.py's
+    headline times — histogram and quantiles included (the nearest-rank rule
+    of monitor_http_responses.py:183-190 on the merged histogram)."""
     spec = anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=500)
     dev = ctx.generate(spec, 1 << 23)
-    t1 = ctx.edge_aggregate(dev)
+    assert dev.unique_ids and dev.hints == (-1, -1)
+    t1 = ctx.edge_aggregate(dev)  # first call: the auto form (pair + resume hand-off)
+    # the call the bench times runs edge_agg_kernel<lds_hist,lds_stats,unique>
+    # (the bidirectional scan of a collector-order unique-id set, pair form)
+    assert dev.hints == (1, 0)
     t2 = ctx.edge_aggregate(dev)
-    for k in FIELDS:
-        np.testing.assert_array_equal(getattr(t1, k), getattr(t2, k))  # deterministic
     assert int(t1.count.sum()) == dev.n_spans
     np.testing.assert_array_equal(t1.hist.sum(axis=1), t1.count)
     host = dev.download()
-    assert_table_equal(t1, native.edge_aggregate(host))
+    ref = native.edge_aggregate(host)
+    assert_table_equal(t1, ref)
+    assert_table_equal(t2, ref)  # hist, p50 / p99 included
 
 
 @pytest.mark.parametrize("cap", [1000, 4096])

@@ -297,7 +297,7 @@ def test_ungrouped_fused_equals_unfused(ctx, env_knob, monkeypatch, S, max_len, 
     dev = ctx.upload_ungrouped(flat)
     monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "1")
     fused = ctx.edge_aggregate(dev)
-    assert ctx.group_info()["path"] == "join"
+    assert ctx.group_info()["path"] == ("join" if join == "1" else "fused-sort")
     assert_table_equal(fused, ref)
     monkeypatch.setenv("ANOMOD_UNGROUPED_FUSED", "0")
     assert_table_equal(ctx.edge_aggregate(dev), ref)
@@ -361,4 +361,59 @@ def test_ungrouped_join_shared_ids_and_big_buckets(ctx):
     got = ctx.edge_aggregate(dev)
     assert ctx.group_info()["path"] == "join"
     assert_table_equal(got, native.edge_aggregate(_oracle_grouped(flat)))
+    dev.free()
+
+
+@pytest.mark.parametrize("pack,stable_b", [("1", "0"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("S,max_len,dup", [(12, 24, 0.05), (46, 60, 0.02)])
+def test_ungrouped_join_two_levels(ctx, env_knob, S, max_len, dup, pack, stable_b):
+    """The join path through BOTH scatter levels (ANOMOD_BUCKET_AVG=64 makes a
+    ~1 M-span set use T >= 12 bucket bits): level B's non-stable scatter
+    (LDS-atomic ranks, the default for the join) with repeated (trace, id)
+    resolved by level-A position, against the stable scatter; the packed key
+    word (service in the bucket's shared key bits) against the separate
+    service array; buckets over 2 048 spans in the big join kernel.  Every
+    table equals the oracle's on the stably grouped spans."""
+    env_knob("ANOMOD_BUCKET_AVG", "64")
+    env_knob("ANOMOD_JOIN_PACK", pack)
+    env_knob("ANOMOD_BK_STABLE_B", stable_b)
+    rng = np.random.default_rng(S * 7 + int(dup * 100))
+    parts = [_random_spanset(rng, S, 60000, max_len, dup=dup)]
+    # a few traces of 1 000-3 000 spans: buckets over 2 048 spans (big kernel)
+    parts.append(_random_spanset(rng, S, 0, 0, dup=dup, lens=[3000, 1500, 1000, 2500]))
+    sp = _with_trace_hashes(anomod.SpanSet.concat(parts), rng)
+    flat = _interleave(sp, rng, "time")
+    ref = native.edge_aggregate(_oracle_grouped(flat))
+    dev = ctx.upload_ungrouped(flat)
+    for _ in range(2):
+        got = ctx.edge_aggregate(dev)
+        info = ctx.group_info()
+        assert info["path"] == "join" and info["levels"] == 2 and info["bits"] >= 12, info
+        assert_table_equal(got, ref)
+    dev.free()
+
+
+def test_ungrouped_join_duplicates_across_level_b_tiles(ctx, env_knob):
+    """Repeated (trace, id) pairs whose copies are far apart in arrival order
+    (other traces' spans between them, so they sit in different level-B tiles
+    and land in a bucket in any order once level B is not stable): the
+    parent of every child is its trace's FIRST span with that id — the copies
+    carry different services, so a wrong pick changes the edge table."""
+    env_knob("ANOMOD_BUCKET_AVG", "64")
+    rng = np.random.default_rng(4242)
+    S, nt, L = 12, 30000, 12
+    sp = _random_spanset(rng, S, nt, 0, dup=0.0, lens=np.full(nt, L))
+    sid = sp.span_id.reshape(nt, L)
+    pid = sp.parent_span_id.reshape(nt, L)
+    sid[:, 6] = sid[:, 1]  # the id of span 1 again at span 6 ...
+    pid[:, 7:] = sid[:, 1:2]  # ... and spans 7.. reference it
+    svc = sp.svc.reshape(nt, L)
+    svc[:, 1] = 3
+    svc[:, 6] = 9  # first match -> service 3, a wrong pick -> 9
+    sp = _with_trace_hashes(sp, rng)
+    flat = _interleave(sp, rng, "random")
+    ref = native.edge_aggregate(_oracle_grouped(flat))
+    dev = ctx.upload_ungrouped(flat)
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    assert ctx.group_info()["levels"] == 2
     dev.free()

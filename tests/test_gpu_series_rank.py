@@ -289,12 +289,17 @@ def test_pagerank_batch_equals_single_solves(ctx, K):
     g.free()
 
 
-@pytest.mark.parametrize("K", [2, 5, 8])
-def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K):
+@pytest.mark.parametrize("K,bsub", [(2, None), (5, None), (8, None), (8, "2"), (16, None),
+                                    (16, "1")])
+def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K, bsub):
     """The persistent batch (one launch, grid barrier, vector ring or the
     two-buffer form) == the per-launch batch loop (ANOMOD_PPR_MODE=1), bit
     for bit, in fixed-iteration and tolerance mode (per-vector freezing);
-    a barrier timeout (ANOMOD_PPR_SPIN=0) reruns per launch, same bits."""
+    a barrier timeout (ANOMOD_PPR_SPIN=0) reruns per launch, same bits.
+    bsub: 256-row blocks per persistent workgroup (ANOMOD_PPR_BSUB; K = 16
+    defaults to 2)."""
+    if bsub:
+        monkeypatch.setenv("ANOMOD_PPR_BSUB", bsub)
     g = anomod.DeviceGraph(ctx, synthetic=(40000, 9, 12))
     rng = np.random.default_rng(K + 40)
     P = rng.random((K, g.N))
@@ -319,13 +324,23 @@ def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K):
     g.free()
 
 
-def test_pagerank_batch_bench_config_is_persistent(ctx):
-    """The bench's batch (config 5: N = 10^5, 8 vectors) fits one resident
-    grid (391 workgroups of 256 threads, three per CU on 256 CUs), so it runs
-    as one persistent launch."""
+@pytest.mark.parametrize("K", [8, 16])
+def test_pagerank_batch_bench_config_is_persistent(ctx, K):
+    """The bench's batches (config 5: N = 10^5, 8 and 16 vectors) fit one
+    resident grid — K = 8: 391 workgroups of 256 threads, three per CU; K =
+    16: 196 workgroups of two 256-row blocks — so each runs as one
+    persistent launch, equal to its per-launch solve."""
     g = anomod.DeviceGraph(ctx, synthetic=(100000, 10, 11))
-    X, d = g.pagerank_batch(np.random.default_rng(3).random((8, g.N)), iters=5)
+    P = np.random.default_rng(3).random((K, g.N))
+    X, d = g.pagerank_batch(P, iters=5)
     assert d == 5 and g.last_solve()[0] == "persistent"
+    import os
+    os.environ["ANOMOD_PPR_MODE"] = "1"
+    try:
+        Xr, _ = g.pagerank_batch(P, iters=5)
+    finally:
+        del os.environ["ANOMOD_PPR_MODE"]
+    np.testing.assert_array_equal(X, Xr)
     g.free()
 
 
