@@ -1422,12 +1422,14 @@ __global__ __launch_bounds__(kSmallW, ANOMOD_BK_PIPE_MINB) void bk_bucket_pipe_k
 // workgroups share a CU (the r04 form, 26 B per span, fit three).
 constexpr uint64_t kKeyLow = (1ull << 52) - 1ull;  // the k bits a PACK key word compares
 
-template <int W, int PER, bool PACK>
+template <int W, int PER, bool PACK, bool T16 = true>
 struct JoinGeom {
   static constexpr int kCap = W * PER;
-  static constexpr uint32_t kSlots = 2u * (uint32_t)kCap;  // u16 slots, two per word
-  static constexpr size_t kOffSid = 8ull * kCap, kOffTab = 16ull * kCap, kOffSvc = 20ull * kCap;
-  static constexpr size_t kBytes = PACK ? 20ull * kCap : 22ull * kCap;
+  static constexpr uint32_t kSlots = 2u * (uint32_t)kCap;  // load <= 1/2
+  static constexpr size_t kTabBytes = T16 ? 4ull * kCap : 8ull * kCap;  // u16 (two per word) / u32
+  static constexpr size_t kOffSid = 8ull * kCap, kOffTab = 16ull * kCap;
+  static constexpr size_t kOffSvc = kOffTab + kTabBytes;
+  static constexpr size_t kBytes = kOffSvc + (PACK ? 0ull : 2ull * kCap);
   static_assert((kSlots & (kSlots - 1u)) == 0u, "join table size");
   static_assert(kCap <= 65535, "u16 slots hold arrival + 1");
 };
@@ -1436,14 +1438,18 @@ __device__ __forceinline__ uint32_t join_slot(uint64_t k, uint64_t id, uint32_t 
   return (uint32_t)(mix64(k ^ (id * 0x9E3779B97F4A7C15ull)) >> 32) & (slots - 1u);
 }
 
+template <bool T16>
 __device__ __forceinline__ uint32_t slot_get(const uint32_t* tab, uint32_t s) {
+  if constexpr (!T16) return tab[s];
   return (tab[s >> 1] >> ((s & 1u) * 16u)) & 0xFFFFu;
 }
 
 // Compare-and-swap of u16 slot s (a 32-bit CAS on its word, retried while only
 // the other half changes): the slot's value before, == expect when swapped.
+template <bool T16>
 __device__ __forceinline__ uint32_t slot_cas(uint32_t* tab, uint32_t s, uint32_t expect,
                                              uint32_t desired) {
+  if constexpr (!T16) return atomicCAS(&tab[s], expect, desired);
   uint32_t* wp = &tab[s >> 1];
   const uint32_t sh = (s & 1u) * 16u, mask = 0xFFFFu << sh;
   uint32_t w = (expect << sh) | (*wp & ~mask);
@@ -1459,11 +1465,11 @@ __device__ __forceinline__ uint32_t slot_cas(uint32_t* tab, uint32_t s, uint32_t
 // One bucket [a0, a0 + m) of the level-B pairs `pin` joined in LDS; every
 // thread of the workgroup calls it.  The records come from `rec` by the pairs'
 // level-A positions.
-template <int W, int PER, bool PACK>
+template <int W, int PER, bool PACK, bool T16 = true>
 __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uint32_t m,
                                             const uint64_t* __restrict__ pin,
                                             const GRec* __restrict__ rec, EdgeOut eo) {
-  using G = JoinGeom<W, PER, PACK>;
+  using G = JoinGeom<W, PER, PACK, T16>;
   constexpr uint32_t kSlots = G::kSlots;
   uint64_t* lkx = reinterpret_cast<uint64_t*>(lds);
   uint64_t* lsid = reinterpret_cast<uint64_t*>(lds + G::kOffSid);
@@ -1485,7 +1491,7 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
     ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
     rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
   }
-  for (uint32_t i = tid; i < kSlots / 8u; i += W)
+  for (uint32_t i = tid; i < (uint32_t)(G::kTabBytes / 16u); i += W)
     reinterpret_cast<uint4*>(tab)[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -1509,7 +1515,7 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
   for (int j = 0; j < PER; ++j)
     sl[j] = v[j] ? join_slot(lkx[p[j]] & (PACK ? kKeyLow : ~0ull), lsid[p[j]], kSlots) : 0u;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) cur[j] = v[j] ? slot_cas(tab, sl[j], 0u, p[j] + 1u) : 0u;
+  for (int j = 0; j < PER; ++j) cur[j] = v[j] ? slot_cas<T16>(tab, sl[j], 0u, p[j] + 1u) : 0u;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     if (cur[j] == 0u) continue;
@@ -1521,14 +1527,14 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
         // a repeated (trace, id): the smallest level-A position keeps the slot
         const uint32_t mine = (uint32_t)pin[a0 + p[j]];
         while ((uint32_t)pin[a0 + q] > mine) {
-          const uint32_t old = slot_cas(tab, s, q + 1u, p[j] + 1u);
+          const uint32_t old = slot_cas<T16>(tab, s, q + 1u, p[j] + 1u);
           if (old == q + 1u) break;
           q = old - 1u;  // another copy took it first: compare with that one
         }
         break;
       }
       s = (s + 1u) & (kSlots - 1u);
-      c = slot_cas(tab, s, 0u, p[j] + 1u);
+      c = slot_cas<T16>(tab, s, 0u, p[j] + 1u);
       if (c == 0u) break;
     }
   }
@@ -1541,7 +1547,7 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
   for (int j = 0; j < PER; ++j) {
     pid[j] = ((uint64_t)rb[j].y << 32) | rb[j].x;
     sl[j] = v[j] ? join_slot(lkx[p[j]] & (PACK ? kKeyLow : ~0ull), pid[j], kSlots) : 0u;
-    e[j] = v[j] && pid[j] != 0ull ? slot_get(tab, sl[j]) : 0u;
+    e[j] = v[j] && pid[j] != 0ull ? slot_get<T16>(tab, sl[j]) : 0u;
   }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -1554,7 +1560,7 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
     e[j] = 0u;
     while (true) {
       s = (s + 1u) & (kSlots - 1u);
-      const uint32_t c = slot_get(tab, s);
+      const uint32_t c = slot_get<T16>(tab, s);
       if (c == 0u) break;
       if (same_trace(lkx[c - 1u], kj) && lsid[c - 1u] == pid[j]) {
         e[j] = c;
@@ -1583,13 +1589,13 @@ constexpr int join_big_per(bool pack) { return pack ? 8 : 4; }  // 8 192 / 4 096
 
 // One workgroup per bucket; a bucket over 2 048 spans is listed for the big
 // kernel (a list overflow: the unfused path).
-template <bool PACK, int MINW = PACK ? ANOMOD_JOIN_MINW : 6>
+template <bool PACK, int MINW = PACK ? ANOMOD_JOIN_MINW : 6, bool T16 = true>
 __global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
     unsigned long long* __restrict__ over_n, uint32_t over_cap,
     unsigned long long* __restrict__ too_big) {
-  using G = JoinGeom<kJoinW, kJoinPer, PACK>;
+  using G = JoinGeom<kJoinW, kJoinPer, PACK, T16>;
   __shared__ __attribute__((aligned(16))) unsigned char lds[G::kBytes];
   const uint32_t c = blockIdx.x;
   const uint32_t a0 = bstart[c], m = bstart[c + 1] - a0;
@@ -1602,7 +1608,7 @@ __global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     return;
   }
   if (m == 0) return;
-  join_bucket<kJoinW, kJoinPer, PACK>(lds, a0, m, pin, rec, eo);
+  join_bucket<kJoinW, kJoinPer, PACK, T16>(lds, a0, m, pin, rec, eo);
 }
 
 // The listed buckets, one workgroup each in turn; one over this kernel's
@@ -1935,7 +1941,11 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       const unsigned big_grid = (unsigned)std::max(ctx->num_cus, 1);
       if (pack) {
         // ANOMOD_JOIN_W6=1: the 3-workgroups-per-CU form (no spills; A/B)
-        auto fn = env_int("ANOMOD_JOIN_W6", 0) ? bk_join_kernel<true, 6> : bk_join_kernel<true>;
+        // (A/B: 1 = three workgroups per CU, u16 slots; 2 = the same with u32
+        // slots, 48 KiB)
+        const int jv = env_int("ANOMOD_JOIN_W6", 0);
+        auto fn = jv == 2 ? bk_join_kernel<true, 6, false>
+                  : jv == 1 ? bk_join_kernel<true, 6> : bk_join_kernel<true>;
         hipLaunchKernelGGL(fn, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
                            recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);

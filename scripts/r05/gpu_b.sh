@@ -8,7 +8,7 @@ O=gpurun_out/r5b
 mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
   > $O/gpu_tests.log 2>&1 || exit 1
-AB_VAR=ANOMOD_JOIN_W6 AB_VALS=0,1 timeout -k 10 240 python3 -u scripts/time_env_ab.py 27 3 \
+AB_VAR=ANOMOD_JOIN_W6 AB_VALS=0,1,2 timeout -k 10 240 python3 -u scripts/time_env_ab.py 27 3 \
   > $O/ab_w6.log 2>&1 || exit 2
 timeout -k 10 240 python3 -u scripts/r05/time_form_ab.py 27 3 SN > $O/form_sn.log 2>&1 || exit 3
 timeout -k 10 240 python3 -u scripts/r05/time_form_ab.py 27 3 SN 1 > $O/form_sn_shuf.log 2>&1 || exit 4
