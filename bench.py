@@ -457,16 +457,22 @@ def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
             "cold": cold}
 
 
-def load_traffic(n_spans: int) -> float | None:
-    """HBM bytes per launch from the committed PMC profile of this workload."""
+def load_traffic(n_spans: int) -> tuple[float | None, dict | None]:
+    """HBM bytes per launch from the committed PMC profile of this workload,
+    and where they came from (file, round, the commit the profiled library was
+    built from, kernel, correction): the value is not measured in this run."""
     p = ROOT / "profiles" / "edge_agg_pmc.json"
     try:
         d = json.loads(p.read_text())
         if int(d["n_spans"]) == n_spans:
-            return float(d["hbm_bytes_per_launch"])
+            src = {"file": str(p.relative_to(ROOT)), "round": d.get("round"),
+                   "commit": d.get("commit"), "kernel": d.get("kernel"),
+                   "correction": d.get("correction"),
+                   "measured_in_this_run": False}
+            return float(d["hbm_bytes_per_launch"]), src
     except Exception:
         pass
-    return None
+    return None, None
 
 
 def main() -> int:
@@ -567,7 +573,7 @@ def main() -> int:
     k_ms = float(np.mean(kernel_ms))
     bytes_launch = algorithmic_bytes(spans.n_spans, spans.n_traces)
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
-    traffic = load_traffic(spans.n_spans)
+    traffic, traffic_src = load_traffic(spans.n_spans)
     result = {
         "metric": METRIC,
         "value": total_spans * args.steps / el,
@@ -592,7 +598,7 @@ def main() -> int:
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "edge_agg_kernel<lds_hist,lds_stats>", "kernel_ms": k_ms,
             "bytes_per_launch": bytes_launch,
         },
