@@ -628,15 +628,21 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   const size_t tcnt_words = std::max<size_t>(tiles * kDig, ws->tile_cap * 2048);
   ws->tcnt_words = tcnt_words;
   const size_t bsum_words = (tiles / kTScanRows + 2) * 2048;
+  // Bytes per span: 64 (two record buffers) + 16 (two pair buffers; the LSD
+  // path's 2-B digits live in the second, which only the bucket path uses)
+  // + 8 (trace_ptr) + ~2 (tile counts, lists) ~= 90 B, plus the input set's
+  // 32 B: 1.15e9 spans take ~104 + 37 GB of the 288 GB, and n is bounded by
+  // the u32 positions (< 2^32) before HBM runs out.
+  static_assert(8 >= 2 + 1, "the digits fit a pair buffer");
   const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
                           ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
-                          ws->list_cap * 8, tcnt_words * 4, bsum_words * 4, 2 * cap + 32,
+                          ws->list_cap * 8, tcnt_words * 4, bsum_words * 4,
                           (ws->bucket_cap + 1) * 4, 2049 * 4, 2049 * 4, ws->tile_cap * 4,
                           (ws->bucket_cap + 1) * 4, ws->bucket_cap * 4,
-                          (ws->bucket_cap / 4096 + 2) * 4, cap * 8, cap * 8};
+                          (ws->bucket_cap / 4096 + 2) * 4, cap * 8, cap * 8 + 32};
   void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
                    (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
-                   (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum, (void**)&ws->dig,
+                   (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum,
                    (void**)&ws->bstart, (void**)&ws->bsA, (void**)&ws->btile, (void**)&ws->tmap,
                    (void**)&ws->dcnt, (void**)&ws->over, (void**)&ws->part,
                    (void**)&ws->pairs[0], (void**)&ws->pairs[1]};
@@ -655,6 +661,10 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
       *ptrs[i] = static_cast<char*>(ws->block) + off;
       off += (sizes[i] + kAlign - 1) / kAlign * kAlign;
     }
+    // the LSD path's next-pass digits (2 B per span + slack) share the
+    // level-B pair buffer: the two paths never hold both at once (the LSD
+    // path runs alone, or after the bucket path handed the set back)
+    ws->dig = reinterpret_cast<uint8_t*>(ws->pairs[1]);
   } else {
     ws->block = nullptr;
   }

@@ -315,6 +315,55 @@ def _evict_page_cache(paths) -> int:
     return done
 
 
+def _fs_type(path: str) -> str:
+    """File-system type of the mount holding path (/proc/mounts, longest prefix)."""
+    best, fstype = "", "unknown"
+    try:
+        real = os.path.realpath(path)
+        for line in Path("/proc/mounts").read_text().splitlines():
+            f = line.split()
+            if len(f) >= 3 and (real == f[1] or real.startswith(f[1].rstrip("/") + "/")) \
+                    and len(f[1]) > len(best):
+                best, fstype = f[1], f[2]
+    except OSError:
+        pass
+    return fstype
+
+
+def _resident_pages(paths) -> tuple[int, int]:
+    """(resident, total) page-cache pages of these files, by mincore(2) over a
+    read-only mapping of each."""
+    import ctypes
+    import mmap
+
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                          ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    libc.mincore.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    page = mmap.PAGESIZE
+    res = tot = 0
+    for p in paths:
+        size = os.path.getsize(p)
+        if size == 0:
+            continue
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            addr = libc.mmap(None, size, mmap.PROT_READ, mmap.MAP_SHARED, fd, 0)
+            if addr in (None, ctypes.c_void_p(-1).value):
+                continue
+            n = (size + page - 1) // page
+            vec = (ctypes.c_ubyte * n)()
+            if libc.mincore(addr, size, vec) == 0:
+                res += sum(b & 1 for b in vec)
+                tot += n
+            libc.munmap(addr, size)
+        finally:
+            os.close(fd)
+    return res, tot
+
+
 def tt_config2_files(ctx, staged: list) -> dict:
     """BASELINE config 2 from files: each experiment's trace payload and long
     metric CSV go through load_experiment (native decoders) -> features() ->
@@ -344,8 +393,14 @@ def tt_config2_files(ctx, staged: list) -> dict:
     # cache first (a collector's fresh files would be in it; a dataset read
     # back later would not)
     cold_dec, cold_tot, evicted = 0.0, 0.0, 0
+    res_pages = tot_pages = 0
+    fstype = _fs_type(str(staged[0][0])) if staged else "unknown"
     for d, mc, fault in staged:
-        evicted += _evict_page_cache([str(x) for x in Path(d).rglob("*") if x.is_file()] + [mc])
+        files = [str(x) for x in Path(d).rglob("*") if x.is_file()] + [mc]
+        evicted += _evict_page_cache(files)
+        r, t = _resident_pages(files)  # what the eviction actually left in memory
+        res_pages += r
+        tot_pages += t
         a = time.perf_counter()
         e = one(d, mc)
         cold_dec += time.perf_counter() - a
@@ -360,10 +415,13 @@ def tt_config2_files(ctx, staged: list) -> dict:
             "top3_hit_rate": float(np.mean(hits)),
             "cold_files": {"ms_per_experiment": cold_tot / len(staged) * 1e3,
                            "decode_ms_per_experiment": cold_dec / len(staged) * 1e3,
-                           "files_evicted": evicted,
+                           "files_fadvised": evicted, "staging_fs": fstype,
+                           "resident_frac_after_evict": res_pages / tot_pages if tot_pages else None,
+                           "valid": bool(tot_pages) and res_pages / tot_pages < 0.05,
                            "what": "load_experiment + features per experiment after "
-                                   "fsync + posix_fadvise(DONTNEED) on its files (best effort: "
-                                   "no effect on a tmpfs)"},
+                                   "fsync + posix_fadvise(DONTNEED) on its files; valid only when "
+                                   "mincore shows < 5 % of their pages still resident (a tmpfs "
+                                   "keeps them all: then this is a warm number)"},
             "note": "files in the dataset layout (collector payload JSON indent=2 + long metric "
                     "CSV) -> load_experiment (native decoders) -> features -> rank"}
 
