@@ -1579,17 +1579,16 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
 }
 
 constexpr int kJoinW = 512, kJoinPer = 4;           // 2 048 spans per bucket
-// Waves per SIMD the small join kernel's registers must allow: 8 = four
-// workgroups per CU (64 VGPRs, a few dwords spilled); 6 = three (72 VGPRs).
-#ifndef ANOMOD_JOIN_MINW
-#define ANOMOD_JOIN_MINW 8
-#endif
+
 constexpr int kJoinBigW = 1024;                     // buckets over 2 048 spans
 constexpr int join_big_per(bool pack) { return pack ? 8 : 4; }  // 8 192 / 4 096 spans
 
 // One workgroup per bucket; a bucket over 2 048 spans is listed for the big
 // kernel (a list overflow: the unfused path).
-template <bool PACK, int MINW = PACK ? ANOMOD_JOIN_MINW : 6, bool T16 = true>
+// MINW: waves per SIMD the registers must allow (6 = three 512-thread
+// workgroups per CU; 8 = four, 64 VGPRs with 28 B per lane spilled); T16: u16
+// table slots (PACK at 2 048 spans: 40 KiB, else 48).
+template <bool PACK, int MINW = 6, bool T16 = !PACK>
 __global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
@@ -1941,11 +1940,13 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       const unsigned big_grid = (unsigned)std::max(ctx->num_cus, 1);
       if (pack) {
         // ANOMOD_JOIN_W6=1: the 3-workgroups-per-CU form (no spills; A/B)
-        // (A/B: 1 = three workgroups per CU, u16 slots; 2 = the same with u32
-        // slots, 48 KiB)
-        const int jv = env_int("ANOMOD_JOIN_W6", 0);
-        auto fn = jv == 2 ? bk_join_kernel<true, 6, false>
-                  : jv == 1 ? bk_join_kernel<true, 6> : bk_join_kernel<true>;
+        // u32 slots, three workgroups per CU (48 KiB): 48.0 ms grouping at
+        // 2^27 SN traces, against 48.3 with u16 slots (40 KiB) at three and
+        // 49.8 at four per CU, which spills (gpurun_out/r5b/ab_w6.log);
+        // ANOMOD_JOIN_FORM = 1 / 2 runs those two (A/B)
+        const int jv = env_int("ANOMOD_JOIN_FORM", 0);
+        auto fn = jv == 2 ? bk_join_kernel<true, 8, true>
+                  : jv == 1 ? bk_join_kernel<true, 6, true> : bk_join_kernel<true, 6, false>;
         hipLaunchKernelGGL(fn, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
                            recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
@@ -1953,7 +1954,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
                            recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
       } else {
-        hipLaunchKernelGGL(bk_join_kernel<false>, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
+        hipLaunchKernelGGL((bk_join_kernel<false, 6, true>), dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
                            recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
         hipLaunchKernelGGL(bk_join_big_kernel<false>, dim3(big_grid), dim3(kJoinBigW), 0, st, pin,

@@ -125,7 +125,8 @@ enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2, kStWide = 3 };
 constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
 constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2;  // u8 trace-start flags [kStage]
-constexpr int kWBytes = kWFlag + kStage;
+constexpr int kWAuto = kWFlag + kStage;           // u64: kModeAuto, first trace of the chunk
+constexpr int kWBytes = kWAuto + 16;
 constexpr int kLdsBytes = kOffWave + kWavesPerWG * kWBytes;
 static_assert(kWBytes % 16 == 0, "wave staging must stay 16-B aligned");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
@@ -149,6 +150,8 @@ struct Table {
   unsigned long long* left;  // kModeAuto: [2 j], [2 j + 1] = trace range j a stopped wave left
   unsigned long long* nleft; // [0] ranges left, [1] resume ticket
   uint32_t mode;             // LaunchMode
+  uint32_t occupancy;        // compact form: report the fullest workgroup's used slots
+                             // (tab.ovf[1], atomic max) at the flush
 };
 
 struct Cols {
@@ -603,9 +606,18 @@ __device__ __forceinline__ void tables_flush(unsigned char* smem, uint32_t E, co
   if constexpr (HT == kHtCompact) {
     auto* hk = reinterpret_cast<uint32_t*>(smem + kOffHt);
     const uint32_t kmask = 0xFFFFFFFFu >> (32u - tab.kb);
+    uint32_t used = 0;
     for (uint32_t s = tid; s < kCmpSlots; s += kThreads) {
       const uint32_t w = hk[s];
+      used += w ? 1u : 0u;
       if (w >> tab.kb) atomicAdd(&tab.hist[(w & kmask) - 1u], (unsigned long long)(w >> tab.kb));
+    }
+    if (tab.occupancy) {  // the workgroup's used slots -> tab.ovf[1] (max over workgroups)
+      auto* ctl = reinterpret_cast<uint32_t*>(smem + kOffCtl);
+      for (int o = 32; o > 0; o >>= 1) used += __shfl_xor(used, o);
+      if ((tid & (kWave - 1)) == 0) atomicAdd(&ctl[1], used);
+      __syncthreads();
+      if (tid == 0) atomicMax(&tab.ovf[1], (unsigned long long)ctl[1]);
     }
   }
   if constexpr (ST == kStSlot) {
@@ -1372,19 +1384,25 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
     Chunk cur = make_chunk(t_begin, t_end, lane, lo, hi, kBigMin);
     Regs R;
     load_regs(col, cur, lane, R);
-    uint64_t t_cur = t_begin;
+    // kModeAuto: the first trace of the current chunk lives in the wave's LDS
+    // word, not a register (a register more spilled the auto form's loop: 16 /
+    // 48 B per lane, 12 % / 40 % slower than the pair form on SN / shuffled SN)
+    uint64_t* wt_cur = reinterpret_cast<uint64_t*>(wsm + kWAuto);
+    if (MODE == kModeAuto && lane == 0) *wt_cur = t_begin;
+    uint64_t t_cur = t_begin;  // (other modes: a register)
     uint64_t t_next = t_begin + (cur.k ? cur.k : 1u);
     load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
     while (true) {
       // A first aggregation (kModeAuto) whose pair table saturated: leave
-      // [t_cur, t_end) to the compact-form resume launch and stop.
+      // [first trace of the chunk, t_end) to the compact-form resume launch
+      // and stop.
       if (MODE == kModeAuto &&
           __builtin_amdgcn_readfirstlane(
               __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >=
               kSatFails) {
         if (lane == 0) {
           const unsigned long long j = atomicAdd(&tab.nleft[0], 1ull);
-          tab.left[2 * j] = t_cur;
+          tab.left[2 * j] = *wt_cur;
           tab.left[2 * j + 1] = t_end;
         }
         stopped = true;
@@ -1392,6 +1410,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       }
       const bool has_next = t_next < t_end;
       const uint64_t t_nxt = t_next;
+      if (MODE == kModeAuto && lane == 0 && has_next) wt_cur[1] = t_next;  // the next chunk's
       Chunk nxt{};
       Regs Rn;
       if (has_next) {
@@ -1401,13 +1420,19 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
         load_bounds(trace_ptr, t_next, t_end, lane, lo, hi);
       }
       if (cur.k == 0) {  // a trace longer than kStage: listed for edge_big_kernel
-        if (lane == 0) tab.big_list[atomicAdd(&tab.big[0], 1ull)] = tab.t_base + t_cur;
+        if (lane == 0)
+          tab.big_list[atomicAdd(&tab.big[0], 1ull)] =
+              tab.t_base + (MODE == kModeAuto ? *wt_cur : t_cur);
       } else {
         process_chunk<HT, ST, UNI, MODE == kModeWideScan>(smem, wsm, lane, cur, R, S, tab);
       }
       if (!has_next) break;
       cur = nxt;
-      t_cur = t_nxt;
+      if (MODE == kModeAuto) {
+        if (lane == 0) wt_cur[0] = wt_cur[1];
+      } else {
+        t_cur = t_nxt;
+      }
       R = Rn;
     }
   }
@@ -1458,17 +1483,7 @@ __global__ __launch_bounds__(kThreads) void edge_rec_kernel(const uint64_t* __re
                        ((x[j] >> 32) & 1ull) ? ANOMOD_FLAG_ERROR : 0u, tab);
   }
   __syncthreads();
-  tables_flush<HT, ST>(smem, E, tab, tid);
-  if constexpr (HT == kHtCompact) {
-    auto* ctl = reinterpret_cast<uint32_t*>(smem + kOffCtl);
-    const auto* hk = reinterpret_cast<const uint32_t*>(smem + kOffHt);
-    uint32_t used = 0;
-    for (uint32_t s = tid; s < kCmpSlots; s += kThreads) used += hk[s] ? 1u : 0u;
-    for (int o = 32; o > 0; o >>= 1) used += __shfl_xor(used, o);
-    if ((tid & (kWave - 1)) == 0) atomicAdd(&ctl[1], used);
-    __syncthreads();
-    if (tid == 0) atomicMax(&tab.ovf[1], (unsigned long long)ctl[1]);
-  }
+  tables_flush<HT, ST>(smem, E, tab, tid);  // (the caller sets tab.occupancy)
 }
 
 // Count + nearest-rank quantiles per edge from the merged histogram: one
@@ -1582,6 +1597,17 @@ using KernelFn1 = void (*)(const uint64_t*, uint64_t, uint32_t, Table);
 // The histogram form a set asks for: 0 pair, 1 compact, -1 unknown (pair with
 // the saturation hand-off to a compact resume launch) — its hint, or
 // ANOMOD_HIST_FORM = pair / compact / auto (tests force each).
+// ANOMOD_HIST_FORM=auto: a form-unknown set takes the r04 auto form (pair
+// table, saturated workgroups resumed compact) instead of the probe.
+bool auto_forced() {
+  const char* f = getenv("ANOMOD_HIST_FORM");
+  return f && !strcmp(f, "auto");
+}
+
+// The form probe of a first aggregation: spans it covers, workgroups it runs.
+constexpr uint64_t kFormProbeSpans = 1ull << 20;
+constexpr uint64_t kFormProbeGroups = 16;
+
 int hist_form_of(const anomod_spans* s) {
   const char* f = getenv("ANOMOD_HIST_FORM");
   if (f && !strcmp(f, "compact")) return 1;
@@ -1792,6 +1818,7 @@ Table table_at(anomod_ctx* ctx, const Layout& L, uint32_t E) {
   tab.nleft = reinterpret_cast<unsigned long long*>(base + L.off_nleft);
   tab.left = reinterpret_cast<unsigned long long*>(base + L.off_left);
   tab.mode = kModeNormal;
+  tab.occupancy = 0;
   tab.kb = 1;
   while (((uint64_t)E * kBins + 1) >> tab.kb) ++tab.kb;  // bits of the largest key
   return tab;
@@ -1903,7 +1930,9 @@ int edge_aggregate_records(anomod_ctx* ctx, const uint64_t* rec, uint64_t n, uin
                         &per_cu, reinterpret_cast<const void*>(fn), kThreads, 0));
     const uint64_t want = (n + (uint64_t)kThreads * kRecLoad - 1) / ((uint64_t)kThreads * kRecLoad);
     const uint64_t grid = std::min<uint64_t>((uint64_t)ctx->num_cus * (per_cu > 0 ? per_cu : 1), want);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, rec, n, E, tab);
+    Table tr = tab;
+    tr.occupancy = ht == kHtCompact;
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kThreads), 0, ctx->stream, rec, n, E, tr);
     ANOMOD_HIP(ctx, hipGetLastError());
   }
   if (int rc = stage_end(ctx, kStageEdgeAgg)) return rc;
@@ -1945,16 +1974,27 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   const uint32_t E = (S + ANOMOD_ROOT_ROWS) * S;
   const uint64_t big_cap = big_capacity(spans);
   // Histogram form: a set known to fit the pair table takes it, a set that
-  // overflowed it the compact form; a set not aggregated before starts in the
-  // pair form (kModeAuto) and any workgroup whose table saturates stops and
-  // leaves its remaining traces to a compact-form resume launch — so a first
-  // call costs about what the right form costs, never a probe-chain cliff.
-  const int form = hist_form_of(spans);
+  // overflowed it the compact form.  A set not aggregated before (form -1)
+  // is probed: its first ~2^20 spans (kFormProbeSpans) run in the compact
+  // form — no probe chain, nothing to saturate — on a few workgroups (each
+  // then sees ~64 k spans, near a full-size workgroup's key diversity) that
+  // report their largest slot occupancy; at most half the pair table's
+  // slots says pair.  The rest of the set runs in that form as an ordinary
+  // launch: the probe's counts are part of the table.  A set of at most
+  // 4 x 2^20 spans runs whole in the compact form and learns the same way.
+  // (r04 started form-unknown sets in a pair form that stopped saturated
+  // workgroups and resumed them compact: its loop spilled 16 / 48 B per
+  // lane, so a first call cost 12 % / 40 % more than the pair form on SN /
+  // in-trace-shuffled SN.  ANOMOD_HIST_FORM=auto keeps it: tests.)
+  int form = hist_form_of(spans);
   const bool uni = use_unique(spans);
-  const bool autof = form < 0 && pick_kernel(E, false, uni).ht == kHtPair;
+  const bool pair_ok = pick_kernel(E, false, uni).ht == kHtPair;
+  const bool autof = form < 0 && pair_ok && auto_forced();
+  const bool probe = form < 0 && pair_ok && !autof && spans->n_traces > 0;
   // (a set with traces longer than a chunk: LONG-like, the wide parent scan)
   const bool long_set = spans->max_trace_len != ~0ull && spans->max_trace_len > (uint64_t)kBigMin;
-  const Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal, long_set);
+  const Pick pc = pick_kernel(E, true, uni, kModeNormal, long_set);  // the probe's compact form
+  Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal, long_set);
   const Pick pr = autof ? pick_kernel(E, true, uni, kModeResume) : pk;  // the resume launch's form
   // As many workgroups as are resident at once (LDS / registers decide).
   int per_cu = 0, per_cu_r = 0;
@@ -1986,7 +2026,38 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
     // trace ranges (split on the device trace_ptr).
     std::vector<uint64_t> cuts;
     if (int rc = span_launch_cuts(ctx, spans, max_launch_spans(), cuts)) return rc;
+    if (probe) {
+      const bool whole = spans->n_spans <= 4 * kFormProbeSpans;
+      uint64_t P = cuts[1];
+      unsigned pgrid = (unsigned)grid;
+      if (!whole) {
+        const uint64_t want = (kFormProbeSpans * spans->n_traces + spans->n_spans - 1) / spans->n_spans;
+        P = std::min<uint64_t>(std::max<uint64_t>(want, 1), cuts[1]);
+        pgrid = (unsigned)std::min<uint64_t>(grid, kFormProbeGroups);
+      }
+      Table tp = tab;
+      tp.t_base = 0;
+      tp.occupancy = 1;
+      hipLaunchKernelGGL(pc.fn, dim3(pgrid), dim3(kThreads), 0, ctx->stream, spans->span_id,
+                         spans->parent_span_id, spans->svc_flags, spans->dur_us, spans->trace_ptr,
+                         P, S, E, tp);
+      ANOMOD_HIP(ctx, hipGetLastError());
+      unsigned long long occ = 0;
+      ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, tab.ovf + 1, 8, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+      ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      occ = *static_cast<const unsigned long long*>(ctx->h_stage);
+      form = occ <= kPairSlots / 2 ? 0 : 1;
+      spans->hist_form = (int8_t)form;
+      pk = pick_kernel(E, form == 1, uni, kModeNormal, long_set);
+      // the rest from P on (ovf[1] back to 0: after the run it counts
+      // pair-table overflows again)
+      ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
+      ANOMOD_HIP(ctx, hipMemsetAsync(tab.ovf + 1, 0, 8, ctx->stream));
+      cuts[0] = P;
+    }
     for (size_t k = 0; k + 1 < cuts.size(); ++k) {
+      if (cuts[k] >= cuts[k + 1]) continue;
       if (k > 0) {
         ANOMOD_HIP(ctx, hipMemsetAsync(tab.ctr, 0, 8, ctx->stream));
         if (autof) ANOMOD_HIP(ctx, hipMemsetAsync(tab.nleft, 0, 16, ctx->stream));

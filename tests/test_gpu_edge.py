@@ -443,3 +443,31 @@ def test_long_set_wide_scan(ctx, monkeypatch, alias):
     for _ in range(2):
         assert_table_equal(ctx.edge_aggregate(dev), ref)
     dev.free()
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_first_call_form_probe(ctx, shuffle):
+    """A set's first aggregation (histogram form unknown) runs its first
+    ~2^20 spans in the compact form on a few workgroups, reads their slot
+    occupancy and runs the rest in the form that says — an ordinary launch,
+    no spilling auto form: it costs about what a later call costs, learns
+    the pair form for SN spans (collector order or shuffled inside traces)
+    and equals the oracle."""
+    dev = ctx.generate(anomod.SynthSpec("SN", seed=31, p_orphan_ppm=500), 1 << 22)
+    if shuffle:
+        d2 = ctx.shuffle(dev, seed=4)
+        dev.free()
+        dev = d2
+    assert dev.hints[1] == -1
+    t1 = ctx.edge_aggregate(dev, with_hist=True)
+    cold = ctx.stage_ms(0)
+    assert dev.hints[1] == 0
+    warm = []
+    for _ in range(3):
+        t2 = ctx.edge_aggregate(dev, with_hist=True)
+        warm.append(ctx.stage_ms(0))
+    for k in FIELDS + ("hist",):
+        np.testing.assert_array_equal(getattr(t1, k), getattr(t2, k))
+    assert cold <= 1.25 * min(warm) + 0.25, (cold, warm)
+    assert_table_equal(t1, native.edge_aggregate(dev.download()))
+    dev.free()
