@@ -1605,7 +1605,7 @@ bool auto_forced() {
 }
 
 // The form probe of a first aggregation: spans it covers, workgroups it runs.
-constexpr uint64_t kFormProbeSpans = 1ull << 20;
+constexpr uint64_t kFormProbeSpans = 1ull << 19;
 constexpr uint64_t kFormProbeGroups = 16;
 
 int hist_form_of(const anomod_spans* s) {
@@ -1642,21 +1642,37 @@ __global__ __launch_bounds__(256) void order_probe_kernel(const uint64_t* __rest
   }
 }
 
-// Sets the set's order hint when unknown (one small kernel and one host
-// wait, the first aggregation of the set only).
-int probe_order(anomod_ctx* ctx, const anomod_spans* s, unsigned long long* d_cnt) {
-  if (!s->unique_ids || s->order >= 0) return ANOMOD_OK;
+// The set's order probe when its order hint is unknown (the first
+// aggregation of a unique-id set): the counts go to h[0..1] (pinned) once the
+// caller waits; probe_order_take sets the hint from them.
+bool need_order_probe(const anomod_spans* s) { return s->unique_ids && s->order < 0; }
+
+int probe_order_launch(anomod_ctx* ctx, const anomod_spans* s, unsigned long long* d_cnt,
+                       unsigned long long* h) {
+  h[0] = h[1] = 0ull;
   const uint64_t n = std::min<uint64_t>(s->n_spans, kProbeSpans);
-  unsigned long long h[2] = {0ull, 0ull};
   if (n > 1) {
     ANOMOD_HIP(ctx, hipMemsetAsync(d_cnt, 0, 16, ctx->stream));
     hipLaunchKernelGGL(order_probe_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 256)),
                        dim3(256), 0, ctx->stream, s->span_id, s->parent_span_id, n, d_cnt);
     ANOMOD_HIP(ctx, hipGetLastError());
     ANOMOD_HIP(ctx, hipMemcpyAsync(h, d_cnt, 16, hipMemcpyDeviceToHost, ctx->stream));
-    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
+  return ANOMOD_OK;
+}
+
+void probe_order_take(const anomod_spans* s, const unsigned long long* h) {
   s->order = 4ull * h[1] >= h[0] ? 1 : 0;
+}
+
+// Sets the set's order hint when unknown (one small kernel and one host
+// wait, the first aggregation of the set only).
+int probe_order(anomod_ctx* ctx, const anomod_spans* s, unsigned long long* d_cnt) {
+  if (!need_order_probe(s)) return ANOMOD_OK;
+  unsigned long long* h = static_cast<unsigned long long*>(ctx->h_stage);
+  if (int rc = probe_order_launch(ctx, s, d_cnt, h)) return rc;
+  ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  probe_order_take(s, h);
   return ANOMOD_OK;
 }
 
@@ -1975,25 +1991,28 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   const uint64_t big_cap = big_capacity(spans);
   // Histogram form: a set known to fit the pair table takes it, a set that
   // overflowed it the compact form.  A set not aggregated before (form -1)
-  // is probed: its first ~2^20 spans (kFormProbeSpans) run in the compact
-  // form — no probe chain, nothing to saturate — on a few workgroups (each
-  // then sees ~64 k spans, near a full-size workgroup's key diversity) that
+  // is probed: its first ~2^19 spans (kFormProbeSpans) run in the compact
+  // form — no probe chain, nothing to saturate — on 16 workgroups (each then
+  // sees ~32 k spans, near a full-size workgroup's key diversity) that
   // report their largest slot occupancy; at most half the pair table's
   // slots says pair.  The rest of the set runs in that form as an ordinary
   // launch: the probe's counts are part of the table.  A set of at most
-  // 4 x 2^20 spans runs whole in the compact form and learns the same way.
-  // (r04 started form-unknown sets in a pair form that stopped saturated
-  // workgroups and resumed them compact: its loop spilled 16 / 48 B per
-  // lane, so a first call cost 12 % / 40 % more than the pair form on SN /
-  // in-trace-shuffled SN.  ANOMOD_HIST_FORM=auto keeps it: tests.)
+  // 4 x 2^19 spans runs whole in the compact form and learns the same way.
+  // The order probe of a unique-id set (probe_order_launch) runs beside it:
+  // one host wait for both.  (r04 started form-unknown sets in a pair form
+  // that stopped saturated workgroups and resumed them compact: its loop
+  // spilled 16 / 48 B per lane, so a first call cost 12 % / 40 % more than
+  // the pair form on SN / in-trace-shuffled SN; ANOMOD_HIST_FORM=auto keeps
+  // it for tests.)
   int form = hist_form_of(spans);
-  const bool uni = use_unique(spans);
+  bool uni = use_unique(spans);  // (re-decided after an order probe)
   const bool pair_ok = pick_kernel(E, false, uni).ht == kHtPair;
   const bool autof = form < 0 && pair_ok && auto_forced();
   const bool probe = form < 0 && pair_ok && !autof && spans->n_traces > 0;
   // (a set with traces longer than a chunk: LONG-like, the wide parent scan)
   const bool long_set = spans->max_trace_len != ~0ull && spans->max_trace_len > (uint64_t)kBigMin;
-  const Pick pc = pick_kernel(E, true, uni, kModeNormal, long_set);  // the probe's compact form
+  // the probe's compact form (the forward scan when the order is still unknown)
+  const Pick pc = pick_kernel(E, true, uni, kModeNormal, long_set);
   Pick pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal, long_set);
   const Pick pr = autof ? pick_kernel(E, true, uni, kModeResume) : pk;  // the resume launch's form
   // As many workgroups as are resident at once (LDS / registers decide).
@@ -2016,8 +2035,18 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
   const Table tab = table_at(ctx, L, E);
   if (int rc = table_clear(ctx, L, tab, E)) return rc;
 
-  if (spans->n_traces > 0)
-    if (int rc = probe_order(ctx, spans, tab.big + 3)) return rc;  // scratch: big counters' 4th word
+  // A first aggregation's probes (order, histogram form) run back to back
+  // and are read back with one host wait.
+  const bool oprobe = spans->n_traces > 0 && need_order_probe(spans);
+  auto* hst = static_cast<unsigned long long*>(ctx->h_stage);  // [0..1] order, [2] occupancy
+  if (oprobe)  // scratch: the big counters' 4th and 5th words
+    if (int rc = probe_order_launch(ctx, spans, tab.big + 3, hst)) return rc;
+  if (!probe && oprobe) {
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    probe_order_take(spans, hst);
+    uni = use_unique(spans);
+    pk = pick_kernel(E, form == 1, uni, autof ? kModeAuto : kModeNormal, long_set);
+  }
   if (int rc = stage_begin(ctx, kStageEdgeAgg)) return rc;
   if (spans->n_traces > 0) {
     // A workgroup's LDS counters (histogram slots, errors) are u32 and the
@@ -2042,12 +2071,14 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
                          spans->parent_span_id, spans->svc_flags, spans->dur_us, spans->trace_ptr,
                          P, S, E, tp);
       ANOMOD_HIP(ctx, hipGetLastError());
-      unsigned long long occ = 0;
-      ANOMOD_HIP(ctx, hipMemcpyAsync(ctx->h_stage, tab.ovf + 1, 8, hipMemcpyDeviceToHost,
+      ANOMOD_HIP(ctx, hipMemcpyAsync(hst + 2, tab.ovf + 1, 8, hipMemcpyDeviceToHost,
                                      ctx->stream));
       ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      occ = *static_cast<const unsigned long long*>(ctx->h_stage);
-      form = occ <= kPairSlots / 2 ? 0 : 1;
+      if (oprobe) {
+        probe_order_take(spans, hst);
+        uni = use_unique(spans);
+      }
+      form = hst[2] <= kPairSlots / 2 ? 0 : 1;
       spans->hist_form = (int8_t)form;
       pk = pick_kernel(E, form == 1, uni, kModeNormal, long_set);
       // the rest from P on (ovf[1] back to 0: after the run it counts

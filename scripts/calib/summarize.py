@@ -5,7 +5,7 @@ profiles/<tag>_fetch_calibration.json: per access pattern, the true bytes one
 launch reads, FETCH_SIZE (bytes), their ratio and the factor that turns a
 kernel's FETCH_SIZE of that pattern into bytes requested from the memory side.
 
-usage: python scripts/calib/summarize.py gpurun_out/r5a r05
+usage: python scripts/calib/summarize.py gpurun_out/r5a r05 [gpurun_out/r5d]
 """
 import csv
 import json
@@ -40,6 +40,14 @@ def per_kernel(path, counter):
 
 
 fetch = per_kernel(src / "calib_fetch.csv", "FETCH_SIZE")
+# request sizes and DRAM-bound requests (a second run: gpurun_out/r5d)
+src2 = Path(sys.argv[3]) if len(sys.argv) > 3 else None
+req = {}
+if src2 and (src2 / "calib_reqsize.csv").exists():
+    for c in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+              "TCC_EA0_RDREQ_128B_sum"):
+        req[c] = per_kernel(src2 / "calib_reqsize.csv", c)
+    req["TCC_EA0_RDREQ_DRAM_sum"] = per_kernel(src2 / "calib_dram.csv", "TCC_EA0_RDREQ_DRAM_sum")
 hit = per_kernel(src / "calib_hitmiss.csv", "TCC_HIT_sum")
 miss = per_kernel(src / "calib_hitmiss.csv", "TCC_MISS_sum")
 out = {"what": "FETCH_SIZE against known byte counts (scripts/calib/fetch_calib.hip, 4 "
@@ -60,15 +68,20 @@ for i, t in enumerate(timing):
         "best_ms": t["best_ms"], "true_GBps": t["GBps"],
         "requested_GBps": round(2 * fb / (t["best_ms"] * 1e6), 1),
     }
+    if req:
+        q = {c: round(sum(v[4 * i:4 * i + 4]) / 4) for c, v in req.items()}
+        out["patterns"][name]["requests"] = q
+        out["patterns"][name]["useful_bytes_per_128B_request"] = round(
+            t["true_bytes"] / max(q["TCC_EA0_RDREQ_128B_sum"], 1), 2)
 out["conclusion"] = (
-    "FETCH_SIZE = 64 B per L2 miss (fetch_bytes_per_miss) for every pattern, streams and "
-    "gathers alike.  For the streams the true bytes are exactly 2 x FETCH_SIZE, i.e. 128 B per "
-    "miss.  A gather's request size cannot be read off FETCH_SIZE (a 64-B and a 128-B request "
-    "tally the same); 128-B lines are consistent with the rates (gather8_far: 67 M misses in "
-    "1.44 ms = 6.0 TB/s of 128-B lines, the stream's rate).  Calibrated factors, FETCH_SIZE -> "
-    "useful bytes: stream 2.0 (8 or 16 B per lane), gather32 0.50, gather16 0.25, gather8 0.125; "
-    "memory-side line traffic = 2 x FETCH_SIZE for all.  Infinity-Cache hits are counted: the "
-    "72-MiB-window gathers miss L2 as often as the 8-GiB ones (gather32_win) at twice the rate.")
+    "Every L2 miss is one 128-B read request (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ, no 32- or "
+    "64-B requests) for streams and gathers alike, and FETCH_SIZE tallies each at 64 B: "
+    "memory-side read bytes = 2 x FETCH_SIZE exactly, for every pattern.  TCC_EA0_RDREQ_DRAM "
+    "equals TCC_EA0_RDREQ, so Infinity-Cache hits are not told apart from HBM reads: the "
+    "72-MiB-window gathers request as many lines as the 8-GiB ones (gather32_win) and run at "
+    "twice the rate, so 2 x FETCH_SIZE is line traffic at the memory side, an upper bound on "
+    "HBM bytes.  Useful bytes per request: 128 for a coalesced stream (8 or 16 B per lane), 32 "
+    "/ 16 / 8 for a gather of that width; FETCH_SIZE per useful byte 0.5 / 2 / 4 / 8.")
 dst = ROOT / "profiles" / f"{tag}_fetch_calibration.json"
 dst.write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps(out, indent=1))
