@@ -379,7 +379,9 @@ __device__ __forceinline__ bool grid_barrier(unsigned int* bar, uint32_t k, int*
 // the per-launch kernel's whatever SUB, only the number of workgroups meeting
 // at the grid barrier shrinks (391 -> 98 at N = 10^5 with SUB = 4).
 constexpr uint32_t kLdsEdgeBytes = 128 * 1024;  // (col, w) staging per workgroup
-constexpr uint64_t kRingBytes = 1ull << 30;       // most HBM the per-iteration vectors take
+constexpr uint64_t kRingBytes = 4ull << 30;       // most HBM the per-iteration vectors take
+// (4 GiB of 288: K = 16 at N = 10^5 takes 12.8 MB per iteration, 1.28 GB per
+// 100-iteration solve; at 1 GiB it ran the two-buffer form, agent-scope loads)
 #ifndef ANOMOD_PPR_GATHER
 #define ANOMOD_PPR_GATHER 4
 #endif
@@ -847,6 +849,209 @@ __global__ __launch_bounds__(kPprThreads * SUB) void ppr_batch_persistent_kernel
 #pragma unroll
     for (int k = 0; k < K; ++k)
       __hip_atomic_store(&x0[(uint64_t)r * K + k], xr[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x == 0) bar[2] = done;
+}
+
+// K = 16 in halves: a workgroup holds two 256-row blocks and, for each, two
+// halves of 256 lanes — lane (block, half, row) computes vectors 8 h .. 8 h + 7
+// of its row, so a lane carries the K = 8 kernel's state (252 VGPRs at one
+// row of 16 vectors per lane left two waves per SIMD).  The vector ring holds
+// each slot as two node-major [N'][8] halves, so a half's gather is the K = 8
+// kernel's 64-B row read; iteration 0 reads no vector at all (x0 = 1/N
+// everywhere: the same double the per-launch path loads).  Per vector the
+// edge order, the 256-row block partition, the wave reduction tree (a wave
+// holds 64 consecutive rows of one half) and the fixed-point slots are those
+// of ppr_batch_iter_kernel<16>, so every column is bit-equal to it; the final
+// vectors land in x0 as [N][16].  RING only (the caller falls back to the
+// SUB form without a ring).
+constexpr int kSplitH = 8;  // vectors per half
+#ifndef ANOMOD_PPR_SPLIT_BATCH
+#define ANOMOD_PPR_SPLIT_BATCH 4
+#endif
+constexpr int kSplitBatch = ANOMOD_PPR_SPLIT_BATCH;  // in-edges gathered together per lane
+__global__ __launch_bounds__(4 * kPprThreads) void ppr_batch_split_kernel(
+    uint32_t N, const uint32_t* __restrict__ in_ptr, const uint32_t* __restrict__ in_col,
+    const float* __restrict__ in_w, const uint8_t* __restrict__ dangling,
+    const double* __restrict__ p, double alpha, double* x0, double* x1, unsigned long long* acc,
+    uint32_t iters, double ntol, unsigned int* bar, uint32_t spin_limit, double* ring,
+    uint64_t slot) {
+  (void)x1;
+  constexpr int K = 16, H = kSplitH, SUB = 2;
+  constexpr uint32_t kLdsE = 3072u * SUB;
+  constexpr int S = kAccSlots * K;
+  constexpr int kNW = kPprThreads / 64;  // waves per 256-row block and half
+  constexpr int kWaves = 4 * kNW;
+  constexpr int Q = H / 2;               // 16-B pieces per half row
+  __shared__ uint32_t lcol[kLdsE];
+  __shared__ float lw[kLdsE];
+  __shared__ double red[SUB * 2 * 2 * H * kNW];
+  __shared__ double s_dsum[K];
+  __shared__ v4u32 stg[kWaves * 64 * (Q + 1)];
+  __shared__ uint32_t s_conv;
+  __shared__ int s_flag;
+  const uint32_t qq = threadIdx.x / kPprThreads, lt = threadIdx.x % kPprThreads;
+  const uint32_t sub = qq >> 1, h = qq & 1u;
+  const uint32_t gb = blockIdx.x * SUB + sub;  // the 256-row block of this lane
+  const uint32_t r = gb * kRowsPerBlock + lt;
+  const uint32_t r0 = blockIdx.x * SUB * kRowsPerBlock;
+  const uint32_t r0e = r0 < N ? r0 : N;
+  const uint32_t r1 = r0 + SUB * kRowsPerBlock < N ? r0 + SUB * kRowsPerBlock : N;
+  const uint32_t e0 = in_ptr[r0e], e1 = in_ptr[r1];
+  const uint32_t nc = e1 - e0 < kLdsE ? e1 - e0 : kLdsE;
+  for (uint32_t i = threadIdx.x; i < nc; i += 4 * kPprThreads) {
+    lcol[i] = in_col[e0 + i];
+    lw[i] = in_w[e0 + i];
+  }
+  uint32_t rb = 0, re = 0;
+  double xr[H];  // (the personalization is re-read per iteration: registers)
+  bool dg = false;
+  const double x0v = 1.0 / (double)N;
+  const double* pr = p + (uint64_t)(r < N ? r : 0u) * K + h * H;
+#pragma unroll
+  for (int k = 0; k < H; ++k) xr[k] = 0.0;
+  if (r < N) {
+    rb = in_ptr[r];
+    re = in_ptr[r + 1];
+    dg = dangling[r] != 0;
+#pragma unroll
+    for (int k = 0; k < H; ++k) xr[k] = x0v;
+  }
+  if (threadIdx.x == 0) s_conv = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t hs = slot / 2;  // doubles per half of a ring slot
+  uint32_t frozen = 0, done = iters;
+  double* const red_me = red + (sub * 2 + h) * 2 * H * kNW;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const double* x_in = it == 0 ? nullptr : ring + (uint64_t)(it - 1u) * slot + h * hs;
+    double* x_out = ring + (uint64_t)it * slot + h * hs;
+    const int rr = it % 3, w = (it + 1) % 3, z = (it + 2) % 3;
+    const bool check = ntol > 0.0 && it > 0;
+    {  // wave wid reads vector wid's slots of the previous iteration
+      const int k = wid;
+      unsigned long long dv = __hip_atomic_load(&acc[rr * S + k * kAccSlots + lane],
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long ev = check ? __hip_atomic_load(&acc[(3 + rr) * S + k * kAccSlots + lane],
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0ull;
+      for (int off = 32; off > 0; off >>= 1) {
+        dv += __shfl_xor(dv, off);
+        ev += __shfl_xor(ev, off);
+      }
+      if (lane == 0) {
+        s_dsum[k] = (double)dv * (1.0 / kDScale);
+        if (check && (double)ev * (1.0 / kEScale) < ntol) atomicOr(&s_conv, 1u << k);
+      }
+    }
+    double sum[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) sum[k] = 0.0;
+    if (r < N) {
+      for (uint32_t k0 = rb; k0 < re; k0 += kSplitBatch) {
+        uint32_t c[kSplitBatch];
+        float wv[kSplitBatch];
+#pragma unroll
+        for (int j = 0; j < kSplitBatch; ++j) {
+          const uint32_t e = k0 + j, li = e - e0;
+          const bool ok = e < re;
+          c[j] = !ok ? r : li < nc ? lcol[li] : in_col[e];
+          wv[j] = !ok ? 0.f : li < nc ? lw[li] : in_w[e];
+        }
+#pragma unroll
+        for (int j = 0; j < kSplitBatch; ++j) {
+          if (k0 + j < re) {
+            double xv[H];
+            if (x_in) {
+              const double* xs = x_in + (uint64_t)c[j] * H;
+#pragma unroll
+              for (int k = 0; k < H; k += 2) {
+                const double2 v2 = *reinterpret_cast<const double2*>(xs + k);
+                xv[k] = v2.x;
+                xv[k + 1] = v2.y;
+              }
+            } else {
+#pragma unroll
+              for (int k = 0; k < H; ++k) xv[k] = x0v;
+            }
+#pragma unroll
+            for (int k = 0; k < H; ++k) sum[k] = ppr_edge(sum[k], xv[k], wv[j]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    frozen |= s_conv;
+    if (check && (frozen & 0xFFFFu) == 0xFFFFu) {
+      done = it;
+      break;
+    }
+    // per vector: the new value, then at once its wave's reduction tree of
+    // the dangling mass and the L1 change (no per-vector arrays kept live)
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      double dacc = 0.0, eacc = 0.0;
+      if (r < N) {
+        const uint32_t kk = h * H + (uint32_t)k;
+        const double y = (frozen >> kk) & 1u ? xr[k] : ppr_row(alpha, sum[k], s_dsum[kk], pr[k]);
+        if (dg) dacc = y;
+        eacc = fabs(y - xr[k]);
+        xr[k] = y;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        dacc += __shfl_xor(dacc, off);
+        eacc += __shfl_xor(eacc, off);
+      }
+      if (lane == 0) {
+        red_me[(2 * k) * kNW + (wid % kNW)] = dacc;
+        red_me[(2 * k + 1) * kNW + (wid % kNW)] = eacc;
+      }
+    }
+    {  // the wave's 64 half rows, written through as 1-KiB store instructions
+      v4u32* st = stg + wid * (64 * (Q + 1));
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint64_t a0 = __double_as_longlong(xr[2 * q]), a1 = __double_as_longlong(xr[2 * q + 1]);
+        st[lane * (Q + 1) + q] = v4u32{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1,
+                                      (uint32_t)(a1 >> 32)};
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t row0 = r - (uint32_t)lane;
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {
+        const uint32_t i = (uint32_t)(j * 64 + lane), row = i / Q, q = i % Q;
+        if (row0 + row < N)
+          store16_wt(x_out + (uint64_t)(row0 + row) * H + 2 * q, st[row * (Q + 1) + q]);
+      }
+    }
+    __syncthreads();
+    if (lt < (uint32_t)H) {  // block_sum's order: the 4 wave partials from 0.0, in wave order
+      const int k = (int)lt;
+      double ds = 0.0, es = 0.0;
+      for (int q = 0; q < kNW; ++q) {
+        ds += red_me[(2 * k) * kNW + q];
+        es += red_me[(2 * k + 1) * kNW + q];
+      }
+      const int sl = (int)(h * H + (uint32_t)k) * kAccSlots + (int)(gb & (kAccSlots - 1));
+      atomicAdd(&acc[w * S + sl], __double2ull_rn(ds * kDScale));
+      atomicAdd(&acc[(3 + w) * S + sl], __double2ull_rn(es * kEScale));
+    }
+    if (blockIdx.x == 0)
+      for (int i = threadIdx.x; i < S; i += 4 * kPprThreads) {
+        __hip_atomic_store(&acc[z * S + i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&acc[(3 + z) * S + i], 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    if (threadIdx.x == 0) s_conv = 0u;  // (read by every thread before the barrier above)
+    if (!grid_barrier(bar, it, &s_flag, spin_limit)) {
+      done = it;
+      break;
+    }
+  }
+  if (r < N)
+#pragma unroll
+    for (int k = 0; k < H; ++k)
+      __hip_atomic_store(&x0[(uint64_t)r * K + h * H + k], xr[k], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == 0 && threadIdx.x == 0) bar[2] = done;
 }
@@ -1449,22 +1654,28 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   const char* ring_env = getenv("ANOMOD_PPR_RING");
   bool ring = !(ring_env && ring_env[0] == '0') && (uint64_t)iters * slot * 8 <= kRingBytes;
   const uint32_t bsub = batch_sub(kb);
-  const uint32_t bgrid = (g->grid + bsub - 1) / bsub;  // persistent workgroups
-  const BatchFn bfn = batch_persistent_fn(kb, ring, bsub);
-  if (g->bcoop_kb != kb || g->bcoop_ring != ring || g->bcoop_sub != bsub) {
+  // K = 16 with a ring: the split kernel (two 256-row blocks x two halves of
+  // 8 vectors per 1024-thread workgroup); ANOMOD_PPR_SPLIT=0 keeps the SUB form
+  const char* split_env = getenv("ANOMOD_PPR_SPLIT");
+  const bool split = kb == 16 && ring && !(split_env && split_env[0] == '0');
+  const uint32_t bthreads = split ? 4u * kPprThreads : kPprThreads * bsub;
+  const uint32_t bgrid = split ? (g->grid + 1) / 2 : (g->grid + bsub - 1) / bsub;  // workgroups
+  const BatchFn bfn = split ? ppr_batch_split_kernel : batch_persistent_fn(kb, ring, bsub);
+  if (g->bcoop_kb != kb || g->bcoop_ring != ring || g->bcoop_sub != bsub + (split ? 16u : 0u)) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfn, kPprThreads * bsub, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bfn, bthreads, 0) != hipSuccess)
       per_cu = 0;
     (void)hipGetLastError();
     g->bcoop_blocks = (per_cu > 1 ? per_cu - 1 : per_cu) * ctx->num_cus;
     g->bcoop_kb = kb;
     g->bcoop_ring = ring;
-    g->bcoop_sub = bsub;
+    g->bcoop_sub = bsub + (split ? 16u : 0u);
   }
   bool persistent = mode != 1 && (int)bgrid <= g->bcoop_blocks;
   if (persistent && ring) {
     ring = ensure_ring(ctx, g, (uint64_t)iters * slot * 8);
-    if (!ring) {  // no ring: the two-buffer instantiation (its own residency)
+    if (!ring && split) persistent = false;  // (the split kernel needs the ring)
+    if (!ring && !split) {  // no ring: the two-buffer instantiation (its own residency)
       int per_cu = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, batch_persistent_fn(kb, false, bsub),
                                                        kPprThreads * bsub, 0) != hipSuccess)
@@ -1480,7 +1691,8 @@ int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* 
   bool fell_back = false;
   if (persistent) {
     const double ntol = tol > 0.0 ? (double)N * tol : 0.0;
-    hipLaunchKernelGGL(batch_persistent_fn(kb, ring, bsub), dim3(bgrid), dim3(kPprThreads * bsub), 0,
+    hipLaunchKernelGGL(split ? ppr_batch_split_kernel : batch_persistent_fn(kb, ring, bsub),
+                       dim3(bgrid), dim3(bthreads), 0,
                        ctx->stream, N, g->in_ptr, g->in_col, g->in_w, g->dangling, g->bp, alpha,
                        g->bx[0], g->bx[1], g->bacc, iters, ntol, g->bar, spin,
                        ring ? g->ring : nullptr, slot);

@@ -297,9 +297,13 @@ def test_pagerank_batch_persistent_equals_per_launch(ctx, monkeypatch, K, bsub):
     for bit, in fixed-iteration and tolerance mode (per-vector freezing);
     a barrier timeout (ANOMOD_PPR_SPIN=0) reruns per launch, same bits.
     bsub: 256-row blocks per persistent workgroup (ANOMOD_PPR_BSUB; K = 16
-    defaults to 2)."""
+    defaults to 2); K = 16 with the vector ring runs the split kernel (two
+    halves of 8 vectors per row), and (16, "1") the one-row-per-lane form
+    (ANOMOD_PPR_SPLIT=0)."""
     if bsub:
         monkeypatch.setenv("ANOMOD_PPR_BSUB", bsub)
+        if K == 16:
+            monkeypatch.setenv("ANOMOD_PPR_SPLIT", "0")
     g = anomod.DeviceGraph(ctx, synthetic=(40000, 9, 12))
     rng = np.random.default_rng(K + 40)
     P = rng.random((K, g.N))
