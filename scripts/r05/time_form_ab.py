@@ -21,14 +21,17 @@ lg = int(sys.argv[1]) if len(sys.argv) > 1 else 27
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 topo = sys.argv[3] if len(sys.argv) > 3 else "SN"
 shuffle = len(sys.argv) > 4 and sys.argv[4] == "1"
+touch = len(sys.argv) > 5 and sys.argv[5] == "1"  # read the set once (trace structure) first
 with anomod.Context(0) as ctx:
     dev = ctx.generate(anomod.SynthSpec(topo, seed=20251103, p_orphan_ppm=100), 1 << lg)
     if shuffle:
         d2 = ctx.shuffle(dev, seed=3)
         dev.free()
         dev = d2
+    if touch:
+        ctx.trace_structure(dev, download=False)
     t = ctx.edge_aggregate(dev, with_hist=False)
-    print(json.dumps({"cold_ms": round(ctx.stage_ms(L.STAGE_EDGE_AGG), 3), "hints": dev.hints}),
+    print(json.dumps({"touched": touch, "cold_ms": round(ctx.stage_ms(L.STAGE_EDGE_AGG), 3), "hints": dev.hints}),
           flush=True)
     for r in range(reps):
         for form in ("auto", "pair", "default"):
