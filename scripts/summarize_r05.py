@@ -105,15 +105,17 @@ def main() -> int:
         if "trace_structure" in ref:
             ts = ref["trace_structure"]
             targets.append(("trace structure", "trace_struct_kernel<true>", ts["bytes_per_launch"],
-                            slice(None), [(26 * ts["spans"], "stream8")]))
+                            slice(None), [(26 * n, "stream8")]))
         if "tt_width" in ref:
             tw = ref["tt_width"]
-            targets.append(("TrainTicket width edge_agg <either histogram form, wide stats>",
-                            r"re:edge_agg_kernel<[12], 3, true, 0>", tw["bytes_per_launch"],
+            # (the first call's form probe, a compact-form launch of 16
+            # workgroups over the first 2^19 spans, has the other form's name)
+            targets.append(("TrainTicket width edge_agg <pair histogram, wide stats>",
+                            "edge_agg_kernel<1, 3, true, 0>", tw["bytes_per_launch"],
                             slice(0, 3), [(tw["bytes_per_launch"], "stream8")]))
         if "long_traces" in ref:
-            targets.append(("LONG chunk walk edge_agg <compact, direct stats, wide scan>",
-                            r"re:edge_agg_kernel<2, 1, true, [03]>", None, slice(0, 3), None))
+            targets.append(("LONG chunk walk edge_agg <compact, direct stats, wide scan | id hash>",
+                            r"re:edge_agg_kernel<2, 1, true, [034]>", None, slice(1, 4), None))
             targets.append(("LONG long-trace resolve", "edge_big_resolve_kernel", None, slice(1, 4),
                             None))
             targets.append(("LONG long-trace record", "edge_big_record_kernel<2, 1>", None,
