@@ -992,7 +992,10 @@ __global__ __launch_bounds__(kBigThreads) void edge_big_kernel(
 // exact-quantile mode, its key — and edge_big_record_kernel streams the
 // listed spans (16 traces per ticket, one load round trip per ticket) into
 // the chunk walk's tables.  Same first-match rule, same table forms.
-constexpr int kResThreads = 512;
+#ifndef ANOMOD_RES_THREADS
+#define ANOMOD_RES_THREADS 512
+#endif
+constexpr int kResThreads = ANOMOD_RES_THREADS;
 #ifndef ANOMOD_RES_WIN
 #define ANOMOD_RES_WIN 2048
 #endif
