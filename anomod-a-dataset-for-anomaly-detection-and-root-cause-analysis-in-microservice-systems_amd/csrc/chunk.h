@@ -178,7 +178,11 @@ static_assert(kFwd % 2 == 0 && kBwd % 2 == 0 && kFwd + kBwd <= 16, "bidirectiona
 
 // MAXS > 0: give up after that many steps and return -2 (not found yet; the
 // caller completes the lookup cooperatively).
-template <uint32_t FW = kFwd, uint32_t BW = kBwd, int MAXS = 0>
+// SEL: the matches found by selects (lowest matching slot of each block, kept
+// if inside the block's valid range) with both blocks' loads issued before
+// the one branch — otherwise the compiler sinks the backward block's loads
+// under the forward block's test, two LDS round trips per step.
+template <uint32_t FW = kFwd, uint32_t BW = kBwd, int MAXS = 0, bool SEL = false>
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,
                                                  uint32_t i, uint64_t pid) {
   int steps = 0;
@@ -194,6 +198,17 @@ __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t 
     for (uint32_t j = 0; j < FW; ++j) v[j] = lsid[f + j];
 #pragma unroll
     for (uint32_t j = 0; j < BW; ++j) w[j] = lsid[gb + j];
+    if constexpr (SEL) {
+    uint32_t qf = FW, qb = BW;
+#pragma unroll
+    for (int j = (int)FW - 1; j >= 0; --j) qf = v[j] == pid ? (uint32_t)j : qf;
+#pragma unroll
+    for (int j = (int)BW - 1; j >= 0; --j) qb = w[j] == pid ? (uint32_t)j : qb;
+    const uint32_t hi = (b - f) < FW ? (b - f) : FW;  // >= 1 while f < b
+    const int32_t nb = g - (int32_t)gb + 1;
+    const bool okf = qf < hi, okb = (int32_t)qb < nb;
+    if (okf || okb) return (int)(okf ? f + qf : gb + qb);
+    } else {
     uint32_t mf = 0, mb = 0;
 #pragma unroll
     for (uint32_t j = 0; j < FW; ++j) mf |= (v[j] == pid ? 1u : 0u) << j;
@@ -206,6 +221,7 @@ __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t 
     mb &= nb > 0 ? (1u << (uint32_t)nb) - 1u : 0u;
     if (mf) return (int)(f + __ffs(mf) - 1u);
     if (mb) return (int)(gb + 31u - __clz(mb));  // unique ids: any match is the match
+    }
     f += FW;
     g -= (int32_t)BW;
     if (f >= b) return -1;

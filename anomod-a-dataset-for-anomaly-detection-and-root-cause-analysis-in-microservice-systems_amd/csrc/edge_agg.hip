@@ -477,6 +477,27 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
 // collector-ordered traces of tens of spans (SN / TrainTicket: 8 / 8 measured
 // 2-10 % slower there), (8, 8) for sets holding traces longer than a chunk
 // (LONG: random ancestors in 128- and 256-span traces, 7.52 vs 8.09 ms).
+// r05: the TrainTicket-width and long-trace instantiations take the
+// select-built scan (one LDS round trip per step): TT 2^27 17.8-18.4 vs
+// 18.5-18.7 ms, LONG 2^23 7.24-7.29 vs 7.60-7.69; the SN pair form gains
+// nothing measurable and keeps the mask form (profiles/r05_experiments/
+// parent_scan_sel_widths.log).
+#ifndef ANOMOD_SEL_SN
+#define ANOMOD_SEL_SN 0
+#endif
+#ifndef ANOMOD_SEL_WIDE
+#define ANOMOD_SEL_WIDE 1
+#endif
+#ifndef ANOMOD_SEL_LONG
+#define ANOMOD_SEL_LONG 1
+#endif
+#ifndef ANOMOD_LFWD
+#define ANOMOD_LFWD 8
+#endif
+#ifndef ANOMOD_LBWD
+#define ANOMOD_LBWD 8
+#endif
+constexpr uint32_t kLFwd = ANOMOD_LFWD, kLBwd = ANOMOD_LBWD;  // the long-trace sets' widths
 template <int HT, int ST, bool UNI, bool WIDE = false>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
                                               const Chunk& c, const Regs& R, uint32_t S,
@@ -484,6 +505,9 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kWSid);
   auto* lsvc = reinterpret_cast<uint16_t*>(wsm + kWSvc);
   auto* lflag = reinterpret_cast<uint8_t*>(wsm + kWFlag);
+  // select-built scan (chunk.h find_parent_bidir SEL) per table form
+  constexpr bool kSel = WIDE ? ANOMOD_SEL_LONG != 0
+                             : (ST == kStWide ? ANOMOD_SEL_WIDE != 0 : ANOMOD_SEL_SN != 0);
   if constexpr (ANOMOD_ABL & 16) {  // stream only: keep the loads, do nothing
     uint64_t x = 0;
 #pragma unroll
@@ -513,8 +537,8 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       trace_bounds(Sm, r, lane, c.n, a, b);
       int q = -1;
       if (has) {
-        q = UNI ? (WIDE ? find_parent_bidir<8, 8, kCoopSteps>(lsid, a, b, i, R.pid[r])
-                        : find_parent_bidir<kFwd, kBwd, kCoopSteps>(lsid, a, b, i, R.pid[r]))
+        q = UNI ? (WIDE ? find_parent_bidir<kLFwd, kLBwd, kCoopSteps, kSel>(lsid, a, b, i, R.pid[r])
+                        : find_parent_bidir<kFwd, kBwd, kCoopSteps, kSel>(lsid, a, b, i, R.pid[r]))
                 : find_parent<kCoopSteps>(lsid, a, b, R.pid[r]);
       }
       coop_parent(lsid, __ballot(q == -2), lane, R.pid[r], a, b, q);
@@ -524,8 +548,8 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
         trace_bounds(Sm, r, lane, c.n, a, b);
-        const int q = UNI ? (WIDE ? find_parent_bidir<8, 8>(lsid, a, b, i, R.pid[r])
-                                  : find_parent_bidir(lsid, a, b, i, R.pid[r]))
+        const int q = UNI ? (WIDE ? find_parent_bidir<kLFwd, kLBwd, 0, kSel>(lsid, a, b, i, R.pid[r])
+                                  : find_parent_bidir<kFwd, kBwd, 0, kSel>(lsid, a, b, i, R.pid[r]))
                           : find_parent(lsid, a, b, R.pid[r]);
         if (q >= 0) p = lsvc[q];
       } else {  // ablation: a parent-like edge without the lookup (keeps key diversity)

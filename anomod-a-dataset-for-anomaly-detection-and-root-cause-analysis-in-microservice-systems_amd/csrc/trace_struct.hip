@@ -41,6 +41,10 @@
 #include "chunk.h"
 #include "common.h"
 
+#ifndef ANOMOD_SEL_TS
+#define ANOMOD_SEL_TS 0  // select-built parent scan (chunk.h find_parent_bidir SEL)
+#endif
+
 namespace anomod {
 namespace {
 
@@ -185,7 +189,8 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
         // i), and the parent reference has at most one match, found from
         // either end (chunk.h find_parent_bidir); no own-id scan
         f[r] = l = (int)i;
-        pf = pid[r] != 0ull ? find_parent_bidir(lsid, a[r], b, i, pid[r]) : -1;
+        pf = pid[r] != 0ull ? find_parent_bidir<kFwd, kBwd, 0, ANOMOD_SEL_TS != 0>(lsid, a[r], b, i, pid[r])
+                            : -1;
         np[r] = pf;
       } else {
         scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
