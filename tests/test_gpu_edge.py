@@ -425,23 +425,54 @@ def test_long_set_wide_scan(ctx, monkeypatch, alias):
     rng.shuffle(lens)
     sp = _random_spanset(rng, 12, 0, 0, lens=lens)
     if alias:  # ids 1..L inside each trace, parents remapped to them
-        ptr = sp.trace_ptr.astype(np.int64)
-        sid = np.empty(sp.n_spans, np.uint64)
-        remap = {}
-        for t in range(len(lens)):
-            a, b = ptr[t], ptr[t + 1]
-            new = np.arange(1, b - a + 1, dtype=np.uint64)
-            remap.update(zip(sp.span_id[a:b].tolist(), new.tolist()))
-            sid[a:b] = new
-        pid = np.array([remap.get(int(p), 10**12 + int(p) % 997) if p else 0
-                        for p in sp.parent_span_id], np.uint64)
-        sp = anomod.SpanSet(sp.services, sp.trace_ptr, sid.copy(), sid, pid, sp.svc, sp.flags,
-                            sp.dur_us)
+        sp = _alias_ids(sp)
     assert sp.check_unique_ids()
     ref = native.edge_aggregate(sp)
     dev = ctx.upload(sp)
     for _ in range(2):
         assert_table_equal(ctx.edge_aggregate(dev), ref)
+    dev.free()
+
+
+def _alias_ids(sp, self_ref=0.0, rng=None):
+    """The same set with ids 1..L inside every trace (parents remapped to
+    them, orphan references to ids no trace holds); self_ref: that share of
+    the spans reference their own id."""
+    ptr = sp.trace_ptr.astype(np.int64)
+    sid = np.empty(sp.n_spans, np.uint64)
+    remap = {}
+    for t in range(sp.n_traces):
+        a, b = ptr[t], ptr[t + 1]
+        new = np.arange(1, b - a + 1, dtype=np.uint64)
+        remap.update(zip(sp.span_id[a:b].tolist(), new.tolist()))
+        sid[a:b] = new
+    pid = np.array([remap.get(int(p), 10**12 + int(p) % 997) if p else 0
+                    for p in sp.parent_span_id], np.uint64)
+    if self_ref:
+        m = rng.random(sp.n_spans) < self_ref
+        pid[m] = sid[m]
+    return anomod.SpanSet(sp.services, sp.trace_ptr, sid.copy(), sid, pid, sp.svc, sp.flags,
+                          sp.dur_us)
+
+
+@pytest.mark.parametrize("S", [12, 46])
+def test_aliased_ids_in_chunk(ctx, S):
+    """Every trace holds ids 1..L, so a wave chunk holds equal ids of
+    different traces on both sides of every trace boundary: the scan's
+    forward block runs past the trace end and its backward block is clamped
+    at the trace start (re-reading the span itself and later ones), and a
+    match there must not count.  SN width (mask-built scan) and TrainTicket
+    width (select-built scan), collector order and shuffled inside the
+    traces, orphans and self references.  Equal to the oracle."""
+    rng = np.random.default_rng(300 + S)
+    sp = _alias_ids(_random_spanset(rng, S, 6000, 40, orphan=0.05), self_ref=0.01, rng=rng)
+    assert sp.check_unique_ids()
+    dev = ctx.upload(sp)
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(sp))
+    shuf = ctx.shuffle(dev, seed=9, window_traces=0)
+    assert shuf.unique_ids
+    assert_table_equal(ctx.edge_aggregate(shuf), native.edge_aggregate(shuf.download()))
+    shuf.free()
     dev.free()
 
 
