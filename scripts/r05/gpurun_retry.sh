@@ -7,7 +7,7 @@ out=$1; shift
 for i in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout 1200 -- "$@" > "$out" 2>&1
   rc=$?
-  if grep -q "retry in a few minutes" "$out" && grep -q "charged=0.0s" "$out"; then
+  if grep -q "retry in" "$out" && grep -Eq "charged=(0\.0s|None)" "$out"; then
     sleep 120
     continue
   fi
