@@ -186,7 +186,7 @@ template <uint32_t FW = kFwd, uint32_t BW = kBwd, int MAXS = 0, bool SEL = false
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,
                                                  uint32_t i, uint64_t pid) {
   int steps = 0;
-  static_assert(FW % 2 == 0 && BW % 2 == 0 && FW + BW <= 16, "bidirectional step");
+  static_assert(FW % 2 == 0 && BW % 2 == 0 && FW <= 32 && BW <= 32, "bidirectional step");
   uint32_t f = a;             // next forward block [f, f + FW)
   int32_t g = (int32_t)i - 1;  // backward blocks end at g (inclusive)
   while (true) {
@@ -226,6 +226,46 @@ __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t 
     g -= (int32_t)BW;
     if (f >= b) return -1;
     if (MAXS > 0 && ++steps >= MAXS) return -2;
+  }
+}
+
+// find_parent_bidir<SEL> over ids staged as two u32 planes (lo[], hi[]): the
+// steps compare low words only (half the LDS bytes, 32-bit compares), and a
+// low-word candidate is confirmed on its high word; a false candidate (two ids
+// of the trace sharing a low word) finishes with an exact forward scan of the
+// trace.  Unique ids: any confirmed match is the match.
+template <uint32_t FW, uint32_t BW>
+__device__ __forceinline__ int find_parent_split(const uint32_t* lo, const uint32_t* hi, uint32_t a,
+                                                 uint32_t b, uint32_t i, uint64_t pid) {
+  const uint32_t plo = (uint32_t)pid, phi = (uint32_t)(pid >> 32);
+  uint32_t f = a;
+  int32_t g = (int32_t)i - 1;
+  while (true) {
+    const int32_t gb0 = g - (int32_t)BW + 1;
+    const uint32_t gb = gb0 < (int32_t)a ? a : (uint32_t)gb0;
+    uint32_t v[FW], w[BW];
+#pragma unroll
+    for (uint32_t j = 0; j < FW; ++j) v[j] = lo[f + j];
+#pragma unroll
+    for (uint32_t j = 0; j < BW; ++j) w[j] = lo[gb + j];
+    uint32_t qf = FW, qb = BW;
+#pragma unroll
+    for (int j = (int)FW - 1; j >= 0; --j) qf = v[j] == plo ? (uint32_t)j : qf;
+#pragma unroll
+    for (int j = (int)BW - 1; j >= 0; --j) qb = w[j] == plo ? (uint32_t)j : qb;
+    const uint32_t hf = (b - f) < FW ? (b - f) : FW;
+    const int32_t nb = g - (int32_t)gb + 1;
+    const bool okf = qf < hf, okb = (int32_t)qb < nb;
+    if (okf || okb) {
+      const uint32_t q = okf ? f + qf : gb + qb;
+      if (hi[q] == phi) return (int)q;
+      for (uint32_t k = a; k < b; ++k)  // a low-word alias: exact scan
+        if (lo[k] == plo && hi[k] == phi) return (int)k;
+      return -1;
+    }
+    f += FW;
+    g -= (int32_t)BW;
+    if (f >= b) return -1;
   }
 }
 

@@ -481,7 +481,11 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
 // select-built scan (one LDS round trip per step): TT 2^27 17.8-18.4 vs
 // 18.5-18.7 ms, LONG 2^23 7.24-7.29 vs 7.60-7.69; the SN pair form gains
 // nothing measurable and keeps the mask form (profiles/r05_experiments/
-// parent_scan_sel_widths.log).
+// parent_scan_sel_widths.log).  Then both take the split-word form
+// (chunk.h find_parent_split: ids staged as u32 planes, low words compared,
+// the candidate confirmed on its high word), whose cheaper steps pay for
+// wider ones: TT 12 / 4 16.3-16.7 ms, LONG 12 / 4 6.96-7.04
+// (split_scan_*.log); the SN pair form again gains nothing.
 #ifndef ANOMOD_SEL_SN
 #define ANOMOD_SEL_SN 0
 #endif
@@ -491,13 +495,29 @@ __device__ __forceinline__ int find_parent(const uint64_t* lsid, uint32_t a, uin
 #ifndef ANOMOD_SEL_LONG
 #define ANOMOD_SEL_LONG 1
 #endif
+#ifndef ANOMOD_SPLIT_LONG
+#define ANOMOD_SPLIT_LONG 1
+#endif
+#ifndef ANOMOD_SPLIT_WIDE
+#define ANOMOD_SPLIT_WIDE 1
+#endif
+#ifndef ANOMOD_SPLIT_SN
+#define ANOMOD_SPLIT_SN 0
+#endif
 #ifndef ANOMOD_LFWD
-#define ANOMOD_LFWD 8
+#define ANOMOD_LFWD 12
 #endif
 #ifndef ANOMOD_LBWD
-#define ANOMOD_LBWD 8
+#define ANOMOD_LBWD 4
 #endif
 constexpr uint32_t kLFwd = ANOMOD_LFWD, kLBwd = ANOMOD_LBWD;  // the long-trace sets' widths
+#ifndef ANOMOD_WFWD
+#define ANOMOD_WFWD 12
+#endif
+#ifndef ANOMOD_WBWD
+#define ANOMOD_WBWD 4
+#endif
+constexpr uint32_t kWFwd = ANOMOD_WFWD, kWBwd = ANOMOD_WBWD;  // TrainTicket width, split scan
 template <int HT, int ST, bool UNI, bool WIDE = false>
 __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char* wsm, int lane,
                                               const Chunk& c, const Regs& R, uint32_t S,
@@ -508,6 +528,13 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   // select-built scan (chunk.h find_parent_bidir SEL) per table form
   constexpr bool kSel = WIDE ? ANOMOD_SEL_LONG != 0
                              : (ST == kStWide ? ANOMOD_SEL_WIDE != 0 : ANOMOD_SEL_SN != 0);
+  // long-trace sets: ids staged as u32 planes, low words scanned (chunk.h
+  // find_parent_split)
+  constexpr bool kSplit =
+      UNI && kCoopSteps == 0 &&
+      (WIDE ? ANOMOD_SPLIT_LONG != 0 : (ST == kStWide ? ANOMOD_SPLIT_WIDE != 0 : ANOMOD_SPLIT_SN != 0));
+  auto* llo = reinterpret_cast<uint32_t*>(wsm + kWSid);
+  uint32_t* lhi = llo + (kStage + 16);
   if constexpr (ANOMOD_ABL & 16) {  // stream only: keep the loads, do nothing
     uint64_t x = 0;
 #pragma unroll
@@ -520,7 +547,12 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
-    lsid[i] = R.sid[r];
+    if constexpr (kSplit) {
+      llo[i] = (uint32_t)R.sid[r];
+      lhi[i] = (uint32_t)(R.sid[r] >> 32);
+    } else {
+      lsid[i] = R.sid[r];
+    }
     lsvc[i] = (uint16_t)R.sf[r];
   }
   uint64_t Sm[kPer];
@@ -548,9 +580,17 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       if constexpr (!(ANOMOD_ABL & 4)) {
         uint32_t a, b;
         trace_bounds(Sm, r, lane, c.n, a, b);
-        const int q = UNI ? (WIDE ? find_parent_bidir<kLFwd, kLBwd, 0, kSel>(lsid, a, b, i, R.pid[r])
-                                  : find_parent_bidir<kFwd, kBwd, 0, kSel>(lsid, a, b, i, R.pid[r]))
-                          : find_parent(lsid, a, b, R.pid[r]);
+        int q;
+        if constexpr (kSplit && WIDE)
+          q = find_parent_split<kLFwd, kLBwd>(llo, lhi, a, b, i, R.pid[r]);
+        else if constexpr (kSplit && ST == kStWide)
+          q = find_parent_split<kWFwd, kWBwd>(llo, lhi, a, b, i, R.pid[r]);
+        else if constexpr (kSplit)
+          q = find_parent_split<kFwd, kBwd>(llo, lhi, a, b, i, R.pid[r]);
+        else
+          q = UNI ? (WIDE ? find_parent_bidir<kLFwd, kLBwd, 0, kSel>(lsid, a, b, i, R.pid[r])
+                          : find_parent_bidir<kFwd, kBwd, 0, kSel>(lsid, a, b, i, R.pid[r]))
+                  : find_parent(lsid, a, b, R.pid[r]);
         if (q >= 0) p = lsvc[q];
       } else {  // ablation: a parent-like edge without the lookup (keeps key diversity)
         p = ((R.sf[r] & 0xFFFFu) + 1u + (uint32_t)(R.pid[r] & 1u)) % S;
