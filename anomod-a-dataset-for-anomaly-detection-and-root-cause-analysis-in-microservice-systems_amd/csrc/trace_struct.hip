@@ -44,6 +44,15 @@
 #ifndef ANOMOD_SEL_TS
 #define ANOMOD_SEL_TS 0  // select-built parent scan (chunk.h find_parent_bidir SEL)
 #endif
+#ifndef ANOMOD_SPLIT_TS
+#define ANOMOD_SPLIT_TS 0  // unique-id sets: split-word scan (chunk.h find_parent_split)
+#endif
+#ifndef ANOMOD_TS_FWD
+#define ANOMOD_TS_FWD 12
+#endif
+#ifndef ANOMOD_TS_BWD
+#define ANOMOD_TS_BWD 4
+#endif
 
 namespace anomod {
 namespace {
@@ -142,6 +151,9 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
                          const uint64_t (&sid)[kPer], const uint64_t (&pid)[kPer],
                          const uint32_t (&svc)[kPer], const TsOut& o) {
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kTSid);
+  constexpr bool kSplit = UNI && ANOMOD_SPLIT_TS != 0;
+  auto* llo = reinterpret_cast<uint32_t*>(wsm + kTSid);  // kSplit: u32 planes in the same area
+  uint32_t* lhi = llo + (kStage + 16);
   auto* lpid = reinterpret_cast<uint64_t*>(wsm + kTPid);
   auto* lnxt = reinterpret_cast<uint32_t*>(wsm + kTNxt);
   auto* ldst = reinterpret_cast<uint32_t*>(wsm + kTDst);
@@ -155,7 +167,12 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
     const uint32_t i = lane + r * kWave;
-    lsid[i] = sid[r];
+    if constexpr (kSplit) {
+      llo[i] = (uint32_t)sid[r];
+      lhi[i] = (uint32_t)(sid[r] >> 32);
+    } else {
+      lsid[i] = sid[r];
+    }
     lpid[i] = pid[r];
     lcnt[i] = 0u;
     lsvc[i] = (uint16_t)svc[r];
@@ -189,8 +206,14 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
         // i), and the parent reference has at most one match, found from
         // either end (chunk.h find_parent_bidir); no own-id scan
         f[r] = l = (int)i;
-        pf = pid[r] != 0ull ? find_parent_bidir<kFwd, kBwd, 0, ANOMOD_SEL_TS != 0>(lsid, a[r], b, i, pid[r])
-                            : -1;
+        if constexpr (kSplit)
+          pf = pid[r] != 0ull
+                   ? find_parent_split<ANOMOD_TS_FWD, ANOMOD_TS_BWD>(llo, lhi, a[r], b, i, pid[r])
+                   : -1;
+        else
+          pf = pid[r] != 0ull
+                   ? find_parent_bidir<kFwd, kBwd, 0, ANOMOD_SEL_TS != 0>(lsid, a[r], b, i, pid[r])
+                   : -1;
         np[r] = pf;
       } else {
         scan_ids(lsid, a[r], b, sid[r], pid[r], f[r], l, pf);
