@@ -528,8 +528,9 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
   // select-built scan (chunk.h find_parent_bidir SEL) per table form
   constexpr bool kSel = WIDE ? ANOMOD_SEL_LONG != 0
                              : (ST == kStWide ? ANOMOD_SEL_WIDE != 0 : ANOMOD_SEL_SN != 0);
-  // long-trace sets: ids staged as u32 planes, low words scanned (chunk.h
-  // find_parent_split)
+  // TrainTicket-width and long-trace sets with unique ids: ids staged as u32
+  // planes, low words scanned (chunk.h find_parent_split; it takes precedence
+  // over kSel)
   constexpr bool kSplit =
       UNI && kCoopSteps == 0 &&
       (WIDE ? ANOMOD_SPLIT_LONG != 0 : (ST == kStWide ? ANOMOD_SPLIT_WIDE != 0 : ANOMOD_SPLIT_SN != 0));
