@@ -757,7 +757,10 @@ constexpr int kBigThreads = kThreads;  // the tables' init / flush loops assume 
 constexpr uint32_t kBigMin = ANOMOD_BIG_MIN;
 constexpr uint32_t kBigWin = 2048;    // ids per table window
 constexpr uint32_t kBigSlots = 4096;  // table slots (load <= 0.5)
-constexpr int kBigPer = 8;            // spans per thread per lookup block
+#ifndef ANOMOD_BIG_PER
+#define ANOMOD_BIG_PER 8
+#endif
+constexpr int kBigPer = ANOMOD_BIG_PER;  // spans per thread per lookup block
 constexpr int kOffBigKey = kOffWave;                          // u64 [kBigSlots], 0 = empty
 constexpr int kOffBigPos = kOffBigKey + (int)kBigSlots * 8;   // u32 [kBigSlots]
 static_assert(kBigWin % kBigThreads == 0 && kBigWin <= 65536, "window: whole rows, position << 16 | svc");
