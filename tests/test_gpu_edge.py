@@ -103,6 +103,31 @@ def test_low_word_aliases(ctx, S, max_len):
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
 
 
+@pytest.mark.parametrize("S,long_set", [(46, False), (12, True)])
+def test_low_word_aliases_unique_ids(ctx, monkeypatch, S, long_set):
+    """Unique ids (so the split-word scan runs: TrainTicket width, and the
+    long-trace instantiation for a set holding a trace over 256 spans) whose
+    low 32-bit words collide inside the trace: a low-word candidate whose
+    high word differs must not count — the scan falls back to the exact one.
+    Collector order and shuffled inside the traces.  Equal to the oracle."""
+    if long_set:
+        monkeypatch.setenv("ANOMOD_HIST_FORM", "compact")
+    rng = np.random.default_rng(500 + S)
+    parts = [_random_spanset(rng, S, 3000, 60, lo_alias=True)]
+    if long_set:
+        parts.append(_random_spanset(rng, S, 0, 0, lo_alias=True,
+                                     lens=rng.integers(100, 257, 300)))
+        parts.append(_random_spanset(rng, S, 0, 0, lo_alias=True, lens=[300]))
+    sp = anomod.SpanSet.concat(parts)
+    assert sp.check_unique_ids()
+    dev = ctx.upload(sp)
+    assert_table_equal(ctx.edge_aggregate(dev), native.edge_aggregate(sp))
+    shuf = ctx.shuffle(dev, seed=11, window_traces=0)
+    assert_table_equal(ctx.edge_aggregate(shuf), native.edge_aggregate(shuf.download()))
+    shuf.free()
+    dev.free()
+
+
 @pytest.mark.parametrize("S,lens", [(46, (30, 200)), (46, (1, 25)), (12, (30, 200))])
 def test_fingerprint_collisions(ctx, S, lens):
     """Ids crafted so that EVERY id of the set — orphan references included —
