@@ -29,6 +29,10 @@ _STATUS = {EINVAL: "EINVAL", EHIP: "EHIP", ERCCL: "ERCCL", ENOMEM: "ENOMEM", EST
 
 (STAGE_EDGE_AGG, STAGE_EDGE_FINAL, STAGE_EDGE_REDUCE, STAGE_EWMA, STAGE_PAGERANK,
  STAGE_TRACE_STRUCT, STAGE_SEGMENTS, STAGE_SUMMARY, STAGE_GROUP) = range(9)
+(HOST_GROUP_ALLOC, HOST_GROUP_PINNED, HOST_GROUP_WALL, HOST_UPLOAD_SETUP,
+ HOST_SET_ALLOC) = range(5)
+HOST_SLOTS = 5
+HOST_SLOT_NAMES = ("group_alloc", "group_pinned", "group_wall", "upload_setup", "set_alloc")
 NO_PARENT = 0xFFFFFFFF
 SPAN_ROOT, SPAN_FIRST = 0x1, 0x2
 
@@ -146,6 +150,7 @@ _SIGS = {
     "anomod_ctx_destroy": (_i32, [_vp]),
     "anomod_ctx_synchronize": (_i32, [_vp]),
     "anomod_ctx_stage_ms": (_i32, [_vp, _i32, _P(_f64)]),
+    "anomod_ctx_host_ms": (_i32, [_vp, _i32, _P(_f64), _P(_u64)]),
     "anomod_hist_bin": (_u32, [_u32]),
     "anomod_hist_bin_bounds": (_i32, [_u32, _P(_u32), _P(_u32)]),
     "anomod_spans_upload": (_i32, [_vp, _P(SpanSoA), _u64, _P(_u64), _u64, _P(_vp)]),

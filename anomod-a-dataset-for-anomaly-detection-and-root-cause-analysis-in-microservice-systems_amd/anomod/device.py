@@ -196,6 +196,17 @@ class Context:
         self._check(self._lib.anomod_ctx_stage_ms(self.handle, stage, C.byref(v)))
         return v.value
 
+    def host_ms(self) -> dict:
+        """Host wall milliseconds of the last occurrence of each one-off setup
+        step / host-side call phase (anomod_ctx_host_ms) and how many times it
+        happened: {name: (ms, count)}."""
+        out = {}
+        for slot, name in enumerate(L.HOST_SLOT_NAMES):
+            v, c = C.c_double(), C.c_uint64()
+            self._check(self._lib.anomod_ctx_host_ms(self.handle, slot, C.byref(v), C.byref(c)))
+            out[name] = (v.value, c.value)
+        return out
+
     def group_info(self) -> dict:
         """How the last grouping ran: path ("bucket" / "join": the bucket
         scatters then the ungrouped aggregation's per-bucket hash join /
@@ -333,21 +344,15 @@ class Context:
                 table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
             spans.scan_order, spans.hist_form = order.value, form.value
             return table
-        tmp = host = None
-        try:
-            table = EdgeTable.empty(spans.services, with_hist)
-            cs = table.c_struct()
-            fn = (self._lib.anomod_edge_aggregate_spans if spans.grouped
-                  else self._lib.anomod_edge_aggregate_ungrouped)
-            self._check(fn(self.handle, spans.handle, len(spans.services), C.byref(cs)))
-            if table.hist is not None:
-                table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
-            if host is not None:
-                host.scan_order, host.hist_form = tmp.hints
-            return table
-        finally:
-            if tmp is not None:
-                tmp.free()
+        # a device set: its hints live on the set itself (libanomod keeps them)
+        table = EdgeTable.empty(spans.services, with_hist)
+        cs = table.c_struct()
+        fn = (self._lib.anomod_edge_aggregate_spans if spans.grouped
+              else self._lib.anomod_edge_aggregate_ungrouped)
+        self._check(fn(self.handle, spans.handle, len(spans.services), C.byref(cs)))
+        if table.hist is not None:
+            table.hist = table.hist.reshape(edge_rows(len(spans.services)), L.HIST_BINS)
+        return table
 
     def edge_quantiles_exact(self, spans: DeviceSpans | SpanSet, q_pct=(50, 99)):
         """Exact per-edge order statistics x[(c*q)//100] of the sorted edge

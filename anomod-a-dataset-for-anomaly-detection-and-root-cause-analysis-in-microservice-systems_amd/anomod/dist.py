@@ -91,9 +91,10 @@ def _reduce(parts: list[np.ndarray], op: int) -> np.ndarray:
     raise ValueError(f"unknown reduction op {op}")
 
 
-def _link_options(sock: socket.socket, timeout_s: float) -> None:
-    """A formed peer link: every recv bounded by timeout_s, TCP keepalive on
-    (probes after 30 s idle, every 10 s, 6 unanswered = dead link)."""
+def _link_options(sock: socket.socket, timeout_s: float | None) -> None:
+    """A formed peer link: every recv bounded by timeout_s (None: unbounded),
+    TCP keepalive on (probes after 30 s idle, every 10 s, 6 unanswered = dead
+    link)."""
     sock.settimeout(timeout_s)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE, 1)
     for name, v in (("TCP_KEEPIDLE", 30), ("TCP_KEEPINTVL", 10), ("TCP_KEEPCNT", 6)):
@@ -112,14 +113,17 @@ class HostGroup:
     def __init__(self, rank: int, world: int, key: str | None = None,
                  timeout_s: float | None = None, rdzv_dir: str | None = None,
                  coll_timeout_s: float | None = None):
-        """timeout_s bounds the rendezvous (ANOMOD_RCCL_TIMEOUT_S, 300 s);
-        once the group is formed a collective waits coll_timeout_s for a peer
-        (ANOMOD_HOSTGROUP_TIMEOUT_S; default 10 x timeout_s, so a barrier
-        behind a slow rank still passes) and then raises TimeoutError.  A rank
-        that exits closes its socket, which every peer sees at once; a rank
-        stuck in a GPU call or a lost host sends nothing, which the timeout
-        and TCP keepalive on every peer link turn into an error instead of a
-        wait without end."""
+        """timeout_s bounds the rendezvous (ANOMOD_RCCL_TIMEOUT_S, 300 s).
+        Once the group is formed a collective waits for its peers without a
+        bound by default, so a barrier behind a rank busy with local work for
+        any time still passes; coll_timeout_s (or ANOMOD_HOSTGROUP_TIMEOUT_S)
+        bounds that wait, after which it raises TimeoutError.  A rank that
+        exits closes its socket, which every peer sees at once; a lost host
+        stops answering TCP keepalive on every peer link (probes after 30 s,
+        dead after ~90 s), which ends the wait with an error.  A collective
+        that fails (timeout, closed or dead link) closes the group: a frame
+        may have been cut, so later collectives raise ConnectionError instead
+        of reading a misaligned stream."""
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"bad rank {rank} of world {world}")
         self.rank, self.world = rank, world
@@ -127,10 +131,11 @@ class HostGroup:
                                else os.environ.get("ANOMOD_RCCL_TIMEOUT_S", "300"))
         if coll_timeout_s is None:
             env = os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S")
-            coll_timeout_s = float(env) if env else 10.0 * self.timeout_s
-        if not coll_timeout_s > 0:
+            coll_timeout_s = float(env) if env else None
+        if coll_timeout_s is not None and not coll_timeout_s > 0:
             raise ValueError(f"collective timeout must be > 0 s, got {coll_timeout_s}")
-        self.coll_timeout_s = float(coll_timeout_s)
+        self.coll_timeout_s = None if coll_timeout_s is None else float(coll_timeout_s)
+        self.broken: str | None = None  # why a failed collective closed the group
         self._peers: list[socket.socket] = []  # rank 0: ranks 1..world-1 in order
         self._sock: socket.socket | None = None  # other ranks: the link to rank 0
         self._file: Path | None = None
@@ -218,6 +223,9 @@ class HostGroup:
         to every rank."""
         if self.world == 1:
             return combine([payload])
+        if self.broken is not None:
+            raise ConnectionError(f"anomod host group: closed after a failed collective "
+                                  f"({self.broken})")
         try:
             if self.rank == 0:
                 out = combine([payload] + [_recv(c) for c in self._peers])
@@ -227,9 +235,22 @@ class HostGroup:
             _send(self._sock, payload)
             return _recv(self._sock)
         except socket.timeout:
+            self._fail("timeout")
             raise TimeoutError(f"anomod host group: rank {self.rank} of {self.world} waited "
                                f"{self.coll_timeout_s:.0f} s for a peer in a collective "
                                f"(ANOMOD_HOSTGROUP_TIMEOUT_S)") from None
+        except (OSError, ConnectionError) as e:
+            self._fail(type(e).__name__)
+            raise
+
+    def _fail(self, why: str) -> None:
+        """A collective failed part-way: its frames may be cut, so the links
+        are closed and the group refuses later collectives."""
+        self.broken = why
+        for c in self._peers:
+            c.close()
+        if self._sock is not None:
+            self._sock.close()
 
     def broadcast(self, data: bytes | None, src: int = 0) -> bytes:
         """src's bytes on every rank."""

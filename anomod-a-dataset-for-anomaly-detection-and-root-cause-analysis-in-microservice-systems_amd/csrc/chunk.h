@@ -175,6 +175,10 @@ __device__ __forceinline__ uint32_t trace_in_chunk(const uint64_t (&Sm)[kPer], i
 #endif
 constexpr uint32_t kFwd = ANOMOD_FWD, kBwd = ANOMOD_BWD;
 static_assert(kFwd % 2 == 0 && kBwd % 2 == 0 && kFwd + kBwd <= 16, "bidirectional step");
+// Ids are staged with this many entries of slack past the chunk (edge_agg.hip
+// kWSid, trace_struct.hip kTSid): a forward block may read that far past the
+// trace end, so no forward block is wider.
+constexpr uint32_t kScanSlack = 16;
 
 // MAXS > 0: give up after that many steps and return -2 (not found yet; the
 // caller completes the lookup cooperatively).
@@ -186,7 +190,8 @@ template <uint32_t FW = kFwd, uint32_t BW = kBwd, int MAXS = 0, bool SEL = false
 __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t a, uint32_t b,
                                                  uint32_t i, uint64_t pid) {
   int steps = 0;
-  static_assert(FW % 2 == 0 && BW % 2 == 0 && FW <= 32 && BW <= 32, "bidirectional step");
+  // FW: the staging slack; BW < 32: the mask form shifts 1u by up to BW
+  static_assert(FW % 2 == 0 && BW % 2 == 0 && FW <= kScanSlack && BW < 32, "bidirectional step");
   uint32_t f = a;             // next forward block [f, f + FW)
   int32_t g = (int32_t)i - 1;  // backward blocks end at g (inclusive)
   while (true) {
@@ -237,6 +242,7 @@ __device__ __forceinline__ int find_parent_bidir(const uint64_t* lsid, uint32_t 
 template <uint32_t FW, uint32_t BW>
 __device__ __forceinline__ int find_parent_split(const uint32_t* lo, const uint32_t* hi, uint32_t a,
                                                  uint32_t b, uint32_t i, uint64_t pid) {
+  static_assert(FW <= kScanSlack && BW < 32, "split-word step: the staging slack");
   const uint32_t plo = (uint32_t)pid, phi = (uint32_t)(pid >> 32);
   uint32_t f = a;
   int32_t g = (int32_t)i - 1;

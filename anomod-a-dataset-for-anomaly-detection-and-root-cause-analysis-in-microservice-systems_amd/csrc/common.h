@@ -35,6 +35,12 @@ enum Stage { kStageEdgeAgg = 0, kStageEdgeFinal = 1, kStageEdgeReduce = 2, kStag
              kStagePagerank = 4, kStageTraceStruct = 5, kStageSegments = 6, kStageSummary = 7,
              kStageGroup = 8, kNumStages = 9 };
 
+// Host wall-clock slots (anomod_ctx_host_ms): the last occurrence of each
+// one-off setup step, or of a call phase the stage events cannot see.
+enum HostSlot { kHostGroupAlloc = ANOMOD_HOST_GROUP_ALLOC, kHostGroupPinned = ANOMOD_HOST_GROUP_PINNED,
+                kHostGroupWall = ANOMOD_HOST_GROUP_WALL, kHostUploadSetup = ANOMOD_HOST_UPLOAD_SETUP,
+                kHostSetAlloc = ANOMOD_HOST_SET_ALLOC, kNumHostSlots = ANOMOD_HOST_SLOTS };
+
 }  // namespace anomod
 
 struct anomod_ctx {
@@ -44,6 +50,8 @@ struct anomod_ctx {
   hipEvent_t ev_begin[anomod::kNumStages] = {};
   hipEvent_t ev_end[anomod::kNumStages] = {};
   bool stage_recorded[anomod::kNumStages] = {};
+  double host_ms[anomod::kNumHostSlots] = {};        // anomod_ctx_host_ms
+  uint64_t host_count[anomod::kNumHostSlots] = {};
   std::string err;
   // RCCL communicator (one process per GPU) ...
   ncclComm_t comm = nullptr;
@@ -158,6 +166,9 @@ int bind(anomod_ctx* ctx);
 // hipEvent bracketing of a stage on the ctx stream.
 int stage_begin(anomod_ctx* ctx, Stage s);
 int stage_end(anomod_ctx* ctx, Stage s);
+// Host wall clock (ms since an arbitrary origin) and the record of a slot.
+double host_now_ms();
+void host_record(anomod_ctx* ctx, HostSlot s, double ms);
 // Wait for the ctx stream.  With a communicator attached, RCCL's async
 // error state is polled while waiting and the communicator is aborted on an
 // error or after ctx->comm_timeout_s (a dead peer must not hang the rank).

@@ -44,6 +44,16 @@ int stage_end(anomod_ctx* ctx, Stage s) {
   return ANOMOD_OK;
 }
 
+double host_now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void host_record(anomod_ctx* ctx, HostSlot s, double ms) {
+  ctx->host_ms[s] = ms;
+  ++ctx->host_count[s];
+}
+
 namespace {
 void abort_comm(anomod_ctx* ctx) {
   if (ctx->comm && !ctx->comm_aborted) {
@@ -383,6 +393,14 @@ int anomod_ctx_stage_ms(const anomod_ctx* cctx, int stage, double* ms) {
   float f = 0.f;
   ANOMOD_HIP(ctx, hipEventElapsedTime(&f, ctx->ev_begin[stage], ctx->ev_end[stage]));
   *ms = (double)f;
+  return ANOMOD_OK;
+}
+
+int anomod_ctx_host_ms(const anomod_ctx* ctx, int slot, double* ms, uint64_t* count) {
+  ANOMOD_REQUIRE(nullptr, ctx != nullptr && ms != nullptr, "anomod_ctx_host_ms: NULL argument");
+  ANOMOD_REQUIRE(nullptr, slot >= 0 && slot < anomod::kNumHostSlots, "unknown host slot %d", slot);
+  *ms = ctx->host_ms[slot];
+  if (count) *count = ctx->host_count[slot];
   return ANOMOD_OK;
 }
 

@@ -122,8 +122,8 @@ constexpr uint32_t kSatFails = 64;
 // kModeWideScan: kModeNormal with the wide parent scan (process_chunk)
 enum LaunchMode : uint32_t { kModeNormal = 0, kModeAuto = 1, kModeResume = 2, kModeWideScan = 3 };
 enum StatsForm { kStHbm = 0, kStDirect = 1, kStSlot = 2, kStWide = 3 };
-constexpr int kWSid = 0;                          // u64 span ids [kStage + 16] (scan slack)
-constexpr int kWSvc = kWSid + (kStage + 16) * 8;  // u16 services [kStage + 8]
+constexpr int kWSid = 0;                          // u64 span ids [kStage + kScanSlack] (scan slack)
+constexpr int kWSvc = kWSid + (kStage + chunk::kScanSlack) * 8;  // u16 services [kStage + 8]
 constexpr int kWFlag = kWSvc + (kStage + 8) * 2;  // u8 trace-start flags [kStage]
 constexpr int kWAuto = kWFlag + kStage;           // u64: kModeAuto, first trace of the chunk
 constexpr int kWBytes = kWAuto + 16;
@@ -535,7 +535,7 @@ __device__ __forceinline__ void process_chunk(unsigned char* smem, unsigned char
       UNI && kCoopSteps == 0 &&
       (WIDE ? ANOMOD_SPLIT_LONG != 0 : (ST == kStWide ? ANOMOD_SPLIT_WIDE != 0 : ANOMOD_SPLIT_SN != 0));
   auto* llo = reinterpret_cast<uint32_t*>(wsm + kWSid);
-  uint32_t* lhi = llo + (kStage + 16);
+  uint32_t* lhi = llo + (kStage + chunk::kScanSlack);
   if constexpr (ANOMOD_ABL & 16) {  // stream only: keep the loads, do nothing
     uint64_t x = 0;
 #pragma unroll
@@ -1740,6 +1740,9 @@ void probe_order_take(const anomod_spans* s, const unsigned long long* h) {
 // wait, the first aggregation of the set only).
 int probe_order(anomod_ctx* ctx, const anomod_spans* s, unsigned long long* d_cnt) {
   if (!need_order_probe(s)) return ANOMOD_OK;
+  // the pinned read-back (a ctx's first call may be this one: the exact
+  // quantiles allocate no staging of their own)
+  if (int rc = ensure_host_stage(ctx, 32)) return rc;
   unsigned long long* h = static_cast<unsigned long long*>(ctx->h_stage);
   if (int rc = probe_order_launch(ctx, s, d_cnt, h)) return rc;
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -654,7 +654,9 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   constexpr size_t kAlign = size_t(2) << 20;
   size_t total = 0;
   for (size_t z : sizes) total += (z + kAlign - 1) / kAlign * kAlign;
+  double t0 = host_now_ms();
   bool ok = hipMalloc(&ws->block, total) == hipSuccess;
+  host_record(ctx, kHostGroupAlloc, host_now_ms() - t0);
   if (ok) {
     size_t off = 0;
     for (int i = 0; i < kBufs; ++i) {
@@ -668,8 +670,10 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   } else {
     ws->block = nullptr;
   }
+  t0 = host_now_ms();
   ok = ok && hipHostMalloc(reinterpret_cast<void**>(&ws->h_misc), kMiscWords * 8,
                            hipHostMallocDefault) == hipSuccess;
+  host_record(ctx, kHostGroupPinned, host_now_ms() - t0);
   if (!ok) {
     free_group_ws(ctx);
     set_error(ctx, "hipMalloc failed for the trace-grouping workspace of %llu spans "
@@ -936,8 +940,10 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
     bool fallback = true;
     if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
     if (rc == ANOMOD_OK) {
+      const double t0 = host_now_ms();
       uint64_t* erec = reinterpret_cast<uint64_t*>(ctx->group_ws->aos[1]);
       rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
+      host_record(ctx, kHostGroupWall, host_now_ms() - t0);
       if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);
       if (rc == ANOMOD_OK && !fallback) {
         ctx->group_path = g.join ? 2 : 3;  // join / fused-sort

@@ -729,10 +729,14 @@ int anomod_edge_aggregate_host(anomod_ctx* ctx, const anomod_span_soa* soa, uint
                                anomod_edge_table* out) {
   ANOMOD_REQUIRE(nullptr, ctx && soa && out && scan_order && hist_form,
                  "anomod_edge_aggregate_host: NULL argument");
-  ANOMOD_REQUIRE(ctx, *scan_order >= -1 && *scan_order <= 1 && *hist_form >= -1 && *hist_form <= 1,
-                 "scan_order=%d / hist_form=%d outside [-1, 1]", *scan_order, *hist_form);
   uint64_t max_len = 0;
-  int local = check_upload(ctx, soa, n_spans, trace_ptr, n_traces, &max_len);
+  // every check goes through `local`: the hints come from this rank's own
+  // host set, so a bad one on one rank must reach comm_agree too
+  int local = ANOMOD_OK;
+  ANOMOD_CHECK_LOCAL(ctx, local,
+                     *scan_order >= -1 && *scan_order <= 1 && *hist_form >= -1 && *hist_form <= 1,
+                     "scan_order=%d / hist_form=%d outside [-1, 1]", *scan_order, *hist_form);
+  if (local == ANOMOD_OK) local = check_upload(ctx, soa, n_spans, trace_ptr, n_traces, &max_len);
   if (local == ANOMOD_OK) local = bind(ctx);
   // the ctx's grow-only set: no trace_hash (a grouped aggregation reads none)
   if (local == ANOMOD_OK &&
@@ -744,7 +748,9 @@ int anomod_edge_aggregate_host(anomod_ctx* ctx, const anomod_span_soa* soa, uint
     }
     const uint64_t cs = std::max<uint64_t>(n_spans, ctx->host_set_spans);
     const uint64_t ct = std::max<uint64_t>(n_traces, ctx->host_set_traces);
+    const double t0 = host_now_ms();
     local = alloc_spans(ctx, cs, ct, false, &ctx->host_set);
+    host_record(ctx, kHostSetAlloc, host_now_ms() - t0);
     ctx->host_set_spans = local == ANOMOD_OK ? cs : 0;
     ctx->host_set_traces = local == ANOMOD_OK ? ct : 0;
   }

@@ -69,8 +69,8 @@ constexpr int kTsThreads = kTsWaves * kWave;
 constexpr uint32_t kDone = 0x80000000u;  // pointer-jumping: chain reached a root
 
 // Per-wave LDS carve (bytes; 16-B aligned offsets).
-constexpr int kTSid = 0;                          // u64 span ids   [kStage + 16] (scan slack)
-constexpr int kTPid = kTSid + (kStage + 16) * 8;  // u64 parent refs [kStage]
+constexpr int kTSid = 0;                          // u64 span ids   [kStage + kScanSlack] (scan slack)
+constexpr int kTPid = kTSid + (kStage + chunk::kScanSlack) * 8;  // u64 parent refs [kStage]
 constexpr int kTNxt = kTPid + kStage * 8;         // u32 jump target | kDone [kStage]
 constexpr int kTDst = kTNxt + kStage * 4;         // u32 distance to the target [kStage]
 constexpr int kTCnt = kTDst + kStage * 4;         // u32 child counts [kStage]
@@ -153,7 +153,7 @@ __device__ void ts_chunk(unsigned char* wsm, int lane, const Chunk& c, uint64_t 
   auto* lsid = reinterpret_cast<uint64_t*>(wsm + kTSid);
   constexpr bool kSplit = UNI && ANOMOD_SPLIT_TS != 0;
   auto* llo = reinterpret_cast<uint32_t*>(wsm + kTSid);  // kSplit: u32 planes in the same area
-  uint32_t* lhi = llo + (kStage + 16);
+  uint32_t* lhi = llo + (kStage + chunk::kScanSlack);
   auto* lpid = reinterpret_cast<uint64_t*>(wsm + kTPid);
   auto* lnxt = reinterpret_cast<uint32_t*>(wsm + kTNxt);
   auto* ldst = reinterpret_cast<uint32_t*>(wsm + kTDst);

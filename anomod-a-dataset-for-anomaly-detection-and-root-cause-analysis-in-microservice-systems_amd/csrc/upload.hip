@@ -96,6 +96,7 @@ namespace {
 
 int make_uploader(anomod_ctx* ctx) {
   if (ctx->uploader) return ANOMOD_OK;
+  const double t0 = host_now_ms();
   auto* u = new Uploader();
   u->device = ctx->device;
   const char* e = std::getenv("ANOMOD_UPLOAD_THREADS");
@@ -124,6 +125,7 @@ int make_uploader(anomod_ctx* ctx) {
     return ANOMOD_ENOMEM;
   }
   for (int w = 0; w < nw; ++w) u->th.emplace_back([u, w] { u->work(w); });
+  host_record(ctx, kHostUploadSetup, host_now_ms() - t0);
   return ANOMOD_OK;
 }
 

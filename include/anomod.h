@@ -121,6 +121,20 @@ int anomod_ctx_synchronize(anomod_ctx* ctx);
  * 7 = value summary (select + sort + sum + picks),
  * 8 = trace grouping of an ungrouped span set (radix passes + copy + trace_ptr). */
 int anomod_ctx_stage_ms(const anomod_ctx* ctx, int stage, double* ms);
+/* Host wall milliseconds of the last occurrence of a one-off setup step or of
+ * a call phase the stage events above cannot see, and how many times it
+ * happened on this ctx (count may be NULL; a caller compares counts around a
+ * call to learn whether that call paid it).  Slots: */
+#define ANOMOD_HOST_GROUP_ALLOC 0  /* grouping workspace: device hipMalloc     */
+#define ANOMOD_HOST_GROUP_PINNED 1 /* grouping workspace: pinned read-back     */
+#define ANOMOD_HOST_GROUP_WALL 2   /* an ungrouped aggregation's grouping:
+                                      first launch to counters read back       */
+#define ANOMOD_HOST_UPLOAD_SETUP 3 /* upload pipeline: threads, streams, pinned
+                                      buffers                                  */
+#define ANOMOD_HOST_SET_ALLOC 4    /* the device set anomod_edge_aggregate_host
+                                      keeps: (re)allocation                    */
+#define ANOMOD_HOST_SLOTS 5
+int anomod_ctx_host_ms(const anomod_ctx* ctx, int slot, double* ms, uint64_t* count);
 
 /* ---- histogram helpers (host) ------------------------------------------- */
 uint32_t anomod_hist_bin(uint32_t v);
@@ -512,7 +526,7 @@ int anomod_graph_last_solve(const anomod_graph* g, uint32_t* path, uint32_t* fal
  * order).  tol > 0: each vector stops at its own convergence iteration
  * (later iterations carry it unchanged); iters_done = iterations run.  One
  * persistent launch (grid barrier) when the batch's workgroups are all
- * resident (N = 10^5: K <= 8), else one launch per iteration.             */
+ * resident (N = 10^5: K <= 16), else one launch per iteration.             */
 int anomod_graph_pagerank_batch(anomod_ctx* ctx, anomod_graph* g, const double* P, uint32_t K,
                                 double alpha, uint32_t iters, double tol, double* X,
                                 uint32_t* iters_done);

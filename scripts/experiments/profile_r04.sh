@@ -1,5 +1,5 @@
 #!/bin/bash
-# r05 profile: the bench process itself under rocprofv3 (kernel trace +
+# r04 profile: the bench process itself under rocprofv3 (kernel trace +
 # stats: the headline kernel's dispatch times and the printed line come from
 # ONE process), then PMC passes (HBM bytes; SQ / LDS counters) over a reduced
 # bench that runs every leg whose kernels the summary names.  Each GPU step
@@ -7,7 +7,7 @@
 # usage (on the box): bash scripts/experiments/profile_r04.sh [OUT]
 cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
-OUT=${1:-$GRAFT_REPO_ROOT/gpurun_out/r05prof}
+OUT=${1:-$GRAFT_REPO_ROOT/gpurun_out/r04prof}
 mkdir -p "$OUT"
 BENCH_ARGS=${BENCH_ARGS:-"--gpus 1 --steps 20 --warmup 5"}
 if [ "${TRACE:-1}" = 1 ]; then

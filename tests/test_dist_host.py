@@ -173,7 +173,7 @@ def test_silent_peer_times_out(tmp_path):
     from anomod import dist
 
     key, errs, formed, release = f"silent{os.getpid()}", {}, threading.Event(), threading.Event()
-    groups = {}
+    groups, keepalive = {}, {}
 
     def rank(r):
         try:
@@ -185,6 +185,7 @@ def test_silent_peer_times_out(tmp_path):
                 release.wait(30)  # silent: socket open, no collective
             else:
                 formed.wait(30)
+                keepalive[r] = g._peers[0].getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE)
                 g.barrier()
         except Exception as e:  # noqa: BLE001
             errs[r] = e
@@ -197,10 +198,15 @@ def test_silent_peer_times_out(tmp_path):
     ts[1].join(30)
     assert isinstance(errs.get(0), TimeoutError), errs
     assert 1 not in errs
-    link = groups[0]._peers[0]
-    assert link.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
+    assert keepalive[0] == 1
     assert groups[0].coll_timeout_s == 1.5
+    # the timed-out group is closed: a later collective fails at once instead
+    # of reading a stream a cut frame may have misaligned
+    assert groups[0].broken == "timeout"
+    with pytest.raises(ConnectionError):
+        groups[0].barrier()
     for g in groups.values():
         g.close()
-    assert dist.HostGroup(0, 1).coll_timeout_s == 10 * 300.0 or os.environ.get(
-        "ANOMOD_HOSTGROUP_TIMEOUT_S") or os.environ.get("ANOMOD_RCCL_TIMEOUT_S")
+    # unbounded by default: a barrier behind a rank busy for any time passes
+    if not os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S"):
+        assert dist.HostGroup(0, 1).coll_timeout_s is None

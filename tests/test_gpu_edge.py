@@ -312,6 +312,28 @@ def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
         np.testing.assert_array_equal(tab[qq][ok], [0.5 * (lo + hi) for lo, hi in b])
 
 
+def test_exact_quantiles_first_call_on_new_context():
+    """The exact quantiles as a fresh context's first call on a unique-id set
+    whose scan order is not known yet: the order probe needs the pinned
+    read-back the aggregation would otherwise have allocated (ADVICE r05:
+    it wrote through a null staging pointer)."""
+    with anomod.Context(0) as maker:
+        gen = maker.generate(anomod.SynthSpec("SN", seed=7, p_orphan_ppm=100), 4096)
+        host = gen.download()
+        gen.free()
+    assert host.unique_ids
+    host.scan_order = -1  # order unknown: the exact quantiles' probe runs
+    with anomod.Context(0) as fresh:
+        dev = fresh.upload(host)
+        assert dev.hints[0] == -1
+        got, cnt = fresh.edge_quantiles_exact(dev, (50, 99))
+        assert dev.hints[0] in (0, 1)
+        dev.free()
+    want = native.exact_quantiles(host, (50, 99))
+    np.testing.assert_array_equal(got, want)
+    assert int(cnt.sum()) == host.n_spans
+
+
 @pytest.mark.parametrize("form", ["pair", "compact", "auto"])
 @pytest.mark.parametrize("S", [14, 46])
 def test_histogram_forms(ctx, monkeypatch, form, S):
