@@ -627,6 +627,79 @@ __global__ __launch_bounds__(kBThreads) void bk_scatter_b_fast_kernel(
   }
 }
 
+// ---- level B moving the records too (ANOMOD_JOIN_RECB=1, r06 A/B) -------------
+// The fast scatter above, plus each pair's 32-B record: read by the pair's
+// level-A position (inside the tile's own 16384 records, 512 KiB that one
+// workgroup brings into L2 once) and written beside the pair at its level-B
+// position, so the join reads its bucket's records contiguously instead of
+// gathering one 128-B line per span.  Bytes per span: 8 + 32 in, 8 + 32 out
+// (against 8 + 8), for a join that reads 8 + 32 contiguously.
+__global__ __launch_bounds__(kBThreads) void bk_scatter_b_rec_kernel(
+    const uint64_t* __restrict__ pin, uint64_t* __restrict__ pout, const GRec* __restrict__ rin,
+    GRec* __restrict__ rout, int db, const uint32_t* __restrict__ toff,
+    const uint32_t* __restrict__ bsA, const uint32_t* __restrict__ btile,
+    const uint32_t* __restrict__ tmap, int na, uint32_t nx) {
+  __shared__ uint64_t stage[kPTile];
+  __shared__ uint32_t lcnt[kNDMax];
+  __shared__ uint32_t delta[kNDMax];
+  __shared__ uint32_t wsum[kBWaves];
+  const int tid = threadIdx.x, lane = tid & (kWv - 1), w = tid / kWv;
+  const int nd = 1 << db, shift = 64 - db;
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x, nx);
+  uint64_t base, nvalid;
+  if (!seg_tile(tile, bsA, btile, tmap, na, &base, &nvalid)) return;
+  uint64_t x[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane);
+    x[k] = loc < nvalid ? pin[base + loc] : 0ull;
+  }
+  for (int dd = tid; dd < nd; dd += kBThreads) lcnt[dd] = 0u;
+  __syncthreads();
+  uint32_t off[kPPer];
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k) {
+    const uint32_t loc = (uint32_t)(w * (kPPer * kWv) + k * kWv + lane);
+    off[k] = loc < nvalid ? atomicAdd(&lcnt[(uint32_t)(x[k] >> shift)], 1u) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  const int dpt = nd > kBThreads ? nd / kBThreads : 1;
+  uint32_t c[2] = {0u, 0u};
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd < nd) c[i] = lcnt[dd];
+  }
+  uint32_t all;
+  const uint32_t pre = block_excl_scan<kBWaves>(c[0] + c[1], wsum, &all);
+  for (int i = 0; i < dpt; ++i) {
+    const int dd = tid * dpt + i;
+    if (dd >= nd) continue;
+    const uint32_t ts = pre + (i ? c[0] : 0u);
+    lcnt[dd] = ts;
+    delta[dd] = toff[tile * nd + dd] - ts;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPPer; ++k)
+    if (off[k] != 0xFFFFFFFFu) stage[lcnt[(uint32_t)(x[k] >> shift)] + off[k]] = x[k];
+  __syncthreads();
+  const uint4* rq = reinterpret_cast<const uint4*>(rin);
+  uint4* wq = reinterpret_cast<uint4*>(rout);
+#pragma unroll 4
+  for (int j = 0; j < kPPer; ++j) {
+    const uint32_t cc = (uint32_t)(tid + j * kBThreads);
+    if (cc < nvalid) {
+      const uint64_t y = stage[cc];
+      const uint64_t g = (uint64_t)(uint32_t)(delta[(uint32_t)(y >> shift)] + cc);
+      const uint64_t src = (uint32_t)y;  // the record's level-A position
+      const uint4 r0 = rq[2 * src], r1 = rq[2 * src + 1];
+      pout[g] = y;
+      wq[2 * g] = r0;
+      wq[2 * g + 1] = r1;
+    }
+  }
+}
+
 // ---- one bucket in (k, arrival) order ---------------------------------------
 template <int W, int PER, bool EDGE = false>
 struct BucketLds {
@@ -1465,7 +1538,7 @@ __device__ __forceinline__ uint32_t slot_cas(uint32_t* tab, uint32_t s, uint32_t
 // One bucket [a0, a0 + m) of the level-B pairs `pin` joined in LDS; every
 // thread of the workgroup calls it.  The records come from `rec` by the pairs'
 // level-A positions.
-template <int W, int PER, bool PACK, bool T16 = true>
+template <int W, int PER, bool PACK, bool T16 = true, bool CONTIG = false>
 __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uint32_t m,
                                             const uint64_t* __restrict__ pin,
                                             const GRec* __restrict__ rec, EdgeOut eo) {
@@ -1486,8 +1559,8 @@ __device__ __forceinline__ void join_bucket(unsigned char* lds, uint32_t a0, uin
   }
   uint4 ra[PER], rb[PER];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {  // the gathers: issued together
-    const uint4* q = reinterpret_cast<const uint4*>(rec + ap[j]);
+  for (int j = 0; j < PER; ++j) {  // the gathers (CONTIG: the bucket's own records) together
+    const uint4* q = reinterpret_cast<const uint4*>(rec + (CONTIG ? a0 + p[j] : ap[j]));
     ra[j] = v[j] ? q[0] : make_uint4(0, 0, 0, 0);
     rb[j] = v[j] ? q[1] : make_uint4(0, 0, 0, 0);
   }
@@ -1588,7 +1661,7 @@ constexpr int join_big_per(bool pack) { return pack ? 8 : 4; }  // 8 192 / 4 096
 // MINW: waves per SIMD the registers must allow (6 = three 512-thread
 // workgroups per CU; 8 = four, 64 VGPRs with 28 B per lane spilled); T16: u16
 // table slots (PACK at 2 048 spans: 40 KiB, else 48).
-template <bool PACK, int MINW = 6, bool T16 = !PACK>
+template <bool PACK, int MINW = 6, bool T16 = !PACK, bool CONTIG = false>
 __global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, uint32_t* __restrict__ over,
@@ -1607,13 +1680,13 @@ __global__ __launch_bounds__(kJoinW, MINW) void bk_join_kernel(
     return;
   }
   if (m == 0) return;
-  join_bucket<kJoinW, kJoinPer, PACK, T16>(lds, a0, m, pin, rec, eo);
+  join_bucket<kJoinW, kJoinPer, PACK, T16, CONTIG>(lds, a0, m, pin, rec, eo);
 }
 
 // The listed buckets, one workgroup each in turn; one over this kernel's
 // capacity (traces of thousands of spans side by side) sends the set to the
 // unfused path (too_big).
-template <bool PACK>
+template <bool PACK, bool CONTIG = false>
 __global__ __launch_bounds__(kJoinBigW) void bk_join_big_kernel(
     const uint64_t* __restrict__ pin, const GRec* __restrict__ rec, EdgeOut eo,
     const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ over,
@@ -1630,7 +1703,7 @@ __global__ __launch_bounds__(kJoinBigW) void bk_join_big_kernel(
       if (threadIdx.x == 0) atomicAdd(too_big, 1ull);
       continue;
     }
-    join_bucket<kJoinBigW, PER, PACK>(lds, a0, m, pin, rec, eo);
+    join_bucket<kJoinBigW, PER, PACK, true, CONTIG>(lds, a0, m, pin, rec, eo);
     __syncthreads();  // the next bucket reuses the LDS
   }
 }
@@ -1766,6 +1839,8 @@ inline int env_int(const char* name, int dflt) {
 
 }  // namespace
 
+bool join_records_through_b() { return env_int("ANOMOD_JOIN_RECB", 0) != 0; }
+
 BucketGeom bucket_geom(uint64_t n) {
   BucketGeom g;
   // mean bucket size in (avg/2, avg]; the small kernel holds 2048 spans (at
@@ -1840,6 +1915,8 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   // the fused aggregation's per-bucket hash join (ANOMOD_FUSED_JOIN=0: the
   // sorting bucket kernels' edge form)
   const bool join = eo && env_int("ANOMOD_FUSED_JOIN", 1) != 0;
+  // (records through level B: the join reads them contiguously; two levels only)
+  const bool recb = join && g.DB > 0 && join_records_through_b();
   uint64_t* pa = ws->pairs[0];                // level-A pairs
   uint64_t* pb = ws->pairs[1];                // level-B pairs
   hipStream_t st = ctx->stream;
@@ -1892,8 +1969,13 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
       g.T = g.DA + g.DB;
     }
     // the join resolves repeated ids by level-A position: level B need not be
-    // stable there (ANOMOD_BK_STABLE_B=1 keeps the stable scatter for A/B)
-    if (join && !env_int("ANOMOD_BK_STABLE_B", 0))
+    // stable there (ANOMOD_BK_STABLE_B=1 keeps the stable scatter for A/B);
+    // ANOMOD_JOIN_RECB=1: level B moves the records too (r06 A/B)
+    if (join && recb)
+      hipLaunchKernelGGL(bk_scatter_b_rec_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st,
+                         pa, pb, recs, ws->aos[1], g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap,
+                         na, nxB);
+    else if (join && !env_int("ANOMOD_BK_STABLE_B", 0))
       hipLaunchKernelGGL(bk_scatter_b_fast_kernel, dim3((unsigned)g.tilesB), dim3(kBThreads), 0, st,
                          pa, pb, g.DB, ws->tcnt, ws->bsA, ws->btile, ws->tmap, na, nxB);
     else
@@ -1945,20 +2027,29 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
         // 49.8 at four per CU, which spills (gpurun_out/r5b/ab_w6.log);
         // ANOMOD_JOIN_FORM = 1 / 2 runs those two (A/B)
         const int jv = env_int("ANOMOD_JOIN_FORM", 0);
-        auto fn = jv == 2 ? bk_join_kernel<true, 8, true>
+        auto fn = recb ? bk_join_kernel<true, 6, false, true>
+                  : jv == 2 ? bk_join_kernel<true, 8, true>
                   : jv == 1 ? bk_join_kernel<true, 6, true> : bk_join_kernel<true, 6, false>;
+        const GRec* jrec = recb ? ws->aos[1] : recs;
         hipLaunchKernelGGL(fn, dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
-                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+                           jrec, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
-        hipLaunchKernelGGL(bk_join_big_kernel<true>, dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
-                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+        auto fb = recb ? bk_join_big_kernel<true, true> : bk_join_big_kernel<true>;
+        hipLaunchKernelGGL(fb,
+                           dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
+                           jrec, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
       } else {
-        hipLaunchKernelGGL((bk_join_kernel<false, 6, true>), dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
-                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+        const GRec* jrec = recb ? ws->aos[1] : recs;
+        auto fs = recb ? bk_join_kernel<false, 6, true, true> : bk_join_kernel<false, 6, true>;
+        auto fb = recb ? bk_join_big_kernel<false, true> : bk_join_big_kernel<false>;
+        hipLaunchKernelGGL(fs,
+                           dim3((unsigned)nbk), dim3(kJoinW), 0, st, pin,
+                           jrec, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
-        hipLaunchKernelGGL(bk_join_big_kernel<false>, dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
-                           recs, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
+        hipLaunchKernelGGL(fb,
+                           dim3(big_grid), dim3(kJoinBigW), 0, st, pin,
+                           jrec, *eo, bstart, ws->over, ws->misc + kMiscBigN, (uint32_t)nbk,
                            ws->misc + kMiscTooBig);
       }
     } else if (pipe)

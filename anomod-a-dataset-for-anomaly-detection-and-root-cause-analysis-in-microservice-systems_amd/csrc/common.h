@@ -71,6 +71,14 @@ struct anomod_ctx {
   // Trace-grouping workspace (segmented radix sort of ungrouped span sets).
   anomod::GroupWs* group_ws = nullptr;
   int group_path = 0, group_levels = 0, group_bits = 0;  // anomod_ctx_group_info
+  // Grow-only device scratch of the calls that need a large one-call
+  // workspace (anomod::ScratchSlot).  Freeing a block of tens of GB costs the
+  // driver's wipe of it (~30 ms/GB, in hipFree or in a later allocation:
+  // scripts/r06/time_cold2.py), so a call reuses its slot instead of
+  // allocating and freeing; released with the ctx, or when an allocation
+  // would otherwise fail (release_scratch).
+  void* scratch[4] = {};
+  size_t scratch_bytes[4] = {};
   // Cached device workspace for the edge table.
   void* d_table = nullptr;
   size_t table_bytes = 0;
@@ -218,6 +226,17 @@ int edge_aggregate_records(anomod_ctx* ctx, const uint64_t* rec, uint64_t n, uin
                            int8_t* hist_form, anomod_edge_table* out);
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
+enum ScratchSlot { kScratchQuantiles = 0, kScratchTraceStruct = 1, kScratchTsLong = 2,
+                   kNumScratch = 3 };
+// *out = the slot's block of at least `bytes` (grown when smaller; on
+// failure the slots outside `keep` (a mask; this slot is always kept) are
+// released and the allocation retried once).
+int ensure_scratch(anomod_ctx* ctx, ScratchSlot slot, size_t bytes, void** out,
+                   unsigned keep = 0u);
+// Frees every scratch slot whose bit is clear in `keep`.  Returns the bytes freed.
+size_t release_scratch(anomod_ctx* ctx, unsigned keep = 0u);
+// hipMalloc with one retry after the ctx's scratch was released.
+hipError_t dev_malloc(anomod_ctx* ctx, void** p, size_t bytes);
 int ensure_host_stage(anomod_ctx* ctx, size_t bytes);
 
 // ---- integer latency histogram (ANOMOD_HIST_*) --------------------------

@@ -280,6 +280,54 @@ int ensure_table(anomod_ctx* ctx, size_t bytes) {
   return ANOMOD_OK;
 }
 
+size_t release_scratch(anomod_ctx* ctx, unsigned keep) {
+  size_t freed = 0;
+  for (int i = 0; i < kNumScratch; ++i) {
+    if (((keep >> i) & 1u) || !ctx->scratch[i]) continue;
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->scratch[i]);
+    freed += ctx->scratch_bytes[i];
+    ctx->scratch[i] = nullptr;
+    ctx->scratch_bytes[i] = 0;
+  }
+  return freed;
+}
+
+hipError_t dev_malloc(anomod_ctx* ctx, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipSuccess) return e;
+  (void)hipGetLastError();  // clear the sticky-free error state of the failed call
+  if (!release_scratch(ctx)) return e;
+  return hipMalloc(p, bytes);
+}
+
+int ensure_scratch(anomod_ctx* ctx, ScratchSlot slot, size_t bytes, void** out, unsigned keep) {
+  *out = nullptr;
+  if (ctx->scratch[slot] && ctx->scratch_bytes[slot] >= bytes) {
+    *out = ctx->scratch[slot];
+    return ANOMOD_OK;
+  }
+  if (ctx->scratch[slot]) {
+    ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ANOMOD_HIP(ctx, hipFree(ctx->scratch[slot]));
+    ctx->scratch[slot] = nullptr;
+    ctx->scratch_bytes[slot] = 0;
+  }
+  const size_t want = bytes ? bytes : 256;
+  void* p = nullptr;
+  if (hipMalloc(&p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    if (!release_scratch(ctx, keep | (1u << slot)) || hipMalloc(&p, want) != hipSuccess) {
+      set_error(ctx, "hipMalloc(%zu) for a scratch workspace failed", want);
+      return ANOMOD_ENOMEM;
+    }
+  }
+  ctx->scratch[slot] = p;
+  ctx->scratch_bytes[slot] = want;
+  *out = p;
+  return ANOMOD_OK;
+}
+
 int ensure_host_stage(anomod_ctx* ctx, size_t bytes) {
   if (ctx->stage_bytes >= bytes) return ANOMOD_OK;
   if (ctx->h_stage) {
@@ -362,6 +410,7 @@ int anomod_ctx_destroy(anomod_ctx* ctx) {
   if (ctx->d_status) (void)hipFree(ctx->d_status);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->d_table) (void)hipFree(ctx->d_table);
+  anomod::release_scratch(ctx);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_coll) (void)hipHostFree(ctx->h_coll);
   for (int s = 0; s < anomod::kNumStages; ++s) {

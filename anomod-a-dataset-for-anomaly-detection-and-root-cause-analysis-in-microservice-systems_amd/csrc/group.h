@@ -99,6 +99,10 @@ struct BucketGeom {
   uint64_t tilesA = 0, tilesB = 0;  // tilesB: upper bound of the level-B grid
 };
 BucketGeom bucket_geom(uint64_t n);
+// ANOMOD_JOIN_RECB=1 (r06 A/B): level B moves the 32-B records beside the
+// pairs (into the second record buffer) and the join reads them
+// contiguously; the edge records then go to the trace_ptr buffer.
+bool join_records_through_b();
 // Runs the bucket path over `in` (ws sized by ensure_group_ws).  *fallback =
 // true when a bucket outgrew the large per-bucket kernel: the caller groups
 // with the LSD path instead (results are identical; only speed differs).

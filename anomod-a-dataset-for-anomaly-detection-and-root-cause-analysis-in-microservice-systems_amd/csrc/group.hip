@@ -655,7 +655,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   size_t total = 0;
   for (size_t z : sizes) total += (z + kAlign - 1) / kAlign * kAlign;
   double t0 = host_now_ms();
-  bool ok = hipMalloc(&ws->block, total) == hipSuccess;
+  bool ok = dev_malloc(ctx, &ws->block, total) == hipSuccess;
   host_record(ctx, kHostGroupAlloc, host_now_ms() - t0);
   if (ok) {
     size_t off = 0;
@@ -941,7 +941,10 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
     if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
     if (rc == ANOMOD_OK) {
       const double t0 = host_now_ms();
-      uint64_t* erec = reinterpret_cast<uint64_t*>(ctx->group_ws->aos[1]);
+      // (the records-through-level-B form fills aos[1] with records: the edge
+      // records go to trace_ptr's buffer, which the join path leaves unused)
+      uint64_t* erec = join_records_through_b() ? ctx->group_ws->tptr
+                                                : reinterpret_cast<uint64_t*>(ctx->group_ws->aos[1]);
       rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
       host_record(ctx, kHostGroupWall, host_now_ms() - t0);
       if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);

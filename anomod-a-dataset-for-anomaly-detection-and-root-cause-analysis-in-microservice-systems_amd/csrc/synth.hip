@@ -410,12 +410,16 @@ int alloc_spans(anomod_ctx* ctx, uint64_t n_spans, uint64_t n_traces, bool with_
   s->n_spans = n_spans;
   s->n_traces = n_traces;
   const uint64_t ns = n_spans ? n_spans : 1;
-  bool ok = hipMalloc(&s->trace_ptr, (n_traces + 1) * 8) == hipSuccess;
-  if (ok && with_hash) ok = hipMalloc(&s->trace_hash, ns * 8) == hipSuccess;
-  ok = ok && hipMalloc(&s->span_id, ns * 8) == hipSuccess;
-  ok = ok && hipMalloc(&s->parent_span_id, ns * 8) == hipSuccess;
-  ok = ok && hipMalloc(&s->svc_flags, ns * 4) == hipSuccess;
-  ok = ok && hipMalloc(&s->dur_us, ns * 4) == hipSuccess;
+  // (a failed allocation is retried once after the ctx's scratch is released)
+  auto dm = [ctx](void* p, size_t b) {
+    return dev_malloc(ctx, static_cast<void**>(p), b) == hipSuccess;
+  };
+  bool ok = dm(&s->trace_ptr, (n_traces + 1) * 8);
+  if (ok && with_hash) ok = dm(&s->trace_hash, ns * 8);
+  ok = ok && dm(&s->span_id, ns * 8);
+  ok = ok && dm(&s->parent_span_id, ns * 8);
+  ok = ok && dm(&s->svc_flags, ns * 4);
+  ok = ok && dm(&s->dur_us, ns * 4);
   if (!ok) {
     free_spans(s);
     set_error(ctx, "hipMalloc failed for a span set of %llu spans / %llu traces",
@@ -541,7 +545,7 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
       (void)hipMemsetAsync(s->trace_ptr, 0, 8, ctx->stream);
       break;
     }
-    if (hipMalloc(&sizes, n_traces * 8) != hipSuccess) {
+    if (dev_malloc(ctx, reinterpret_cast<void**>(&sizes), n_traces * 8) != hipSuccess) {
       set_error(ctx, "hipMalloc sizes failed");
       rc = ANOMOD_ENOMEM;
       break;
@@ -550,7 +554,7 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
                        shard, n_traces, sizes);
     // trace_ptr = [0, inclusive_scan(sizes)]
     uint64_t* tptr = nullptr;
-    if (hipMalloc(&tptr, (n_traces + 1) * 8) != hipSuccess) {
+    if (dev_malloc(ctx, reinterpret_cast<void**>(&tptr), (n_traces + 1) * 8) != hipSuccess) {
       set_error(ctx, "hipMalloc trace_ptr failed");
       rc = ANOMOD_ENOMEM;
       break;
@@ -558,7 +562,7 @@ int anomod_spans_generate(anomod_ctx* ctx, const anomod_synth_spec* spec, uint64
     size_t tmp_bytes = 0;
     (void)hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, sizes, tptr + 1, n_traces,
                                            ctx->stream);
-    if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) {
+    if (dev_malloc(ctx, &tmp, tmp_bytes) != hipSuccess) {
       (void)hipFree(tptr);
       set_error(ctx, "hipMalloc scan workspace failed");
       rc = ANOMOD_ENOMEM;

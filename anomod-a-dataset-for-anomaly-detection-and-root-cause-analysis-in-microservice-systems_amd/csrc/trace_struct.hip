@@ -707,15 +707,12 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   const size_t off_ctr = off_big + 32;
   const size_t off_list = off_ctr + 8;
   const size_t bytes = off_list + big_cap * 16;
+  // the ctx's scratch slots (reused by the next call instead of freed)
   char* d = nullptr;
-  if (hipMalloc(&d, bytes) != hipSuccess) {
-    set_error(ctx, "hipMalloc(%zu) for trace-structure outputs failed", bytes);
-    return ANOMOD_ENOMEM;
-  }
+  if (int rc = ensure_scratch(ctx, kScratchTraceStruct, bytes, reinterpret_cast<void**>(&d)))
+    return rc;
   uint32_t* scr = nullptr;
   auto fail = [&](hipError_t e, const char* what) {
-    (void)hipFree(d);
-    if (scr) (void)hipFree(scr);
     set_error(ctx, "%s failed: %s", what, hipGetErrorString(e));
     return ANOMOD_EHIP;
   };
@@ -736,10 +733,7 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   o.big_list = reinterpret_cast<unsigned long long*>(d + off_list);
   o.scr = nullptr;
   o.scr_n = 0;
-  if (int rc = stage_begin(ctx, kStageTraceStruct)) {
-    (void)hipFree(d);
-    return rc;
-  }
+  if (int rc = stage_begin(ctx, kStageTraceStruct)) return rc;
   if (nt > 0) {
     // ids unique within every trace (the set's declaration; ANOMOD_UNIQUE_SCAN=0
     // forces the general scan): no own-id scans, no duplicate path
@@ -764,11 +758,9 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return fail(e, "reading the long-trace count");
     if (cnt[0]) {
-      if (hipMalloc(&scr, cnt[1] * 16) != hipSuccess) {
-        (void)hipFree(d);
-        set_error(ctx, "hipMalloc(%llu) for the long-trace scratch failed", cnt[1] * 16);
-        return ANOMOD_ENOMEM;
-      }
+      if (int rc = ensure_scratch(ctx, kScratchTsLong, cnt[1] * 16, reinterpret_cast<void**>(&scr),
+                                  1u << kScratchTraceStruct))
+        return rc;
       o.scr = scr;
       o.scr_n = cnt[1];
       hipLaunchKernelGGL(ts_big_kernel, dim3((unsigned)std::min<uint64_t>(cnt[0], ctx->num_cus)),
@@ -778,11 +770,7 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
       if (e != hipSuccess) return fail(e, "ts_big_kernel launch");
     }
   }
-  if (int rc = stage_end(ctx, kStageTraceStruct)) {
-    (void)hipFree(d);
-    if (scr) (void)hipFree(scr);
-    return rc;
-  }
+  if (int rc = stage_end(ctx, kStageTraceStruct)) return rc;
   auto d2h = [&](void* dst, const void* src, size_t nbytes) -> hipError_t {
     if (!dst || nbytes == 0) return hipSuccess;
     return hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToHost, ctx->stream);
@@ -797,8 +785,6 @@ int anomod_trace_structure_spans(anomod_ctx* ctx, const anomod_spans* spans,
   if (e == hipSuccess && big_cap) e = d2h(&too_long, o.big + 3, 8);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return fail(e, "trace-structure download");
-  (void)hipFree(d);
-  if (scr) (void)hipFree(scr);
   ANOMOD_REQUIRE(ctx, !too_long, "a trace holds 2^31 spans or more");
   return ANOMOD_OK;
 }

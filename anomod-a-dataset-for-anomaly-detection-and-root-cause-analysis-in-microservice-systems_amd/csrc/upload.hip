@@ -11,6 +11,16 @@
 // own stream, so host copies, packing and PCIe transfers overlap and the
 // DMA sees W streams at once.  The workers, their streams and pinned
 // buffers live with the ctx.
+//
+// r06: a plain column (kind 0) no longer goes through a bounce buffer: it is
+// registered with the driver for the call (hipHostRegister, ~2 ms per GB the
+// first time, then ~0.02 ms; unregistered before the call returns, so no
+// registration outlives the caller's buffer) and copied by the DMA engine
+// straight from the caller's pages on one stream — 53 GB/s on the GPU box
+// against 33 GB/s through the bounce (scripts/r06/time_upload.py: more
+// concurrent DMA streams from registered memory measured slower, 21-28 GB/s
+// at 8).  Only svc|flags (kind 1, packed on the way) and a column the driver
+// refuses to register still take the bounce pipeline, beside the direct copies.
 #include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
@@ -31,6 +41,7 @@ struct Uploader {
   int device = 0, nw = 0;
   std::vector<std::thread> th;
   std::vector<hipStream_t> st;
+  hipStream_t direct = nullptr;  // DMA straight from registered caller memory
   std::vector<void*> pin;       // two per worker
   std::vector<hipEvent_t> ev;   // two per worker
   std::mutex m;
@@ -111,6 +122,7 @@ int make_uploader(anomod_ctx* ctx) {
   u->wmax.assign(nw, 0u);
   u->werr.assign(nw, hipSuccess);
   bool ok = true;
+  ok = hipStreamCreateWithFlags(&u->direct, hipStreamNonBlocking) == hipSuccess;
   for (int w = 0; ok && w < nw; ++w) {
     ok = hipStreamCreateWithFlags(&u->st[w], hipStreamNonBlocking) == hipSuccess;
     for (int s = 0; ok && s < 2; ++s) {
@@ -142,6 +154,7 @@ void free_uploader(anomod_ctx* ctx) {
   for (auto& t : u->th) t.join();
   for (auto s : u->st)
     if (s) (void)hipStreamDestroy(s);
+  if (u->direct) (void)hipStreamDestroy(u->direct);
   for (auto p : u->pin)
     if (p) (void)hipHostFree(p);
   for (auto e : u->ev)
@@ -160,19 +173,52 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
   // the ctx stream's earlier work on these buffers (a previous call's kernels
   // reading a reused set) must be done before the worker streams write them
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // plain columns of at least a piece: registered for this call and copied
+  // directly (ANOMOD_UPLOAD_DIRECT=0 keeps every item on the bounce pipeline)
+  const char* de = std::getenv("ANOMOD_UPLOAD_DIRECT");
+  const bool direct_ok = !(de && de[0] == '0');
+  std::vector<const void*> registered;
+  std::vector<char> direct(n_items, 0);
+  hipError_t derr = hipSuccess;
+  for (int i = 0; direct_ok && i < n_items; ++i) {
+    const UpItem& it = items[i];
+    if (it.kind != 0 || it.n < Uploader::kPiece) continue;
+    void* a = const_cast<void*>(it.a);
+    // any refusal (read-only pages, a page another column registered first,
+    // memory the caller pinned) leaves the column on the bounce pipeline: a
+    // range only partly registered must never be handed to the DMA engine
+    if (hipHostRegister(a, it.n, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
+    }
+    registered.push_back(a);
+    direct[i] = 1;
+    derr = hipMemcpyAsync(it.dst, it.a, it.n, hipMemcpyHostToDevice, u->direct);
+    if (derr != hipSuccess) break;
+  }
   u->pieces.clear();
   for (int i = 0; i < n_items; ++i) {
+    if (direct[i]) continue;
     const uint64_t unit = items[i].kind == 1 ? Uploader::kPiece / 4 : Uploader::kPiece;
     for (uint64_t off = 0; off < items[i].n; off += unit)
       u->pieces.push_back({i, off, std::min<uint64_t>(unit, items[i].n - off)});
   }
-  {
+  if (!u->pieces.empty()) {
     std::unique_lock<std::mutex> lk(u->m);
     u->items = items;
     u->pending = u->nw;
     ++u->gen;
     u->cv_go.notify_all();
     u->cv_done.wait(lk, [&] { return u->pending == 0; });
+  } else {
+    for (int w = 0; w < u->nw; ++w) u->werr[w] = hipSuccess, u->wmax[w] = 0u;
+  }
+  const hipError_t dsync = hipStreamSynchronize(u->direct);
+  if (derr == hipSuccess) derr = dsync;
+  for (const void* a : registered) (void)hipHostUnregister(const_cast<void*>(a));
+  if (derr != hipSuccess) {
+    set_error(ctx, "span upload (direct copy) failed: %s", hipGetErrorString(derr));
+    return ANOMOD_EHIP;
   }
   uint32_t mx = 0;
   for (int w = 0; w < u->nw; ++w) {

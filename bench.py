@@ -482,13 +482,21 @@ def group_bytes(info: dict, n: int, n_traces: int) -> int:
     return 8 * n + 2 * (P - 1) * n + 64 * P * n + 16 * n + 8 * n_traces
 
 
+def host_paid(ctx, before: dict) -> dict:
+    """The host slots (anomod_ctx_host_ms) a call paid since `before`: the
+    one-off setup steps (workspace allocations, upload pipeline) and the
+    grouping stage's host wall, in ms."""
+    return {k: round(v[0], 3) for k, v in ctx.host_ms().items() if v[1] != before[k][1]}
+
+
 def ungrouped_leg(ctx, inter, n_traces: int, allsum) -> dict:
     """Grouping + edge aggregation of an ungrouped resident set (n_traces:
     the traces it holds, all non-empty)."""
+    h0 = ctx.host_ms()
     t0 = time.perf_counter()
     ctx.edge_aggregate(inter, with_hist=False)
     cold = {"wall_ms": (time.perf_counter() - t0) * 1e3, "group_ms": ctx.stage_ms(L.STAGE_GROUP),
-            "edge_ms": ctx.stage_ms(L.STAGE_EDGE_AGG)}
+            "edge_ms": ctx.stage_ms(L.STAGE_EDGE_AGG), "host_ms": host_paid(ctx, h0)}
     g, e, wall = [], [], []
     for _ in range(3):
         t0 = time.perf_counter()
@@ -752,10 +760,12 @@ def main() -> int:
         lh.free()
         calls = []
         for _ in range(3):
+            h0 = ctx.host_ms()
             t0 = time.perf_counter()
             ctx.edge_aggregate(host, with_hist=True)
             calls.append({"wall_ms": (time.perf_counter() - t0) * 1e3,
-                          "kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG)})
+                          "kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG),
+                          "host_ms": host_paid(ctx, h0)})
         result["long_traces"]["host_set_calls"] = {
             "spans": host.n_spans, "what": "Context.edge_aggregate(host SpanSet): upload + "
                                            "aggregate + download, first call then two more",

@@ -364,19 +364,23 @@ def test_ungrouped_join_shared_ids_and_big_buckets(ctx):
     dev.free()
 
 
-@pytest.mark.parametrize("pack,stable_b", [("1", "0"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("pack,stable_b,recb", [("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"),
+                                                ("1", "0", "1"), ("0", "0", "1")])
 @pytest.mark.parametrize("S,max_len,dup", [(12, 24, 0.05), (46, 60, 0.02)])
-def test_ungrouped_join_two_levels(ctx, env_knob, S, max_len, dup, pack, stable_b):
+def test_ungrouped_join_two_levels(ctx, env_knob, S, max_len, dup, pack, stable_b, recb):
     """The join path through BOTH scatter levels (ANOMOD_BUCKET_AVG=64 makes a
     ~1 M-span set use T >= 12 bucket bits): level B's non-stable scatter
     (LDS-atomic ranks, the default for the join) with repeated (trace, id)
     resolved by level-A position, against the stable scatter; the packed key
     word (service in the bucket's shared key bits) against the separate
-    service array; buckets over 2 048 spans in the big join kernel.  Every
-    table equals the oracle's on the stably grouped spans."""
+    service array; buckets over 2 048 spans in the big join kernel; the r06
+    form whose level B moves the records too (ANOMOD_JOIN_RECB=1: the join
+    reads them contiguously).  Every table equals the oracle's on the stably
+    grouped spans."""
     env_knob("ANOMOD_BUCKET_AVG", "64")
     env_knob("ANOMOD_JOIN_PACK", pack)
     env_knob("ANOMOD_BK_STABLE_B", stable_b)
+    env_knob("ANOMOD_JOIN_RECB", recb)
     rng = np.random.default_rng(S * 7 + int(dup * 100))
     parts = [_random_spanset(rng, S, 60000, max_len, dup=dup)]
     # a few traces of 1 000-3 000 spans: buckets over 2 048 spans (big kernel)
@@ -393,13 +397,15 @@ def test_ungrouped_join_two_levels(ctx, env_knob, S, max_len, dup, pack, stable_
     dev.free()
 
 
-def test_ungrouped_join_duplicates_across_level_b_tiles(ctx, env_knob):
+@pytest.mark.parametrize("recb", ["0", "1"])
+def test_ungrouped_join_duplicates_across_level_b_tiles(ctx, env_knob, recb):
     """Repeated (trace, id) pairs whose copies are far apart in arrival order
     (other traces' spans between them, so they sit in different level-B tiles
     and land in a bucket in any order once level B is not stable): the
     parent of every child is its trace's FIRST span with that id — the copies
     carry different services, so a wrong pick changes the edge table."""
     env_knob("ANOMOD_BUCKET_AVG", "64")
+    env_knob("ANOMOD_JOIN_RECB", recb)
     rng = np.random.default_rng(4242)
     S, nt, L = 12, 30000, 12
     sp = _random_spanset(rng, S, nt, 0, dup=0.0, lens=np.full(nt, L))

@@ -107,3 +107,31 @@ def test_upload_rejects_bad_trace_ptr(ctx):
                          sp.svc, sp.flags, sp.dur_us)
     with pytest.raises(anomod.AnomodError):
         ctx.upload(bad)
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_upload_direct_and_bounce_columns(monkeypatch, direct):
+    """r06: plain columns of >= one piece are registered for the call and
+    copied straight from the caller's pages (ANOMOD_UPLOAD_DIRECT=0: all
+    through the bounce pipeline).  Columns that share a page (two views of
+    one buffer, so the second registration is refused and that column falls
+    back to the bounce pipeline), a read-only column and a plain one all
+    arrive bit-equal, and repeated calls on the same arrays (registered and
+    unregistered each time) too."""
+    monkeypatch.setenv("ANOMOD_UPLOAD_DIRECT", direct)
+    rng = np.random.default_rng(11)
+    n = 3 * PIECE_U64 + 123  # not a page multiple: the two views share a page
+    sp = _flat_spanset(rng, n)
+    both = np.concatenate([sp.span_id, sp.parent_span_id])
+    dur = sp.dur_us.copy()
+    dur.flags.writeable = False
+    shared = anomod.SpanSet(sp.services, sp.trace_ptr, sp.trace_hash, both[:n], both[n:],
+                            sp.svc, sp.flags, dur)
+    with anomod.Context(0) as c:
+        for _ in range(2):
+            dev = c.upload(shared)
+            _assert_columns_equal(dev.download(), sp)
+            dev.free()
+        sp2 = _random_spanset(rng, 12, PIECE_U64 // 4, 9)
+        for _ in range(2):
+            assert_table_equal(c.edge_aggregate(sp2), native.edge_aggregate(sp2))
