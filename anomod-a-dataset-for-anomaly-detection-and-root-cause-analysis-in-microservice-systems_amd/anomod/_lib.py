@@ -167,6 +167,7 @@ _SIGS = {
     "anomod_spans_grouped": (_i32, [_vp, _P(_i32)]),
     "anomod_spans_group": (_i32, [_vp, _vp, _P(_vp)]),
     "anomod_ctx_group_info": (_i32, [_vp, _P(_i32), _P(_i32), _P(_i32)]),
+    "anomod_ctx_reserve_grouping": (_i32, [_vp, _u64, C.c_int]),
     "anomod_spans_shuffle": (_i32, [_vp, _vp, _u64, _u64, _P(_vp)]),
     "anomod_edge_aggregate_ungrouped": (_i32, [_vp, _vp, _u32, _P(EdgeTableC)]),
     "anomod_edge_quantiles_exact": (_i32, [_vp, _vp, _u32, _P(_u32), _u32, _P(_f64), _P(_u64)]),

@@ -1910,7 +1910,7 @@ int bucket_run_geom(anomod_ctx* ctx, const anomod_spans* in, BucketGeom g, Group
   };
   const SoaIn sin{in->trace_hash, in->span_id, in->parent_span_id, in->svc_flags, in->dur_us};
   GRec* recs = ws->aos[0];                    // level-A records (gathered by the buckets)
-  SoaOut cols = soa_of(ws->aos[1]);           // the grouped columns
+  SoaOut cols = ws->aos[1] ? soa_of(ws->aos[1]) : SoaOut{};  // the grouped columns
   if (!want_h) cols.h = nullptr;              // an aggregation reads no trace_hash column
   // the fused aggregation's per-bucket hash join (ANOMOD_FUSED_JOIN=0: the
   // sorting bucket kernels' edge form)

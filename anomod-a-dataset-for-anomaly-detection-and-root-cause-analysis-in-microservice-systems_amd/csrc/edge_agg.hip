@@ -1229,197 +1229,20 @@ __device__ void res_batch(unsigned long long* bkey, uint32_t* bval,
   __syncthreads();
 }
 
-// ---- r06 form: a position-slot table over ids staged in LDS ----------------
-// The r05 form keyed its slots by the 64-bit id (ds_cmpst_b64 inserts + an
-// atomicMin of (position, service) per span: ~1.35 of its 2.2 ms at LONG
-// 2^23 traces).  Here the window's ids are staged by position with plain
-// stores and a slot is one u32, (position + 1) << 16 | service (0 = empty):
-// an insert is one 32-bit CAS that compares the staged id of a taken slot, a
-// repeated id keeps its smallest position (a CAS loop, repeats only), and a
-// lookup compares the staged id of each candidate (the full 64-bit id: no
-// alias can match) — two dependent LDS reads per hit, as in the r05 form.
-// Bytes per window position: 8 (id) + 8 (two slots) = 16 against 24, and
-// nothing to clear but the slots.
-#ifndef ANOMOD_RES_FORM
-#define ANOMOD_RES_FORM 0  // 0 = position slots (r06), 1 = 64-bit id keys (r05)
-#endif
-
-struct ResLds {
-  uint64_t* lid;  // [kResWin] ids by window position
-  uint32_t* tab;  // [kResSlots] (position + 1) << 16 | service, 0 = empty
-};
-
-// Insert window position k holding id (service sv) into the slots [rb, rb +
-// rs) (its probe starts at r): the first position of an id keeps the slot.
-__device__ __forceinline__ void resp_insert(const ResLds& T, uint32_t rb, uint32_t rs, uint32_t r,
-                                            uint32_t k, uint64_t id, uint32_t sv) {
-  const uint32_t mine = ((k + 1u) << 16) | sv;
-  while (true) {
-    const uint32_t sl = rb + r;
-    uint32_t c = atomicCAS(&T.tab[sl], 0u, mine);
-    if (c == 0u) return;
-    if (T.lid[(c >> 16) - 1u] == id) {  // the id again: the smaller position keeps the slot
-      while ((c >> 16) - 1u > k) {
-        const uint32_t old = atomicCAS(&T.tab[sl], c, mine);
-        if (old == c) return;
-        c = old;  // another copy took it first: compare with that one
-      }
-      return;
-    }
-    r = r + 1u == rs ? 0u : r + 1u;
-  }
-}
-
-// The service of the first span of the region whose id is pid, or ~0.
-__device__ __forceinline__ uint32_t resp_lookup(const ResLds& T, uint32_t rb, uint32_t rs,
-                                                uint32_t r, uint64_t pid) {
-  for (uint32_t probe = 0; probe < rs; ++probe) {
-    const uint32_t c = T.tab[rb + r];
-    if (c == 0u) return 0xFFFFFFFFu;
-    if (T.lid[(c >> 16) - 1u] == pid) return c & 0xFFFFu;
-    r = r + 1u == rs ? 0u : r + 1u;
-  }
-  return 0xFFFFFFFFu;
-}
-
-// One trace longer than a window (res_one's walk with the position slots).
-__device__ void resp_one(const ResLds& T, const uint64_t* __restrict__ span_id,
-                         const uint64_t* __restrict__ parent, const uint32_t* __restrict__ svcfl,
-                         const uint32_t* __restrict__ dur, uint64_t lo, uint64_t L, uint32_t S,
-                         const Table& tab) {
-  const int tid = threadIdx.x;
-  for (uint64_t b0 = 0; b0 < L; b0 += (uint64_t)kResThreads * kBigPer) {
-    uint64_t pid[kBigPer];
-    uint32_t psv[kBigPer];  // ~0: not found yet
-    bool need = false;
-#pragma unroll
-    for (int r = 0; r < kBigPer; ++r) {
-      const uint64_t i = b0 + (uint64_t)r * kResThreads + tid;
-      pid[r] = i < L ? parent[lo + i] : 0ull;
-      psv[r] = 0xFFFFFFFFu;
-      need |= pid[r] != 0ull;
-    }
-    for (uint64_t w0 = 0; w0 < L; w0 += kResWin) {
-      if (!__syncthreads_or(need)) break;  // also orders the previous clear
-      uint64_t id[kResPer];
-      uint32_t sv[kResPer];
-#pragma unroll
-      for (int u = 0; u < kResPer; ++u) {
-        const uint32_t k = (uint32_t)(u * kResThreads + tid);
-        id[u] = w0 + k < L ? span_id[lo + w0 + k] : 0ull;
-        sv[u] = w0 + k < L ? svcfl[lo + w0 + k] & 0xFFFFu : 0u;
-        T.lid[k] = id[u];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < kResPer; ++u)
-        if (id[u] != 0ull)
-          resp_insert(T, 0u, kResSlots, res_slot(id[u]), (uint32_t)(u * kResThreads + tid), id[u],
-                      sv[u]);
-      __syncthreads();
-      need = false;
-#pragma unroll
-      for (int r = 0; r < kBigPer; ++r) {
-        if (pid[r] == 0ull || psv[r] != 0xFFFFFFFFu) continue;
-        psv[r] = resp_lookup(T, 0u, kResSlots, res_slot(pid[r]), pid[r]);
-        need |= psv[r] == 0xFFFFFFFFu;
-      }
-      __syncthreads();
-      for (uint32_t k = tid; k < kResSlots / 4u; k += kResThreads)
-        reinterpret_cast<uint4*>(T.tab)[k] = make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int r = 0; r < kBigPer; ++r) {
-      const uint64_t i = b0 + (uint64_t)r * kResThreads + tid;
-      if (i >= L) continue;
-      const uint32_t p = pid[r] == 0ull ? S : psv[r] == 0xFFFFFFFFu ? S + 1u : psv[r];
-      res_out(tab, lo + i, p, tab.keys ? svcfl[lo + i] : 0u, tab.keys ? dur[lo + i] : 0u, S);
-    }
-  }
-  __syncthreads();  // the last window's clear before the next user of the table
-}
-
-// Up to kGroup traces (bm) packed into one window, each in a private slot
-// region [2 off_i, 2 off_i + 2 L_i) over its staged positions [off_i, off_i + L_i).
-__device__ void resp_batch(const ResLds& T, const uint64_t* __restrict__ span_id,
-                           const uint64_t* __restrict__ parent, const uint32_t* __restrict__ svcfl,
-                           const uint32_t* __restrict__ dur, const uint64_t (&lo)[kGroup],
-                           const uint64_t (&L)[kGroup], uint32_t bm, uint32_t S, const Table& tab) {
-  const int tid = threadIdx.x;
-  uint32_t off[kGroup + 1];
-  off[0] = 0;
-#pragma unroll
-  for (int i = 0; i < kGroup; ++i) off[i + 1] = off[i] + (((bm >> i) & 1u) ? (uint32_t)L[i] : 0u);
-  const uint32_t tot = off[kGroup];
-  uint64_t id[kResPer], pid[kResPer], g[kResPer];
-  uint32_t rb[kResPer], rs[kResPer], sv[kResPer];
-  bool v[kResPer];
-#pragma unroll
-  for (int u = 0; u < kResPer; ++u) {
-    const uint32_t q = (uint32_t)(u * kResThreads + tid);
-    v[u] = q < tot;
-    uint32_t a0 = 0, a1 = off[1];
-    uint64_t tl = lo[0];
-#pragma unroll
-    for (int i = 1; i < kGroup; ++i)
-      if (q >= off[i] && ((bm >> i) & 1u)) {
-        a0 = off[i];
-        a1 = off[i + 1];
-        tl = lo[i];
-      }
-    rb[u] = 2u * a0;
-    rs[u] = 2u * (a1 - a0);
-    g[u] = tl + (q - a0);
-    id[u] = v[u] ? span_id[g[u]] : 0ull;
-    pid[u] = v[u] ? parent[g[u]] : 0ull;
-    sv[u] = v[u] ? svcfl[g[u]] & 0xFFFFu : 0u;
-    if (v[u]) T.lid[q] = id[u];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kResPer; ++u)
-    if (v[u] && id[u] != 0ull)
-      resp_insert(T, rb[u], rs[u], big_region_slot(id[u], rs[u]), (uint32_t)(u * kResThreads + tid),
-                  id[u], sv[u]);
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kResPer; ++u) {
-    if (!v[u]) continue;
-    const uint32_t psv =
-        pid[u] != 0ull ? resp_lookup(T, rb[u], rs[u], big_region_slot(pid[u], rs[u]), pid[u])
-                       : 0xFFFFFFFFu;
-    const uint32_t p = pid[u] == 0ull ? S : psv == 0xFFFFFFFFu ? S + 1u : psv;
-    res_out(tab, g[u], p, tab.keys ? svcfl[g[u]] : 0u, tab.keys ? dur[g[u]] : 0u, S);
-  }
-  __syncthreads();  // every lookup done before the clear
-  for (uint32_t k = tid; k < 2u * tot; k += kResThreads) T.tab[k] = 0u;
-  __syncthreads();
-}
-
 __global__ __launch_bounds__(kResThreads, ANOMOD_RES_MINB) void edge_big_resolve_kernel(
     const uint64_t* __restrict__ span_id, const uint64_t* __restrict__ parent,
     const uint32_t* __restrict__ svcfl, const uint32_t* __restrict__ dur,
     const uint64_t* __restrict__ trace_ptr, uint32_t S, Table tab) {
-#if ANOMOD_RES_FORM == 1
   __shared__ unsigned long long bkey[kResSlots];  // 0 = empty (id 0 is never a parent ref)
   __shared__ uint32_t bval[kResSlots];            // (first position) << 16 | svc
-#else
-  __shared__ uint64_t s_lid[kResWin];
-  __shared__ uint32_t s_tab[kResSlots];
-  const ResLds T{s_lid, s_tab};
-#endif
   __shared__ unsigned long long s_g[kGroup][2];
   const int tid = threadIdx.x;
   const uint64_t nbig = tab.big[0];
   if (nbig == 0) return;
-#if ANOMOD_RES_FORM == 1
   for (uint32_t k = tid; k < kResSlots; k += kResThreads) {
     bkey[k] = 0ull;
     bval[k] = 0xFFFFFFFFu;
   }
-#else
-  for (uint32_t k = tid; k < kResSlots; k += kResThreads) s_tab[k] = 0u;
-#endif
   unsigned long long nlo = 0, nL = 0;
   auto fetch = [&]() {
     unsigned long long j = 0;
@@ -1463,11 +1286,7 @@ __global__ __launch_bounds__(kResThreads, ANOMOD_RES_MINB) void edge_big_resolve
           Lk = gL[q];
         }
       if (Lk > kResWin) {
-#if ANOMOD_RES_FORM == 1
         res_one(bkey, bval, span_id, parent, svcfl, dur, lk, Lk, S, tab);
-#else
-        resp_one(T, span_id, parent, svcfl, dur, lk, Lk, S, tab);
-#endif
         left &= ~(1u << k);
         continue;
       }
@@ -1481,11 +1300,7 @@ __global__ __launch_bounds__(kResThreads, ANOMOD_RES_MINB) void edge_big_resolve
           tot += gL[q];
         }
       }
-#if ANOMOD_RES_FORM == 1
       res_batch(bkey, bval, span_id, parent, svcfl, dur, glo, gL, bm, S, tab);
-#else
-      resp_batch(T, span_id, parent, svcfl, dur, glo, gL, bm, S, tab);
-#endif
       left &= ~bm;
     }
   }

@@ -69,6 +69,7 @@ struct GroupWs {
   uint64_t tcnt_words = 0;            // u32 words of tcnt (tile x digit counts)
   unsigned long long* h_misc = nullptr;  // pinned read-back of the counters
   void* block = nullptr;  // one allocation the device buffers are carved from
+  void* aos1_block = nullptr;  // aos[1]: allocated when a path writes it
 };
 
 // misc layout (u64 words)

@@ -607,9 +607,29 @@ __global__ __launch_bounds__(256) void shuffle_in_trace_kernel(SoaIn in, SoaOut 
   }
 }
 
-int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
+// The second record buffer (aos[1]): the LSD passes' ping-pong and the
+// sorting bucket kernels' grouped columns.  The ungrouped aggregation's join
+// needs none of it (its edge records go to the trace_ptr buffer), so it is
+// its own allocation, made only when a path that writes it runs.
+int ensure_group_aos1(anomod_ctx* ctx) {
   GroupWs* ws = ctx->group_ws;
-  if (ws && ws->cap >= n) return ANOMOD_OK;
+  if (ws->aos1_block) return ANOMOD_OK;
+  const double t0 = host_now_ms();
+  const bool ok = dev_malloc(ctx, &ws->aos1_block, ws->cap * sizeof(GRec)) == hipSuccess;
+  host_record(ctx, kHostGroupAlloc, host_now_ms() - t0);
+  if (!ok) {
+    ws->aos1_block = nullptr;
+    set_error(ctx, "hipMalloc failed for the trace-grouping record buffer of %llu spans",
+              (unsigned long long)ws->cap);
+    return ANOMOD_ENOMEM;
+  }
+  ws->aos[1] = static_cast<GRec*>(ws->aos1_block);
+  return ANOMOD_OK;
+}
+
+int ensure_group_ws(anomod_ctx* ctx, uint64_t n, bool both_records) {
+  GroupWs* ws = ctx->group_ws;
+  if (ws && ws->cap >= n) return both_records ? ensure_group_aos1(ctx) : ANOMOD_OK;
   free_group_ws(ctx);
   ws = new GroupWs();
   ctx->group_ws = ws;
@@ -628,19 +648,21 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   const size_t tcnt_words = std::max<size_t>(tiles * kDig, ws->tile_cap * 2048);
   ws->tcnt_words = tcnt_words;
   const size_t bsum_words = (tiles / kTScanRows + 2) * 2048;
-  // Bytes per span: 64 (two record buffers) + 16 (two pair buffers; the LSD
-  // path's 2-B digits live in the second, which only the bucket path uses)
-  // + 8 (trace_ptr) + ~2 (tile counts, lists) ~= 90 B, plus the input set's
-  // 32 B: 1.15e9 spans take ~104 + 37 GB of the 288 GB, and n is bounded by
-  // the u32 positions (< 2^32) before HBM runs out.
+  // Bytes per span: 32 (the level-A record buffer) + 16 (two pair buffers;
+  // the LSD path's 2-B digits live in the second, which only the bucket path
+  // uses) + 8 (trace_ptr, or the join's edge records) + ~2 (tile counts,
+  // lists) ~= 58 B, plus 32 for the second record buffer when a grouping
+  // path needs it (ensure_group_aos1), plus the input set's 32 B: 1.15e9
+  // spans take ~67 (+ 37) + 37 GB of the 288 GB, and n is bounded by the u32
+  // positions (< 2^32) before HBM runs out.
   static_assert(8 >= 2 + 1, "the digits fit a pair buffer");
-  const size_t sizes[] = {cap * sizeof(GRec), cap * sizeof(GRec), (cap + 1) * 8,
+  const size_t sizes[] = {cap * sizeof(GRec), (cap + 1) * 8,
                           ws->state_words * 8, kMiscWords * 8, ws->list_cap * 8,
                           ws->list_cap * 8, tcnt_words * 4, bsum_words * 4,
                           (ws->bucket_cap + 1) * 4, 2049 * 4, 2049 * 4, ws->tile_cap * 4,
                           (ws->bucket_cap + 1) * 4, ws->bucket_cap * 4,
                           (ws->bucket_cap / 4096 + 2) * 4, cap * 8, cap * 8 + 32};
-  void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->aos[1], (void**)&ws->tptr,
+  void** ptrs[] = {(void**)&ws->aos[0], (void**)&ws->tptr,
                    (void**)&ws->state, (void**)&ws->misc, (void**)&ws->list,
                    (void**)&ws->owned, (void**)&ws->tcnt, (void**)&ws->bsum,
                    (void**)&ws->bstart, (void**)&ws->bsA, (void**)&ws->btile, (void**)&ws->tmap,
@@ -682,7 +704,7 @@ int ensure_group_ws(anomod_ctx* ctx, uint64_t n) {
   }
   ANOMOD_HIP(ctx, hipMemsetAsync(ws->state, 0, ws->state_words * 8, ctx->stream));
   ws->epoch = 0;
-  return ANOMOD_OK;
+  return both_records ? ensure_group_aos1(ctx) : ANOMOD_OK;
 }
 
 uint32_t next_epoch(anomod_ctx* ctx) {
@@ -708,7 +730,7 @@ int group_run(anomod_ctx* ctx, const anomod_spans* in, GroupResult* res, bool wa
               (unsigned long long)n, kSTile);
     return ANOMOD_EINVAL;
   }
-  if (int rc = ensure_group_ws(ctx, n)) return rc;
+  if (int rc = ensure_group_ws(ctx, n, true)) return rc;
   GroupWs* ws = ctx->group_ws;
   if (n > 0 && !force_lsd()) {
     bool fallback = false;
@@ -838,6 +860,7 @@ void free_group_ws(anomod_ctx* ctx) {
   if (!ws) return;
   (void)hipStreamSynchronize(ctx->stream);
   if (ws->block) (void)hipFree(ws->block);
+  if (ws->aos1_block) (void)hipFree(ws->aos1_block);
   if (ws->h_misc) (void)hipHostFree(ws->h_misc);
   delete ws;
   ctx->group_ws = nullptr;
@@ -857,6 +880,15 @@ int anomod_spans_upload_ungrouped(anomod_ctx* ctx, const anomod_span_soa* soa, u
   if (int rc = anomod_spans_upload(ctx, soa, n_spans, nullptr, 0, out)) return rc;
   (*out)->grouped = false;
   return ANOMOD_OK;
+}
+
+int anomod_ctx_reserve_grouping(anomod_ctx* ctx, uint64_t n_spans, int both_records) {
+  ANOMOD_REQUIRE(nullptr, ctx, "anomod_ctx_reserve_grouping: NULL ctx");
+  ANOMOD_REQUIRE(ctx, n_spans <= 0xFFFFFFFFull - kSTile,
+                 "trace grouping of %llu spans: at most 2^32 - %d per call",
+                 (unsigned long long)n_spans, kSTile);
+  if (int rc = bind(ctx)) return rc;
+  return ensure_group_ws(ctx, n_spans, both_records != 0);
 }
 
 int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits) {
@@ -936,15 +968,17 @@ int anomod_edge_aggregate_ungrouped(anomod_ctx* ctx, const anomod_spans* spans,
   const uint64_t n = spans->n_spans;
   if (rc == ANOMOD_OK && n > 0 && !force_lsd() && !(fz && fz[0] == '0') && n_services >= 1 &&
       n_services <= 4096 && spans->max_svc < n_services && n <= 0xFFFFFFFFull - 4096) {
-    rc = ensure_group_ws(ctx, n);
+    // (the sorting bucket kernels' edge form, ANOMOD_FUSED_JOIN=0, and the
+    // records-through-level-B join write the second record buffer)
+    const char* fj = std::getenv("ANOMOD_FUSED_JOIN");
+    rc = ensure_group_ws(ctx, n, join_records_through_b() || (fj && fj[0] == '0'));
     bool fallback = true;
     if (rc == ANOMOD_OK) rc = stage_begin(ctx, kStageGroup);
     if (rc == ANOMOD_OK) {
       const double t0 = host_now_ms();
-      // (the records-through-level-B form fills aos[1] with records: the edge
-      // records go to trace_ptr's buffer, which the join path leaves unused)
-      uint64_t* erec = join_records_through_b() ? ctx->group_ws->tptr
-                                                : reinterpret_cast<uint64_t*>(ctx->group_ws->aos[1]);
+      // edge records (8 B per span) in trace_ptr's buffer, which the join
+      // path leaves unused
+      uint64_t* erec = ctx->group_ws->tptr;
       rc = bucket_group_run(ctx, spans, &g, &fallback, erec, n_services);
       host_record(ctx, kHostGroupWall, host_now_ms() - t0);
       if (rc == ANOMOD_OK) rc = stage_end(ctx, kStageGroup);

@@ -42,6 +42,8 @@ struct Uploader {
   std::vector<std::thread> th;
   std::vector<hipStream_t> st;
   hipStream_t direct = nullptr;  // DMA straight from registered caller memory
+  hipStream_t shared = nullptr;  // the workers' one DMA stream beside direct copies
+  bool one_stream = false;       // this call: workers' DMAs on `shared`
   std::vector<void*> pin;       // two per worker
   std::vector<hipEvent_t> ev;   // two per worker
   std::mutex m;
@@ -53,6 +55,10 @@ struct Uploader {
   std::vector<Piece> pieces;
   std::vector<uint32_t> wmax;
   std::vector<hipError_t> werr;
+
+  // Beside direct copies the workers' DMAs share one stream: registered
+  // memory measured 53 GB/s on 1-4 concurrent DMA streams and 21-28 GB/s on 8.
+  hipStream_t stream(int w) const { return one_stream ? shared : st[w]; }
 
   void work(int w) {
     uint64_t seen = 0;
@@ -89,11 +95,11 @@ struct Uploader {
           bytes = P.len;
           dst = static_cast<char*>(it.dst) + P.off;
         }
-        err = hipMemcpyAsync(dst, buf, bytes, hipMemcpyHostToDevice, st[w]);
-        if (err == hipSuccess) err = hipEventRecord(ev[2 * w + slot], st[w]);
+        err = hipMemcpyAsync(dst, buf, bytes, hipMemcpyHostToDevice, stream(w));
+        if (err == hipSuccess) err = hipEventRecord(ev[2 * w + slot], stream(w));
         slot ^= 1;
       }
-      const hipError_t e2 = hipStreamSynchronize(st[w]);
+      const hipError_t e2 = hipStreamSynchronize(stream(w));
       if (err == hipSuccess) err = e2;
       std::lock_guard<std::mutex> lk(m);
       wmax[w] = mx;
@@ -122,7 +128,8 @@ int make_uploader(anomod_ctx* ctx) {
   u->wmax.assign(nw, 0u);
   u->werr.assign(nw, hipSuccess);
   bool ok = true;
-  ok = hipStreamCreateWithFlags(&u->direct, hipStreamNonBlocking) == hipSuccess;
+  ok = hipStreamCreateWithFlags(&u->direct, hipStreamNonBlocking) == hipSuccess &&
+       hipStreamCreateWithFlags(&u->shared, hipStreamNonBlocking) == hipSuccess;
   for (int w = 0; ok && w < nw; ++w) {
     ok = hipStreamCreateWithFlags(&u->st[w], hipStreamNonBlocking) == hipSuccess;
     for (int s = 0; ok && s < 2; ++s) {
@@ -155,6 +162,7 @@ void free_uploader(anomod_ctx* ctx) {
   for (auto s : u->st)
     if (s) (void)hipStreamDestroy(s);
   if (u->direct) (void)hipStreamDestroy(u->direct);
+  if (u->shared) (void)hipStreamDestroy(u->shared);
   for (auto p : u->pin)
     if (p) (void)hipHostFree(p);
   for (auto e : u->ev)
@@ -205,6 +213,7 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
   }
   if (!u->pieces.empty()) {
     std::unique_lock<std::mutex> lk(u->m);
+    u->one_stream = !registered.empty();
     u->items = items;
     u->pending = u->nw;
     ++u->gen;

@@ -729,8 +729,14 @@ def main() -> int:
         # pulls hits sorted by start_time across concurrent traces
         # (enhanced_trace_collector.py:80-90); a step = device grouping
         # (segmented radix sort) + edge aggregation
+        h0 = ctx.host_ms()
+        t0 = time.perf_counter()
         inter = ctx.shuffle(spans, seed=args.seed + 2, window_traces=4096)
+        prep = {"wall_ms": (time.perf_counter() - t0) * 1e3, "host_ms": host_paid(ctx, h0)}
         result["ungrouped"] = ungrouped_leg(ctx, inter, spans.n_traces, allsum)
+        # making the interleaved set (not timed: input preparation) reserves the
+        # context's grouping workspace for it (anomod_ctx_reserve_grouping)
+        result["ungrouped"]["set_prep"] = prep
         inter.free()
         if cpu_legs:
             result["ungrouped"]["cpu_baseline"] = cpu_group(spec, 1 << 18, args.leg_cpu_seconds)

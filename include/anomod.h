@@ -201,6 +201,16 @@ int anomod_spans_group(anomod_ctx* ctx, const anomod_spans* ungrouped, anomod_sp
  * edge records (the fused aggregation with ANOMOD_FUSED_JOIN=0), 0 LSD path (8-bit radix passes + bucket fix-up); *levels = scatter levels / radix passes run;
  * *bits = bucket bits (bucket path) or 8 * passes.  All 0 before any grouping. */
 int anomod_ctx_group_info(const anomod_ctx* ctx, int* path, int* levels, int* bits);
+/* Size the ctx's grouping workspace (grow-only, kept until the ctx is
+ * destroyed) for sets of up to n_spans spans ahead of their first
+ * aggregation: ~58 B per span for the ungrouped aggregation's join path,
+ * + 32 B with both_records (grouping into columns, the LSD path).  A
+ * workspace of tens of GB can take seconds to obtain from the driver when
+ * the memory it gets was in use earlier in the process; reserving it when the
+ * set is made keeps that out of the aggregation call.  Context.upload_ungrouped
+ * and Context.shuffle (interleaving) in the Python package reserve for the
+ * set they return.                                                         */
+int anomod_ctx_reserve_grouping(anomod_ctx* ctx, uint64_t n_spans, int both_records);
 /* Rearranged copies of a grouped set (synthetic arrival orders for tests
  * and benchmarks): window_traces = 0 shuffles the spans inside every trace
  * (the result stays grouped); window_traces = W interleaves the spans of

@@ -30,7 +30,7 @@ import shutil
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 CORR = ("hbm_bytes = FETCH_SIZE (KiB) x 1024 x 2 + WRITE_SIZE x 1024 (memory-side line traffic: "
         "FETCH_SIZE tallies 64 B per 128-B line request, profiles/r05_fetch_calibration.json); "
         "calibrated_ratio = FETCH_SIZE / (sum over the kernel's read patterns of bytes x the "

@@ -5,7 +5,8 @@
 #
 #   gpurun -- 'bash scripts/gpu_steps.sh OUT "name|seconds|command" ...'
 #
-# OUT is a directory under gpurun_out/; step `name` writes OUT/name.log.  A
+# OUT is a directory under gpurun_out/; step `name` writes OUT/name.log; in a
+# command @OUT@ stands for that directory and @ROOT@ for the repo root.  A
 # command runs from the repo root; one that profiles puts `cd /tmp && export
 # TMPDIR=/tmp &&` first and the program itself right after rocprofv3's `--`.
 set -o pipefail
@@ -21,6 +22,8 @@ for step in "$@"; do
   rest=${step#*|}
   secs=${rest%%|*}
   cmd=${rest#*|}
+  cmd=${cmd//@OUT@/$out}
+  cmd=${cmd//@ROOT@/$GRAFT_REPO_ROOT}
   echo "[$i] $name (limit $secs s): $cmd"
   (cd "$GRAFT_REPO_ROOT" && timeout -k 10 "$secs" bash -c "$cmd") > "$out/$name.log" 2>&1
   rc=$?

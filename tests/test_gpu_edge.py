@@ -103,6 +103,23 @@ def test_low_word_aliases(ctx, S, max_len):
     assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
 
 
+@pytest.mark.parametrize("dup", [0.0, 0.05])
+def test_low_word_aliases_long_windows(ctx, dup):
+    """The long-trace resolve keys its slots by the low id word and confirms
+    the high word staged by position (r06): traces of 300-5 000 spans (packed
+    windows and traces over one 2 048-id window) whose ids share low words
+    three ways, orphans whose low word matches, repeated ids (the first
+    position must keep the slot).  Equal to the oracle."""
+    rng = np.random.default_rng(777 + int(dup * 100))
+    parts = [_random_spanset(rng, 12, 0, 0, dup=dup, lo_alias=True,
+                             lens=list(rng.integers(300, 2049, 12)) + [2049, 3000, 5000])]
+    parts.append(_random_spanset(rng, 12, 2000, 40, dup=dup, lo_alias=True))
+    sp = anomod.SpanSet.concat(parts)
+    assert_table_equal(ctx.edge_aggregate(sp), native.edge_aggregate(sp))
+    q, _ = ctx.edge_quantiles_exact(sp, (50, 99))
+    np.testing.assert_array_equal(q, native.exact_quantiles(sp, (50, 99)))
+
+
 @pytest.mark.parametrize("S,long_set", [(46, False), (12, True)])
 def test_low_word_aliases_unique_ids(ctx, monkeypatch, S, long_set):
     """Unique ids (so the split-word scan runs: TrainTicket width, and the
