@@ -329,6 +329,22 @@ def test_exact_quantiles_match_sorted_latencies(ctx, S, n_traces, max_len):
         np.testing.assert_array_equal(tab[qq][ok], [0.5 * (lo + hi) for lo, hi in b])
 
 
+def test_exact_quantiles_scratch_reuse_across_sizes():
+    """r06: the exact quantiles keep their workspace in a context scratch
+    slot: a large set, a small one (stale keys past its end must not count),
+    a larger one with long traces (the slot grows), the small one again."""
+    rng = np.random.default_rng(23)
+    big = _random_spanset(rng, 12, 20000, 24, dup=0.02)
+    small = _random_spanset(rng, 7, 300, 9)
+    longs = anomod.SpanSet.concat([_random_spanset(rng, 12, 30000, 24),
+                                   _random_spanset(rng, 12, 0, 0, lens=[700, 2500])])
+    with anomod.Context(0) as c:
+        for sp in (big, small, longs, small):
+            got, cnt = c.edge_quantiles_exact(sp, (50, 99))
+            np.testing.assert_array_equal(got, native.exact_quantiles(sp, (50, 99)))
+            assert int(cnt.sum()) == sp.n_spans
+
+
 def test_exact_quantiles_first_call_on_new_context():
     """The exact quantiles as a fresh context's first call on a unique-id set
     whose scan order is not known yet: the order probe needs the pinned

@@ -423,3 +423,28 @@ def test_ungrouped_join_duplicates_across_level_b_tiles(ctx, env_knob, recb):
     assert_table_equal(ctx.edge_aggregate(dev), ref)
     assert ctx.group_info()["levels"] == 2
     dev.free()
+
+
+def test_reserve_grouping_then_aggregate(ctx):
+    """anomod_ctx_reserve_grouping sizes the workspace ahead of the first
+    call (the join path's part, then both record buffers for a grouping into
+    columns); aggregations and groupings after it equal the oracle, and a
+    reservation smaller than the workspace is a no-op."""
+    rng = np.random.default_rng(31)
+    sp = _with_trace_hashes(_random_spanset(rng, 12, 20000, 24, dup=0.02), rng)
+    flat = _interleave(sp, rng, "time")
+    ref = native.edge_aggregate(_oracle_grouped(flat))
+    with anomod.Context(0) as c:
+        dev = c.upload_ungrouped(flat)  # reserves the join path's workspace
+        h = c.host_ms()
+        assert h["group_alloc"][1] == 1
+        c.reserve_grouping(flat.n_spans // 2)  # smaller: nothing allocated
+        assert c.host_ms()["group_alloc"][1] == 1
+        assert_table_equal(c.edge_aggregate(dev), ref)
+        assert c.host_ms()["group_alloc"][1] == 1  # the call allocated nothing
+        g = c.group(dev)  # grouping into columns: the second record buffer now
+        assert c.host_ms()["group_alloc"][1] == 2
+        assert_table_equal(c.edge_aggregate(g), ref)
+        g.free()
+        dev.free()
+

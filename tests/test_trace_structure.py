@@ -162,3 +162,19 @@ def test_gpu_synthetic_sn_device_resident(ctx):
         np.testing.assert_array_equal(getattr(got, k), ref[k], err_msg=k)
     # SN templates: one root per trace unless the generator dropped a parent
     assert (got.n_roots >= 1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_scratch_reuse_across_sizes():
+    """r06: the outputs and the long-trace scratch live in the context's
+    scratch slots and are reused, not freed: a larger set, then a smaller one
+    (the slot is larger than the call needs; nothing of the previous call may
+    show), then one with long traces (the long-trace slot grows), then the
+    first again — every call equal to the oracle."""
+    rng = np.random.default_rng(21)
+    big = _random_set(rng, 12, 30000, 30)
+    small = _random_set(rng, 5, 700, 12)
+    longs = anomod.SpanSet.concat([_random_set(rng, 12, 50, 20), _random_set(rng, 12, 3, 1200)])
+    with anomod.Context(0) as c:
+        for sp in (big, small, longs, small, big):
+            _gpu_equal(c, sp)
