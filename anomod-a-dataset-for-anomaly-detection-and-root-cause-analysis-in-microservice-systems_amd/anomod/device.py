@@ -301,8 +301,18 @@ class Context:
         d = DeviceSpans(self, h, spans.services)
         d.unique_ids = spans.unique_ids
         d.set_hints(spans.scan_order, spans.hist_form)
-        self.reserve_grouping(spans.n_spans)
+        self._reserve_for(d)
         return d
+
+    def _reserve_for(self, d: DeviceSpans):
+        """Best effort: the workspace for an ungrouped set's first aggregation
+        now (a set that fits HBM while its workspace does not still uploads;
+        its aggregation then reports the shortage)."""
+        try:
+            self.reserve_grouping(d.n_spans)
+        except L.AnomodError as e:
+            if "ENOMEM" not in str(e):
+                raise
 
     def reserve_grouping(self, n_spans: int, both_records: bool = False):
         """Size the context's grouping workspace for an ungrouped set of
@@ -327,7 +337,7 @@ class Context:
                                                    C.byref(h)))
         d = DeviceSpans(self, h, spans.services)
         if window_traces:  # an ungrouped set: its grouping workspace now, not at the first call
-            self.reserve_grouping(d.n_spans)
+            self._reserve_for(d)
         return d
 
     def generate(self, spec: SynthSpec, n_traces: int, shard: int = 0) -> DeviceSpans:
