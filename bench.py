@@ -429,9 +429,11 @@ def tt_config2_files(ctx, staged: list) -> dict:
 def edge_leg(ctx, spans, reps: int, what: str) -> dict:
     """Edge-kernel time of a resident span set (hipEvents, ctx stream); the
     set's first aggregation (hints not learned yet) is reported as "cold"."""
+    h0 = ctx.host_ms()
     t0 = time.perf_counter()
     ctx.edge_aggregate(spans, with_hist=False)
-    cold = {"kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG), "wall_ms": (time.perf_counter() - t0) * 1e3}
+    cold = {"kernel_ms": ctx.stage_ms(L.STAGE_EDGE_AGG), "wall_ms": (time.perf_counter() - t0) * 1e3,
+            "host_ms": host_paid(ctx, h0)}
     ms = []
     for _ in range(reps):
         ctx.edge_aggregate(spans, with_hist=False)
