@@ -360,13 +360,13 @@ struct Builder {
       last_c = col[i++] = it->second;
     }
     std::vector<uint32_t> ord(out->ts.size());
-    for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    for (uint32_t k = 0; k < ord.size(); ++k) ord[k] = k;
     std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return out->ts[a] < out->ts[b]; });
     std::vector<uint32_t> crank(ord.size());
     std::vector<double> sorted_ts(ord.size());
-    for (uint32_t i = 0; i < ord.size(); ++i) {
-      crank[ord[i]] = i;
-      sorted_ts[i] = out->ts[ord[i]];
+    for (uint32_t k = 0; k < ord.size(); ++k) {
+      crank[ord[k]] = k;
+      sorted_ts[k] = out->ts[ord[k]];
     }
     out->ts.swap(sorted_ts);
     const size_t T = out->ts.size(), S = out->series.size();
