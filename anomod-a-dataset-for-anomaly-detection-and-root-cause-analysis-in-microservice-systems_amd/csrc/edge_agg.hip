@@ -1468,7 +1468,7 @@ __global__ __launch_bounds__(kThreads) void edge_agg_kernel(
       // [first trace of the chunk, t_end) to the compact-form resume launch
       // and stop.
       if (MODE == kModeAuto &&
-          __builtin_amdgcn_readfirstlane(
+          (uint32_t)__builtin_amdgcn_readfirstlane(
               __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >=
               kSatFails) {
         if (lane == 0) {
