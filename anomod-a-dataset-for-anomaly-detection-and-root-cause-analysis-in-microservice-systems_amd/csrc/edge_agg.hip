@@ -2169,6 +2169,8 @@ int anomod_edge_aggregate_spans(anomod_ctx* ctx, const anomod_spans* spans, uint
       ANOMOD_HIP(ctx, hipMemsetAsync(tab.ovf + 1, 0, 8, ctx->stream));
       cuts[0] = P;
     }
+    if (const char* lg = getenv("ANOMOD_LOG_KERNEL"); lg && lg[0] == '1')  // (tests)
+      fprintf(stderr, "anomod: edge aggregation kernel %s\n", pk.name);
     for (size_t k = 0; k + 1 < cuts.size(); ++k) {
       if (cuts[k] >= cuts[k + 1]) continue;
       if (k > 0) {

@@ -492,14 +492,18 @@ def test_duplicate_ids_are_not_declared_unique(ctx):
 
 
 @pytest.mark.parametrize("alias", [False, True])
-def test_long_set_wide_scan(ctx, monkeypatch, alias):
+def test_long_set_wide_scan(ctx, monkeypatch, capfd, alias):
     """Sets holding a trace longer than a chunk take the long-trace kernel
-    instantiation (8 / 8 bidirectional scan, compact form).  Traces of
-    49..256 spans with random ancestors, unique ids per trace; alias: every
-    trace reuses the same id values, so a chunk holds equal ids of different
-    traces (the scan stays inside the span's own trace).  Orphans, roots, a
-    300-span trace for the long-trace pass.  Equal to the oracle."""
+    instantiation (the wide split-word scan, compact form).
+    Traces of 49..256 spans with random ancestors, unique ids per trace;
+    alias: every trace reuses the same id values, so a chunk holds equal ids
+    of different traces (the lookup keeps to the span's own trace).  Orphans,
+    roots, a 300-span trace for the long-trace pass.  Equal to the oracle,
+    and the instantiation is the one that ran (random ancestors are not
+    collector order, so the bidirectional scans are forced on)."""
     monkeypatch.setenv("ANOMOD_HIST_FORM", "compact")
+    monkeypatch.setenv("ANOMOD_UNIQUE_SCAN", "1")
+    monkeypatch.setenv("ANOMOD_LOG_KERNEL", "1")
     rng = np.random.default_rng(71 + alias)
     lens = np.r_[rng.integers(49, 257, 600), rng.integers(1, 40, 400), [300]]
     rng.shuffle(lens)
@@ -509,8 +513,61 @@ def test_long_set_wide_scan(ctx, monkeypatch, alias):
     assert sp.check_unique_ids()
     ref = native.edge_aggregate(sp)
     dev = ctx.upload(sp)
+    capfd.readouterr()
     for _ in range(2):
         assert_table_equal(ctx.edge_aggregate(dev), ref)
+    assert "wide_scan" in capfd.readouterr().err
+    dev.free()
+
+
+@pytest.mark.parametrize("self_ref", [0.0, 0.1])
+def test_long_set_hash_chains(ctx, monkeypatch, capfd, self_ref):
+    """The long-trace instantiation on ids crafted so that every id of the
+    set — orphan references included — has the same m = (lo ^ hi *
+    0x85EBCA77) * 0x9E3779B1 (mod 2^32): the key of the per-chunk id table
+    measured in r06 (not kept), under which a chunk's ids fill
+    one probe chain with equal tags.  Whatever keys a lookup uses, such ids
+    must be told apart by the full 64-bit id and the span's trace.  Random
+    ancestors, spans that reference their own id, traces of 1..256 spans and
+    a 300-span trace.  Equal to the oracle."""
+    monkeypatch.setenv("ANOMOD_HIST_FORM", "compact")
+    monkeypatch.setenv("ANOMOD_UNIQUE_SCAN", "1")
+    monkeypatch.setenv("ANOMOD_LOG_KERNEL", "1")
+    rng = np.random.default_rng(4242 + int(self_ref * 10))
+    lens = np.r_[rng.integers(100, 257, 300), rng.integers(1, 30, 200), [300]]
+    rng.shuffle(lens)
+    sp = _random_spanset(rng, 12, 0, 0, lens=lens)
+    n = sp.n_spans
+    M = 0x13572468
+
+    def same_m(hi):  # the lo word that gives every hi the same m
+        return (np.uint64(M) ^ ((hi * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)))
+
+    # distinct high words for the ids, other high words for orphan references
+    his = rng.permutation(np.arange(1, 2 * n + 1, dtype=np.uint64) * np.uint64(977))
+    sid_hi = his[:n]
+    remap = dict(zip(sp.span_id.tolist(), (sid_hi << np.uint64(32) | same_m(sid_hi)).tolist()))
+    sid = np.array([remap[int(x)] for x in sp.span_id], np.uint64)
+    orph_hi = his[n:]
+    pid = np.zeros(n, np.uint64)
+    for j, p in enumerate(sp.parent_span_id.tolist()):
+        if p:
+            if p in remap:
+                pid[j] = remap[p]
+            else:
+                h = orph_hi[j]
+                pid[j] = (int(h) << 32) | int(same_m(h))
+    if self_ref:
+        m = rng.random(n) < self_ref
+        pid[m] = sid[m]
+    sp = anomod.SpanSet(sp.services, sp.trace_ptr, sid.copy(), sid, pid, sp.svc, sp.flags,
+                        sp.dur_us)
+    assert sp.check_unique_ids()
+    ref = native.edge_aggregate(sp)
+    dev = ctx.upload(sp)
+    capfd.readouterr()
+    assert_table_equal(ctx.edge_aggregate(dev), ref)
+    assert "wide_scan" in capfd.readouterr().err
     dev.free()
 
 
