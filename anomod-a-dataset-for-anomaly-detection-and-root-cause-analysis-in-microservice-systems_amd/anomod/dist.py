@@ -30,7 +30,7 @@ from typing import Callable
 
 import numpy as np
 
-from ._lib import OP_MAX, OP_MIN, OP_SUM
+from ._lib import ERCCL, OP_MAX, OP_MIN, OP_SUM, AnomodError
 from .device import Context
 from .spans import SpanSet
 
@@ -321,6 +321,43 @@ def attach_rccl(ctx: Context, info: RankInfo,
         with HostGroup(info.rank, info.world) as g:
             uid = g.broadcast(uid)
     ctx.attach_comm(uid, info.world, info.rank)
+
+
+def attach(ctx: Context, info: RankInfo, group: HostGroup, fallback: bool = True) -> str:
+    """This rank's collective transport: RCCL when every rank's communicator
+    comes up, else — when RCCL refused on every rank (ranks sharing one device,
+    a node without peer access) and ``fallback`` — the host transport over
+    ``group`` (attach_host).  Every rank reaches the same answer (one
+    HostGroup sum of the successes), and a refusal on some ranks only raises
+    AnomodError on all of them.  A failed unique id on rank 0 reaches the
+    others as an empty broadcast instead of leaving them waiting.  Returns
+    "rccl", "host (RCCL refused: ...)" or "none" (world == 1)."""
+    if info.world <= 1:
+        return "none"
+    uid, err = None, ""
+    if info.rank == 0:
+        try:
+            uid = Context.unique_id()
+        except AnomodError as e:
+            err = str(e)
+    uid = group.broadcast(uid if uid is not None else b"")
+    ok = 0.0
+    if uid:
+        try:
+            ctx.attach_comm(uid, info.world, info.rank)
+            ok = 1.0
+        except AnomodError as e:
+            err = str(e)
+    else:
+        err = err or "rank 0 could not make the RCCL unique id"
+    n_ok = int(group.allreduce_scalar(ok, OP_SUM))
+    if n_ok == info.world:
+        return "rccl"
+    if n_ok > 0 or not fallback:
+        raise AnomodError(ERCCL, f"RCCL communicator up on {n_ok} of {info.world} "
+                          f"ranks (this rank: {err or 'up'})")
+    attach_host(ctx, group)
+    return f"host (RCCL refused: {err[-200:]})"
 
 
 def attach_host(ctx: Context, group: HostGroup) -> None:

@@ -488,7 +488,11 @@ int anomod_ctx_attach_comm(anomod_ctx* ctx, const uint8_t* unique_id, int nranks
   }
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
-  ANOMOD_RCCL(ctx, ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  // into a local: a refused init (e.g. two ranks on one device) leaves the
+  // ctx without a communicator, so the caller may attach the host transport
+  ncclComm_t comm = nullptr;
+  ANOMOD_RCCL(ctx, ncclCommInitRank(&comm, nranks, id, rank));
+  ctx->comm = comm;
   ctx->nranks = nranks;
   ctx->rank = rank;
   return ANOMOD_OK;

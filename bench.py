@@ -607,11 +607,14 @@ def main() -> int:
         t_stage = time.perf_counter() - t_stage
 
     ctx = anomod.Context(0 if args.host_comm else local)
+    transport = "none"
     if world > 1:
         if args.host_comm:  # ranks sharing one GPU (RCCL refuses): same calls, host transport
             dist.attach_host(ctx, group)
-        else:
-            dist.attach_rccl(ctx, dist.RankInfo(rank, world, local), group)
+            transport = "host (HostGroup, one device)"
+        else:  # RCCL; the host transport only if RCCL refuses on every rank (said in the line)
+            transport = dist.attach(ctx, dist.RankInfo(rank, world, local), group)
+    coll = "RCCL" if transport == "rccl" else "host"
     cpu_legs = rank == 0 and world == 1 and not args.no_cpu_baseline
 
     spec = anomod.SynthSpec("SN", seed=args.seed, p_orphan_ppm=100)
@@ -661,7 +664,7 @@ def main() -> int:
                         "per GPU, edge table + 896-bin histograms + p50/p99 per step",
             "spans_per_gpu": spans.n_spans, "traces_per_gpu": spans.n_traces,
             "services": len(spans.services), "hist_bins": L.HIST_BINS,
-            "parallelism": f"dp{world} (traceId shards)" + (" + RCCL all-reduce" if world > 1
+            "parallelism": f"dp{world} (traceId shards)" + (f" + {coll} all-reduce" if world > 1
                                                             else ""),
         },
         "roofline": {
@@ -673,7 +676,7 @@ def main() -> int:
         "cold": cold,
     }
     if world > 1:
-        result["transport"] = "host (HostGroup, one device)" if args.host_comm else "rccl"
+        result["transport"] = transport
     if "general_scan" in legs:
         # --- the same spans without the generator's unique-id declaration
         # (ANOMOD_UNIQUE_SCAN=0): the first-match forward parent scan every
@@ -826,7 +829,7 @@ def main() -> int:
         result["pagerank"]["sharded"] = {
             "iters_per_s": args.ppr_iters / (s_ms * 1e-3), "shards": world,
             "us_per_iter": s_ms * 1e3 / args.ppr_iters,
-            "mode": "row-sharded, per-iteration launches + RCCL all-reduce/all-gather"
+            "mode": f"row-sharded, per-iteration launches + {coll} all-reduce/all-gather"
                     if world > 1 else "row-sharded path, 1 shard (per-iteration launches)"}
         # batched personalizations (one per fault hypothesis)
         # (one persistent launch per batch: K vectors per grid barrier; K = 16

@@ -210,3 +210,65 @@ def test_silent_peer_times_out(tmp_path):
     # unbounded by default: a barrier behind a rank busy for any time passes
     if not os.environ.get("ANOMOD_HOSTGROUP_TIMEOUT_S"):
         assert dist.HostGroup(0, 1).coll_timeout_s is None
+
+
+@pytest.mark.parametrize("refuse,uid_fails,expect", [
+    ((False, False), False, "rccl"),
+    ((True, True), False, "host"),    # RCCL refused everywhere (ranks sharing a device)
+    ((False, True), False, "raise"),  # refused on one rank only: every rank raises
+    ((False, False), True, "host"),   # rank 0 could not make the unique id
+])
+def test_attach_transport_agreement(tmp_path, monkeypatch, refuse, uid_fails, expect):
+    """dist.attach (bench.py's transport choice): RCCL when every rank's
+    communicator comes up, the host transport when RCCL refused on every rank,
+    AnomodError on every rank when only some refused; a failed unique id on
+    rank 0 reaches rank 1 as an empty broadcast, not a hang.  Fake contexts
+    (no device): the agreement logic over a real two-rank HostGroup."""
+    import threading
+
+    from anomod import dist
+    from anomod._lib import ERCCL, AnomodError
+
+    def uid():
+        if uid_fails:
+            raise AnomodError(ERCCL, "ncclGetUniqueId failed")
+        return b"u" * 128
+
+    monkeypatch.setattr(dist.Context, "unique_id", staticmethod(uid))
+
+    class FakeCtx:
+        def __init__(self, refuse_init):
+            self.refuse_init, self.comm, self.host = refuse_init, None, None
+
+        def attach_comm(self, u, n, r):
+            assert u == b"u" * 128
+            if self.refuse_init:
+                raise AnomodError(ERCCL, "ncclCommInitRank failed: invalid usage")
+            self.comm = (n, r)
+
+        def attach_host_comm(self, n, r, allreduce, allgather):
+            self.host = (n, r)
+
+    key, res, ctxs = f"attach{os.getpid()}", {}, {r: FakeCtx(refuse[r]) for r in (0, 1)}
+
+    def rank(r):
+        with dist.HostGroup(r, 2, key=key, rdzv_dir=str(tmp_path), timeout_s=30,
+                            coll_timeout_s=30) as g:
+            try:
+                res[r] = dist.attach(ctxs[r], dist.RankInfo(r, 2, r), g)
+            except AnomodError as e:
+                res[r] = e
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert set(res) == {0, 1}, res
+    for r in (0, 1):
+        if expect == "rccl":
+            assert res[r] == "rccl" and ctxs[r].comm == (2, r) and ctxs[r].host is None
+        elif expect == "host":
+            assert res[r].startswith("host (RCCL refused") and ctxs[r].host == (2, r), res
+        else:
+            assert isinstance(res[r], AnomodError) and "up on 1 of 2" in str(res[r])
