@@ -123,12 +123,17 @@ def test_two_ranks_host_transport(tmp_path):
     assert str(r0["agree_err"]) != ""                 # its peer failed with it
 
 
-def test_bench_two_ranks_host_comm(tmp_path):
+@pytest.mark.parametrize("mode", ["host_comm", "fallback"])
+def test_bench_two_ranks_host_comm(tmp_path, mode):
     """bench.py's N > 1 code — HostGroup rendezvous, per-step edge-table
     merge, barriers, allmax / allsum weak-scaling accounting — run for real
-    at world 2 on one MI355X through the host transport (--host-comm; RCCL
-    refuses two ranks on a device).  bench.py itself asserts the merged
-    count.sum() equals the spans of both shards."""
+    at world 2 on one MI355X through the host transport, with every leg the
+    driver's N > 1 runs (each rank must enter the same collectives in the
+    same order, or the run hangs), at small sizes.  host_comm: --host-comm;
+    fallback: no flag and both ranks on device 0 (LOCAL_RANK 0), so RCCL
+    refuses on both and dist.attach takes the host transport, saying so in
+    the line.  bench.py itself asserts the merged count.sum() equals the
+    spans of both shards."""
     import json
 
     with socket.socket() as s:
@@ -137,16 +142,19 @@ def test_bench_two_ranks_host_comm(tmp_path):
     procs = []
     for r in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
-                   WORLD_SIZE="2", LOCAL_RANK=str(r), ANOMOD_RDZV_DIR=str(tmp_path))
+                   WORLD_SIZE="2", LOCAL_RANK=str(r if mode == "host_comm" else 0),
+                   ANOMOD_RDZV_DIR=str(tmp_path))
         procs.append(subprocess.Popen(
-            [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--host-comm", "--steps", "3",
-             "--warmup", "1", "--traces-per-gpu", "30000", "--legs", "pagerank,ungrouped",
-             "--ppr-nodes", "20000", "--ppr-iters", "20", "--no-cpu-baseline"],
+            [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3",
+             "--warmup", "1", "--traces-per-gpu", "30000", "--ppr-nodes", "20000",
+             "--ppr-iters", "20", "--ewma-series", "2000", "--ewma-steps", "1920",
+             "--ewma-chunks", "2", "--no-cpu-baseline"]
+            + (["--host-comm"] if mode == "host_comm" else []),
             env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, start_new_session=True))
     outs = []
     for p in procs:
         try:
-            o, e = p.communicate(timeout=100)
+            o, e = p.communicate(timeout=150)
             outs.append((o.decode(errors="replace"), e.decode(errors="replace")))
         except subprocess.TimeoutExpired:
             for q in procs:
@@ -157,6 +165,12 @@ def test_bench_two_ranks_host_comm(tmp_path):
     line = json.loads(outs[0][0].strip().splitlines()[-1])
     assert outs[1][0].strip() == ""  # only rank 0 prints
     assert line["n_gpus"] == 2 and line["transport"].startswith("host")
+    if mode == "fallback":
+        assert line["transport"].startswith("host (RCCL refused")
+        assert "host all-reduce" in line["config"]["parallelism"]
+    for leg in ("sn_general_scan", "trace_structure", "exact_quantiles", "sn_in_trace_shuffled",
+                "ungrouped", "tt_width", "long_traces", "pagerank", "ewma"):
+        assert leg in line, leg
     n0 = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100),
                                     30000, shard=0).n_spans
     n1 = anomod.synth_generate_host(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100),
