@@ -227,7 +227,7 @@ int edge_aggregate_records(anomod_ctx* ctx, const uint64_t* rec, uint64_t n, uin
 // Grow-only device workspace owned by the ctx.
 int ensure_table(anomod_ctx* ctx, size_t bytes);
 enum ScratchSlot { kScratchQuantiles = 0, kScratchTraceStruct = 1, kScratchTsLong = 2,
-                   kNumScratch = 3 };
+                   kScratchUpload = 3, kNumScratch = 4 };
 // *out = the slot's block of at least `bytes` (grown when smaller; on
 // failure the slots outside `keep` (a mask; this slot is always kept) are
 // released and the allocation retried once).

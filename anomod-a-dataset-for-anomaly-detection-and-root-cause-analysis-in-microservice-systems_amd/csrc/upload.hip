@@ -16,11 +16,16 @@
 // registered with the driver for the call (hipHostRegister, ~2 ms per GB the
 // first time, then ~0.02 ms; unregistered before the call returns, so no
 // registration outlives the caller's buffer) and copied by the DMA engine
-// straight from the caller's pages on one stream — 53 GB/s on the GPU box
+// straight from the caller's pages on the ctx stream — 53 GB/s on the GPU box
 // against 33 GB/s through the bounce (scripts/r06/time_upload.py: more
 // concurrent DMA streams from registered memory measured slower, 21-28 GB/s
-// at 8).  Only svc|flags (kind 1, packed on the way) and a column the driver
-// refuses to register still take the bounce pipeline, beside the direct copies.
+// at 8).  svc|flags (kind 1) goes the same way: its two u16 columns are
+// copied into a device scratch and packed there by pack_svc_flags_kernel,
+// which also takes the largest service.  Items under a piece are copied from
+// pageable memory (svc|flags packed on the host first).  So the pipeline of
+// worker threads and pinned buffers (~0.1 s to create: the first host call's
+// cost in r05 / early r06) is made only for a column the driver refuses to
+// register, or when ANOMOD_UPLOAD_DIRECT=0 asks for it.
 #include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
@@ -41,7 +46,6 @@ struct Uploader {
   int device = 0, nw = 0;
   std::vector<std::thread> th;
   std::vector<hipStream_t> st;
-  hipStream_t direct = nullptr;  // DMA straight from registered caller memory
   hipStream_t shared = nullptr;  // the workers' one DMA stream beside direct copies
   bool one_stream = false;       // this call: workers' DMAs on `shared`
   std::vector<void*> pin;       // two per worker
@@ -128,8 +132,7 @@ int make_uploader(anomod_ctx* ctx) {
   u->wmax.assign(nw, 0u);
   u->werr.assign(nw, hipSuccess);
   bool ok = true;
-  ok = hipStreamCreateWithFlags(&u->direct, hipStreamNonBlocking) == hipSuccess &&
-       hipStreamCreateWithFlags(&u->shared, hipStreamNonBlocking) == hipSuccess;
+  ok = hipStreamCreateWithFlags(&u->shared, hipStreamNonBlocking) == hipSuccess;
   for (int w = 0; ok && w < nw; ++w) {
     ok = hipStreamCreateWithFlags(&u->st[w], hipStreamNonBlocking) == hipSuccess;
     for (int s = 0; ok && s < 2; ++s) {
@@ -161,7 +164,6 @@ void free_uploader(anomod_ctx* ctx) {
   for (auto& t : u->th) t.join();
   for (auto s : u->st)
     if (s) (void)hipStreamDestroy(s);
-  if (u->direct) (void)hipStreamDestroy(u->direct);
   if (u->shared) (void)hipStreamDestroy(u->shared);
   for (auto p : u->pin)
     if (p) (void)hipHostFree(p);
@@ -171,66 +173,160 @@ void free_uploader(anomod_ctx* ctx) {
   ctx->uploader = nullptr;
 }
 
+namespace {
+
+// svc (u16) | flags (u16) << 16 -> u32, and the largest service (atomic max
+// of the waves' maxima into *mx)
+__global__ __launch_bounds__(256) void pack_svc_flags_kernel(const uint16_t* __restrict__ svc,
+                                                             const uint16_t* __restrict__ fl,
+                                                             uint32_t* __restrict__ out, uint64_t n,
+                                                             unsigned int* __restrict__ mx) {
+  uint32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256u) {
+    const uint32_t s = svc[i];
+    out[i] = s | ((uint32_t)fl[i] << 16);
+    m = s > m ? s : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)m, o);
+    m = y > m ? y : m;
+  }
+  if ((threadIdx.x & 63u) == 0 && m) atomicMax(mx, m);
+}
+
+}  // namespace
+
 int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* max_svc) {
   if (max_svc) *max_svc = 0;
   uint64_t total = 0;
   for (int i = 0; i < n_items; ++i) total += items[i].n;
   if (total == 0) return ANOMOD_OK;
-  if (int rc = make_uploader(ctx)) return rc;
-  Uploader* u = ctx->uploader;
   // the ctx stream's earlier work on these buffers (a previous call's kernels
-  // reading a reused set) must be done before the worker streams write them
+  // reading a reused set) must be done before other streams write them
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  // plain columns of at least a piece: registered for this call and copied
-  // directly (ANOMOD_UPLOAD_DIRECT=0 keeps every item on the bounce pipeline)
-  const char* de = std::getenv("ANOMOD_UPLOAD_DIRECT");
+  const char* de = getenv("ANOMOD_UPLOAD_DIRECT");
   const bool direct_ok = !(de && de[0] == '0');
   std::vector<const void*> registered;
-  std::vector<char> direct(n_items, 0);
-  hipError_t derr = hipSuccess;
-  for (int i = 0; direct_ok && i < n_items; ++i) {
-    const UpItem& it = items[i];
-    if (it.kind != 0 || it.n < Uploader::kPiece) continue;
-    void* a = const_cast<void*>(it.a);
-    // any refusal (read-only pages, a page another column registered first,
-    // memory the caller pinned) leaves the column on the bounce pipeline: a
-    // range only partly registered must never be handed to the DMA engine
-    if (hipHostRegister(a, it.n, hipHostRegisterDefault) != hipSuccess) {
+  std::vector<char> done(n_items, 0);
+  std::vector<std::vector<uint32_t>> packed;  // small svc|flags items, packed on the host
+  uint32_t mx = 0;
+  unsigned int* d_mx = nullptr;  // the device pack's largest service
+  hipError_t err = hipSuccess;
+  // any refusal (read-only pages, a page another column registered first,
+  // memory the caller pinned) leaves the item to the bounce pipeline: a range
+  // only partly registered must never be handed to the DMA engine
+  auto reg = [&](const void* a, uint64_t bytes) {
+    if (hipHostRegister(const_cast<void*>(a), bytes, hipHostRegisterDefault) != hipSuccess) {
       (void)hipGetLastError();
-      continue;
+      return false;
     }
     registered.push_back(a);
-    direct[i] = 1;
-    derr = hipMemcpyAsync(it.dst, it.a, it.n, hipMemcpyHostToDevice, u->direct);
-    if (derr != hipSuccess) break;
+    return true;
+  };
+  auto unreg_last = [&]() {
+    (void)hipHostUnregister(const_cast<void*>(registered.back()));
+    registered.pop_back();
+  };
+  for (int i = 0; direct_ok && err == hipSuccess && i < n_items; ++i) {
+    const UpItem& it = items[i];
+    const uint64_t bytes = it.kind == 1 ? it.n * 4 : it.n;
+    if (bytes == 0) {
+      done[i] = 1;
+      continue;
+    }
+    if (bytes < Uploader::kPiece) {  // small: from pageable memory
+      if (it.kind == 0) {
+        err = hipMemcpyAsync(it.dst, it.a, it.n, hipMemcpyHostToDevice, ctx->stream);
+      } else {
+        packed.emplace_back(it.n);
+        const auto* sv = static_cast<const uint16_t*>(it.a);
+        const auto* fl = static_cast<const uint16_t*>(it.b);
+        uint32_t* o = packed.back().data();
+        for (uint64_t j = 0; j < it.n; ++j) {
+          o[j] = (uint32_t)sv[j] | ((uint32_t)fl[j] << 16);
+          mx = sv[j] > mx ? sv[j] : mx;
+        }
+        err = hipMemcpyAsync(it.dst, o, bytes, hipMemcpyHostToDevice, ctx->stream);
+      }
+      done[i] = 1;
+      continue;
+    }
+    if (it.kind == 0) {
+      if (!reg(it.a, it.n)) continue;
+      err = hipMemcpyAsync(it.dst, it.a, it.n, hipMemcpyHostToDevice, ctx->stream);
+      done[i] = 1;
+      continue;
+    }
+    // svc | flags: both u16 columns registered and copied into the scratch,
+    // packed on the device (one such item per call: the scratch holds one)
+    if (d_mx) continue;
+    if (!reg(it.a, it.n * 2)) continue;
+    if (!reg(it.b, it.n * 2)) {
+      unreg_last();
+      continue;
+    }
+    void* scr = nullptr;
+    const uint64_t half = (it.n * 2 + 255) & ~255ull;
+    if (ensure_scratch(ctx, kScratchUpload, 2 * half + 256, &scr) != ANOMOD_OK) {
+      unreg_last();
+      unreg_last();
+      continue;
+    }
+    char* base = static_cast<char*>(scr);
+    auto* dsv = reinterpret_cast<uint16_t*>(base);
+    auto* dfl = reinterpret_cast<uint16_t*>(base + half);
+    d_mx = reinterpret_cast<unsigned int*>(base + 2 * half);
+    err = hipMemcpyAsync(dsv, it.a, it.n * 2, hipMemcpyHostToDevice, ctx->stream);
+    if (err == hipSuccess)
+      err = hipMemcpyAsync(dfl, it.b, it.n * 2, hipMemcpyHostToDevice, ctx->stream);
+    if (err == hipSuccess) err = hipMemsetAsync(d_mx, 0, 4, ctx->stream);
+    if (err == hipSuccess) {
+      const uint64_t blocks = std::min<uint64_t>((it.n + 255) / 256, (uint64_t)ctx->num_cus * 8);
+      hipLaunchKernelGGL(pack_svc_flags_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                         dsv, dfl, static_cast<uint32_t*>(it.dst), it.n, d_mx);
+      err = hipGetLastError();
+    }
+    done[i] = 1;
   }
-  u->pieces.clear();
-  for (int i = 0; i < n_items; ++i) {
-    if (direct[i]) continue;
-    const uint64_t unit = items[i].kind == 1 ? Uploader::kPiece / 4 : Uploader::kPiece;
-    for (uint64_t off = 0; off < items[i].n; off += unit)
-      u->pieces.push_back({i, off, std::min<uint64_t>(unit, items[i].n - off)});
-  }
-  if (!u->pieces.empty()) {
+  // the rest (a refused registration, or ANOMOD_UPLOAD_DIRECT=0): the bounce
+  // pipeline, its DMAs on one stream beside the ctx stream's direct copies
+  bool rest = false;
+  for (int i = 0; i < n_items; ++i) rest = rest || !done[i];
+  Uploader* u = nullptr;
+  if (rest && err == hipSuccess) {
+    if (int rc = make_uploader(ctx)) {
+      (void)hipStreamSynchronize(ctx->stream);
+      for (const void* a : registered) (void)hipHostUnregister(const_cast<void*>(a));
+      return rc;
+    }
+    u = ctx->uploader;
+    u->pieces.clear();
+    for (int i = 0; i < n_items; ++i) {
+      if (done[i]) continue;
+      const uint64_t unit = items[i].kind == 1 ? Uploader::kPiece / 4 : Uploader::kPiece;
+      for (uint64_t off = 0; off < items[i].n; off += unit)
+        u->pieces.push_back({i, off, std::min<uint64_t>(unit, items[i].n - off)});
+    }
     std::unique_lock<std::mutex> lk(u->m);
-    u->one_stream = !registered.empty();
+    u->one_stream = done != std::vector<char>(n_items, 0);
     u->items = items;
     u->pending = u->nw;
     ++u->gen;
     u->cv_go.notify_all();
     u->cv_done.wait(lk, [&] { return u->pending == 0; });
-  } else {
-    for (int w = 0; w < u->nw; ++w) u->werr[w] = hipSuccess, u->wmax[w] = 0u;
   }
-  const hipError_t dsync = hipStreamSynchronize(u->direct);
-  if (derr == hipSuccess) derr = dsync;
+  const hipError_t sync = hipStreamSynchronize(ctx->stream);
+  if (err == hipSuccess) err = sync;
+  uint32_t dmx = 0;
+  if (err == hipSuccess && d_mx) err = hipMemcpy(&dmx, d_mx, 4, hipMemcpyDeviceToHost);
   for (const void* a : registered) (void)hipHostUnregister(const_cast<void*>(a));
-  if (derr != hipSuccess) {
-    set_error(ctx, "span upload (direct copy) failed: %s", hipGetErrorString(derr));
+  if (err != hipSuccess) {
+    set_error(ctx, "span upload failed: %s", hipGetErrorString(err));
     return ANOMOD_EHIP;
   }
-  uint32_t mx = 0;
-  for (int w = 0; w < u->nw; ++w) {
+  mx = std::max(mx, dmx);
+  for (int w = 0; u && w < u->nw; ++w) {
     if (u->werr[w] != hipSuccess) {
       set_error(ctx, "span upload failed: %s", hipGetErrorString(u->werr[w]));
       return ANOMOD_EHIP;

@@ -1,10 +1,14 @@
-"""GPU: the host -> device span upload pipeline (csrc/upload.hip) — the
-columns cut into 8-MiB pieces (2 Mi packed svc|flags elements) dealt to W
-worker threads with their own streams and pinned buffers.  Every column must
-arrive bit-equal whatever the worker count and wherever the piece cuts fall,
-the largest service must come from the packing pass, and the context's reused
-host-call set (anomod_edge_aggregate_host) must never show a previous call's
-spans."""
+"""GPU: the host -> device span upload (csrc/upload.hip).  Direct (default):
+columns of at least a piece registered for the call and copied from the
+caller's pages, svc | flags copied as two u16 columns and packed on the
+device, smaller items from pageable memory (svc | flags packed on the host).
+Bounce (a refused registration, or ANOMOD_UPLOAD_DIRECT=0): the columns cut
+into 8-MiB pieces (2 Mi packed svc|flags elements) dealt to W worker threads
+with their own streams and pinned buffers.  Every column must arrive
+bit-equal whatever the path, the worker count and wherever the piece cuts
+fall, the largest service must come from whichever packing ran, and the
+context's reused host-call set (anomod_edge_aggregate_host) must never show
+a previous call's spans."""
 import numpy as np
 import pytest
 
@@ -38,12 +42,14 @@ def _assert_columns_equal(a: anomod.SpanSet, b: anomod.SpanSet):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
 
 
-@pytest.mark.parametrize("threads", ["1", "3", "8"])
-def test_upload_roundtrip_piece_cuts(monkeypatch, threads):
+@pytest.mark.parametrize("threads,direct", [("1", "0"), ("3", "0"), ("8", "0"), ("8", "1")])
+def test_upload_roundtrip_piece_cuts(monkeypatch, threads, direct):
     """Sizes around the piece cuts of both item kinds (u64 columns: 2^20
     elements a piece; packed svc|flags: 2^21), one span, and none — through a
-    fresh context whose pipeline has `threads` workers."""
+    fresh context whose bounce pipeline has `threads` workers (direct "0"),
+    or the direct path (small items pageable, large ones registered)."""
     monkeypatch.setenv("ANOMOD_UPLOAD_THREADS", threads)
+    monkeypatch.setenv("ANOMOD_UPLOAD_DIRECT", direct)
     rng = np.random.default_rng(int(threads))
     with anomod.Context(0) as c:
         for n in (0, 1, PIECE_U64 - 1, PIECE_U64 + 1, PIECE_PACKED + 3, 3 * PIECE_U64 + 5):
@@ -53,11 +59,22 @@ def test_upload_roundtrip_piece_cuts(monkeypatch, threads):
             dev.free()
 
 
-def test_upload_max_service_from_packing(ctx):
-    """The set's largest service comes from the workers' packing pass: a set
-    whose one out-of-range service sits in the last piece of a multi-piece
-    upload is refused by the aggregation (not silently indexed past the
-    table); the same set in range aggregates oracle-equal."""
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_upload_max_service_from_packing(ctx, monkeypatch, direct):
+    """The set's largest service comes from the packing — the device pack
+    kernel (direct) or the workers' pass (bounce): a set whose one
+    out-of-range service sits in the last piece of a multi-piece upload is
+    refused by the aggregation (not silently indexed past the table); the
+    same set in range aggregates oracle-equal.  A small set (host packing)
+    likewise."""
+    monkeypatch.setenv("ANOMOD_UPLOAD_DIRECT", direct)
+    small = _random_spanset(np.random.default_rng(6), 12, 50, 9)
+    sbad = small.svc.copy()
+    sbad[-1] = 12
+    with pytest.raises(anomod.AnomodError, match="service index 12"):
+        ctx.edge_aggregate(anomod.SpanSet(small.services, small.trace_ptr, small.trace_hash,
+                                          small.span_id, small.parent_span_id, sbad,
+                                          small.flags, small.dur_us))
     rng = np.random.default_rng(5)
     sp = _random_spanset(rng, 12, PIECE_PACKED // 3, 9)
     n = sp.n_spans
