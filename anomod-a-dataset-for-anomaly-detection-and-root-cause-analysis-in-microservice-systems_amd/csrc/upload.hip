@@ -1,6 +1,7 @@
-// Host -> device span upload through a pinned staging pipeline (the product
-// path's one conversion per experiment: collect_trace.sh:70 converts each
-// dump once, then every feature is computed from it).
+// Host -> device span upload (the product path's one conversion per
+// experiment: collect_trace.sh:70 converts each dump once, then every feature
+// is computed from it): DMA from the caller's registered pages, with a pinned
+// staging pipeline as the fallback (history below).
 //
 // r04 uploaded with pageable hipMemcpyAsync calls after two serial host passes
 // (the max-service scan and a fresh svc|flags packing vector): 108.9 ms for
