@@ -205,6 +205,7 @@ _SIGS = {
     "anomod_metrics_series_name": (C.c_char_p, [_vp, _u64]),
     "anomod_metrics_series_nlabels": (_u32, [_vp, _u64]),
     "anomod_metrics_series_label": (C.c_char_p, [_vp, _u64, _u32, _P(C.c_char_p)]),
+    "anomod_metrics_series_packed": (_i32, [_vp, C.c_char_p, _u64, _P(_u32), _P(_u64)]),
     "anomod_metrics_free": (_i32, [_vp]),
     "anomod_ewma_z": (_i32, [_vp, _P(_f32), _u64, _u64, _f32, _u32, _f32, _P(_f32)]),
     "anomod_series_create": (_i32, [_vp, _u64, _u64, _P(_vp)]),

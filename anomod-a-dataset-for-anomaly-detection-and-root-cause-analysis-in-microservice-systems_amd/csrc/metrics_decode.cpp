@@ -60,6 +60,26 @@ namespace {
 
 using Labels = std::vector<std::pair<std::string, std::string>>;
 
+// First byte of [p, end) that is ',', '\n' or '\r' (end if none): eight bytes
+// at a time (a zero byte of x ^ c marks a match; the classic haszero test
+// can flag a 0x01 byte after a true match, never before one, so the lowest
+// flagged byte is exact).
+inline const char* field_end(const char* p, const char* end) {
+  constexpr uint64_t kOnes = 0x0101010101010101ull, kHigh = 0x8080808080808080ull;
+  while (end - p >= 8) {
+    uint64_t x;
+    memcpy(&x, p, 8);
+    const uint64_t a = x ^ (kOnes * (uint8_t)','), n = x ^ (kOnes * (uint8_t)'\n'),
+                   r = x ^ (kOnes * (uint8_t)'\r');
+    const uint64_t m = ((a - kOnes) & ~a & kHigh) | ((n - kOnes) & ~n & kHigh) |
+                       ((r - kOnes) & ~r & kHigh);
+    if (m) return p + (__builtin_ctzll(m) >> 3);
+    p += 8;
+  }
+  while (p < end && *p != ',' && *p != '\n' && *p != '\r') ++p;
+  return p;
+}
+
 // One CSV record: field views (quoted fields with "" escapes are unescaped
 // into `scratch`, which stays alive until the next record).
 struct CsvReader {
@@ -104,7 +124,7 @@ struct CsvReader {
         fields.emplace_back(s);
       } else {
         const char* f = p;
-        while (p < end && *p != ',' && *p != '\n' && *p != '\r') ++p;
+        p = field_end(p, end);
         fields.emplace_back(f, (size_t)(p - f));
       }
       if (p < end && *p == ',') {
@@ -275,6 +295,8 @@ struct SampleRun {
   const std::vector<uint32_t>* map;
 };
 
+int metric_threads();
+
 struct Builder {
   std::unordered_map<std::string, uint32_t> index;  // serialised key -> provisional series
   std::vector<std::string> keys;                      // by series id (the fast path's keys)
@@ -371,17 +393,38 @@ struct Builder {
     out->ts.swap(sorted_ts);
     const size_t T = out->ts.size(), S = out->series.size();
     out->X.assign(T * S, std::nanf(""));
-    // first occurrence per (series, t): later rows of the same cell skipped
+    // first occurrence per (series, t): later rows of the same cell skipped.
+    // Series-major rows put consecutive samples S cells apart in X[T][S], one
+    // cache miss each on one thread; so the series ranks are cut into ranges,
+    // one per thread, and every thread walks all samples in row order and
+    // writes only its own columns (a T x S/threads block that stays in cache).
+    // Cells are disjoint between threads and each cell sees its samples in
+    // row order, so the result is the one-thread one.
     std::vector<uint8_t> seen(T * S, 0);
-    i = 0;
-    for (const SampleRun& r : runs)  // samples in row order
-      for (const Sample& sm : *r.samples) {
-        const uint32_t sid = r.map ? (*r.map)[sm.series] : sm.series;
-        const size_t cell = (size_t)crank[col[i++]] * S + rank[sid];
-        if (seen[cell]) continue;
-        seen[cell] = 1;
-        out->X[cell] = sm.v;
-      }
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)metric_threads(),
+                                                             n_samples / (1u << 16)));
+    auto fill = [&](uint32_t lo, uint32_t hi) {
+      size_t j = 0;
+      for (const SampleRun& r : runs)  // samples in row order
+        for (const Sample& sm : *r.samples) {
+          const uint32_t c = col[j++];
+          const uint32_t rk = rank[r.map ? (*r.map)[sm.series] : sm.series];
+          if (rk < lo || rk >= hi) continue;
+          const size_t cell = (size_t)crank[c] * S + rk;
+          if (seen[cell]) continue;
+          seen[cell] = 1;
+          out->X[cell] = sm.v;
+        }
+    };
+    if (nt <= 1) {
+      fill(0, (uint32_t)S);
+    } else {
+      std::vector<std::thread> th;
+      for (int k = 0; k < nt; ++k)
+        th.emplace_back(fill, (uint32_t)(S * (size_t)k / (size_t)nt),
+                        (uint32_t)(S * (size_t)(k + 1) / (size_t)nt));
+      for (auto& x : th) x.join();
+    }
     return out;
   }
 };
@@ -414,7 +457,9 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
                      uint64_t row0) {
   CsvReader rd(p, (size_t)(end - p));
   Labels labels;
-  std::string key;
+  std::string key, prev_key;
+  uint32_t prev_s = 0;
+  bool have_prev = false;
   uint64_t row = row0;
   while (rd.next()) {
     if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;  // blank line (skipped)
@@ -445,15 +490,21 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
                         (int)vs.size(), vs.data());
       return ANOMOD_EINVAL;
     }
-    const uint32_t s = b.series_of_key(key, [&] {
-      labels.clear();
-      for (int c : H.label_cols) {
-        const std::string_view lv = field(c);
-        if (!lv.empty()) labels.emplace_back(H.hdr[c], std::string(lv));
-      }
-      return anomod_metrics::Series{std::string(nm), labels};
-    });
-    b.samples.push_back({t, (float)v, s});
+    // series-major files: the row's series is usually the previous row's
+    // (one compare instead of hashing the key)
+    if (!have_prev || key != prev_key) {
+      prev_s = b.series_of_key(key, [&] {
+        labels.clear();
+        for (int c : H.label_cols) {
+          const std::string_view lv = field(c);
+          if (!lv.empty()) labels.emplace_back(H.hdr[c], std::string(lv));
+        }
+        return anomod_metrics::Series{std::string(nm), labels};
+      });
+      prev_key.swap(key);
+      have_prev = true;
+    }
+    b.samples.push_back({t, (float)v, prev_s});
   }
   return ANOMOD_OK;
 }
@@ -690,6 +741,37 @@ const char* anomod_metrics_series_label(const anomod_metrics* m, uint64_t s, uin
   if (!m || s >= m->series.size() || j >= m->series[s].labels.size()) return nullptr;
   if (value) *value = m->series[s].labels[j].second.c_str();
   return m->series[s].labels[j].first.c_str();
+}
+
+int anomod_metrics_series_packed(const anomod_metrics* m, char* buf, uint64_t cap,
+                                 uint32_t* nlabels, uint64_t* bytes) {
+  if (!m || !bytes) {
+    anomod::set_error(nullptr, "anomod_metrics_series_packed: NULL argument");
+    return ANOMOD_EINVAL;
+  }
+  uint64_t need = 0;
+  for (size_t s = 0; s < m->series.size(); ++s) {
+    const auto& sr = m->series[s];
+    need += sr.name.size() + 1;
+    for (const auto& kv : sr.labels) need += kv.first.size() + kv.second.size() + 2;
+    if (nlabels) nlabels[s] = (uint32_t)sr.labels.size();
+  }
+  *bytes = need;
+  if (!buf || cap < need) return ANOMOD_OK;
+  char* o = buf;
+  auto put = [&](const std::string& x) {
+    memcpy(o, x.data(), x.size());
+    o += x.size();
+    *o++ = '\0';
+  };
+  for (const auto& sr : m->series) {
+    put(sr.name);
+    for (const auto& kv : sr.labels) {
+      put(kv.first);
+      put(kv.second);
+    }
+  }
+  return ANOMOD_OK;
 }
 
 int anomod_metrics_free(anomod_metrics* m) {

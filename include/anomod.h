@@ -306,6 +306,11 @@ const char* anomod_metrics_series_name(const anomod_metrics* m, uint64_t s);
 uint32_t anomod_metrics_series_nlabels(const anomod_metrics* m, uint64_t s);
 const char* anomod_metrics_series_label(const anomod_metrics* m, uint64_t s, uint32_t j,
                                         const char** value);
+/* every series at once: name \0 (label name \0 label value \0) x nlabels[s],
+ * series after series; *bytes = the size needed.  buf == NULL or cap < *bytes
+ * writes nothing but *bytes (and nlabels, when given: [S]). */
+int anomod_metrics_series_packed(const anomod_metrics* m, char* buf, uint64_t cap,
+                                 uint32_t* nlabels, uint64_t* bytes);
 int anomod_metrics_free(anomod_metrics* m);
 
 /* ---- edge aggregation (the hot path) -------------------------------------

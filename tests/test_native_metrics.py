@@ -101,3 +101,45 @@ def test_bad_rows_raise():
         anomod.decode_metric_long_csv_native(b"metric_name,timestamp,datetime,value\nup,x,y,1\n")
     with pytest.raises(anomod.AnomodError):
         anomod.decode_metric_long_csv_native(b"metric_name,timestamp,datetime,value\nup,1,y,zz\n")
+
+
+@pytest.mark.parametrize("order", ["series_major", "shuffled"])
+def test_long_csv_threaded_pieces_and_fill(order, tmp_path, monkeypatch):
+    """A long CSV over the 8-MiB piece threshold (parsed in newline-aligned
+    pieces on several threads) with enough samples that the matrix fill runs
+    on several threads too (series-rank ranges, every thread walking the
+    samples in row order): series with 0, 1 and 2 labels, repeated
+    (series, timestamp) rows with other values (the first row must win, also
+    when the repeats land in another piece), missing values, rows in series-
+    major or shuffled order.  Equal on 1 and 8 threads, and to the Python
+    decoder."""
+    rng = random.Random(3 if order == "shuffled" else 4)
+    cols = ["metric_name", "timestamp", "datetime", "value", "instance", "service"]
+    series = [(f"m{k % 37}", f"10.0.0.{k % 7}" if k % 3 else "", f"svc{k % 11}" if k % 5 else "")
+              for k in range(1100)]
+    rows = []
+    for name, inst, svc in series:
+        for t in range(0, 15 * 180, 15):
+            v = "" if rng.random() < 0.01 else repr(round(rng.uniform(0, 1e4), 6))
+            rows.append([name, str(t), "1970-01-01 00:00:00", v, inst, svc])
+    dups = [list(r) for r in rng.sample(rows, 8000)]
+    for r in dups:
+        r[3] = repr(round(rng.uniform(-1e4, 0), 6))  # later rows of a cell: skipped
+    rows = rows + dups  # (shuffled: a repeat may come first, and then it is the one kept)
+    if order == "shuffled":
+        rng.shuffle(rows)
+    buf = io.StringIO()
+    w = csv.writer(buf, lineterminator="\n")
+    w.writerow(cols)
+    w.writerows(rows)
+    data = buf.getvalue().encode()
+    assert len(data) > (8 << 20) + (1 << 20)
+    p = tmp_path / "m.csv"
+    p.write_bytes(data)
+    monkeypatch.setenv("ANOMOD_DECODE_THREADS", "1")
+    one = anomod.decode_metric_long_csv_native(p)
+    monkeypatch.setenv("ANOMOD_DECODE_THREADS", "8")
+    many = anomod.decode_metric_long_csv_native(p)
+    _same(many, one)
+    _same(one, anomod.decode_metric_long_csv(p))
+    assert one.S == len(set(series)) and one.T == 180
