@@ -283,16 +283,19 @@ bool iso_timestamp(std::string_view s, double& out) {
 }
 
 struct Sample {  // kept in row order: the first occurrence of a cell wins
-  double t;
+  uint32_t lc;      // the piece's timestamp column (Piece::lts)
   float v;
-  uint32_t series;
+  uint32_t series;  // the piece's series id
 };
 
-// A run of samples in row order whose series ids go through `map` (nullptr:
-// the builder's own ids).
-struct SampleRun {
-  const std::vector<Sample>* samples;
-  const std::vector<uint32_t>* map;
+// One parser's samples in row order, with what finish() needs to place them
+// without another pass over them: the distinct timestamps in first-seen order
+// (samples refer to them by index) and the runs of rows of one series.
+struct Piece {
+  std::vector<Sample> samples;
+  std::vector<double> lts;               // distinct timestamps, first-seen order
+  std::vector<uint32_t> run_at, run_sid;  // series runs: first sample, series id
+  std::vector<uint32_t> map;             // piece series -> builder series (empty: identity)
 };
 
 int metric_threads();
@@ -301,11 +304,39 @@ struct Builder {
   std::unordered_map<std::string, uint32_t> index;  // serialised key -> provisional series
   std::vector<std::string> keys;                      // by series id (the fast path's keys)
   std::vector<anomod_metrics::Series> series;
-  std::vector<Sample> samples;
-  std::vector<SampleRun> runs;  // set by the threaded decode: the pieces' samples, in file order
-  std::deque<std::vector<Sample>> part_samples;  // (deque: stable addresses for runs)
-  std::deque<std::vector<uint32_t>> part_maps;
+  Piece own;                // the rows this builder parsed itself
+  std::deque<Piece> parts;  // set by the threaded decode: the pieces, in file order
   std::string key;
+  // the timestamp column of the next row: series-major files repeat one
+  // series' timestamps in order, so the column after the previous row's is
+  // the usual answer (no hash lookup)
+  std::unordered_map<double, uint32_t> lidx;
+  double last_t = std::nan("");
+  uint32_t last_lc = 0, last_s = ~0u;
+
+  void add(double t, float v, uint32_t s) {
+    uint32_t lc;
+    if (t == last_t) {  // (NaN never matches: timestamps are never NaN)
+      lc = last_lc;
+    } else if (last_lc + 1 < own.lts.size() && own.lts[last_lc + 1] == t) {
+      lc = last_lc + 1;
+    } else {
+      auto it = lidx.find(t);
+      if (it == lidx.end()) {
+        it = lidx.emplace(t, (uint32_t)own.lts.size()).first;
+        own.lts.push_back(t);
+      }
+      lc = it->second;
+    }
+    last_t = t;
+    last_lc = lc;
+    if (s != last_s) {
+      own.run_at.push_back((uint32_t)own.samples.size());
+      own.run_sid.push_back(s);
+      last_s = s;
+    }
+    own.samples.push_back({lc, v, s});
+  }
 
   // Series id of a key already serialised as name \0 k1 \0 v1 ...; `make`
   // builds the (name, labels) only when the series is new.
@@ -349,37 +380,27 @@ struct Builder {
     for (uint32_t i = 0; i < order.size(); ++i) rank[order[i]] = i;
     out->series.reserve(series.size());
     for (uint32_t i : order) out->series.push_back(std::move(series[i]));
-    // distinct timestamps: a hash map to a provisional column, then sorted
-    if (runs.empty()) runs.push_back({&samples, nullptr});
+    std::vector<const Piece*> ps;
+    if (parts.empty()) ps.push_back(&own);
+    for (const Piece& p : parts) ps.push_back(&p);
+    // distinct timestamps over the pieces (a hash map to a provisional column,
+    // then sorted); each piece's columns -> output rows
+    std::unordered_map<double, uint32_t> gidx;
+    gidx.reserve(1024);
+    std::vector<std::vector<uint32_t>> row_of(ps.size());
     size_t n_samples = 0;
-    for (const SampleRun& r : runs) n_samples += r.samples->size();
-    std::unordered_map<double, uint32_t> col_of;
-    col_of.reserve(1024);
-    std::vector<uint32_t> col(n_samples);
-    double last = std::nan("");
-    uint32_t last_c = 0;
-    size_t i = 0;
-    for (const SampleRun& r : runs)
-    for (const Sample& sm : *r.samples) {
-      const double t = sm.t;
-      if (t == last) {  // (NaN never matches: timestamps are never NaN)
-        col[i++] = last_c;
-        continue;
+    for (size_t k = 0; k < ps.size(); ++k) {
+      n_samples += ps[k]->samples.size();
+      row_of[k].resize(ps[k]->lts.size());
+      for (size_t j = 0; j < ps[k]->lts.size(); ++j) {
+        const double t = ps[k]->lts[j];
+        auto it = gidx.find(t);
+        if (it == gidx.end()) {
+          it = gidx.emplace(t, (uint32_t)out->ts.size()).first;
+          out->ts.push_back(t);
+        }
+        row_of[k][j] = it->second;
       }
-      // series-major files repeat the first series' timestamps in order: the
-      // column after the previous row's is the usual answer (no hash lookup)
-      if (last_c + 1 < out->ts.size() && out->ts[last_c + 1] == t) {
-        last = t;
-        col[i++] = ++last_c;
-        continue;
-      }
-      auto it = col_of.find(t);
-      if (it == col_of.end()) {
-        it = col_of.emplace(t, (uint32_t)out->ts.size()).first;
-        out->ts.push_back(t);
-      }
-      last = t;
-      last_c = col[i++] = it->second;
     }
     std::vector<uint32_t> ord(out->ts.size());
     for (uint32_t k = 0; k < ord.size(); ++k) ord[k] = k;
@@ -391,30 +412,39 @@ struct Builder {
       sorted_ts[k] = out->ts[ord[k]];
     }
     out->ts.swap(sorted_ts);
+    for (auto& r : row_of)
+      for (uint32_t& x : r) x = crank[x];
     const size_t T = out->ts.size(), S = out->series.size();
     out->X.assign(T * S, std::nanf(""));
     // first occurrence per (series, t): later rows of the same cell skipped.
     // Series-major rows put consecutive samples S cells apart in X[T][S], one
     // cache miss each on one thread; so the series ranks are cut into ranges,
-    // one per thread, and every thread walks all samples in row order and
-    // writes only its own columns (a T x S/threads block that stays in cache).
-    // Cells are disjoint between threads and each cell sees its samples in
-    // row order, so the result is the one-thread one.
+    // one per thread, and every thread walks the pieces' series runs in row
+    // order, taking only the runs of its own series (its writes stay in a
+    // T x S/threads block).  Cells are disjoint between threads and each cell
+    // sees its samples in row order, so the result is the one-thread one.
     std::vector<uint8_t> seen(T * S, 0);
     const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)metric_threads(),
                                                              n_samples / (1u << 16)));
     auto fill = [&](uint32_t lo, uint32_t hi) {
-      size_t j = 0;
-      for (const SampleRun& r : runs)  // samples in row order
-        for (const Sample& sm : *r.samples) {
-          const uint32_t c = col[j++];
-          const uint32_t rk = rank[r.map ? (*r.map)[sm.series] : sm.series];
+      for (size_t k = 0; k < ps.size(); ++k) {
+        const Piece& P = *ps[k];
+        const uint32_t* row = row_of[k].data();
+        const size_t nr = P.run_at.size();
+        for (size_t r = 0; r < nr; ++r) {
+          const uint32_t sid = P.run_sid[r];
+          const uint32_t rk = rank[P.map.empty() ? sid : P.map[sid]];
           if (rk < lo || rk >= hi) continue;
-          const size_t cell = (size_t)crank[c] * S + rk;
-          if (seen[cell]) continue;
-          seen[cell] = 1;
-          out->X[cell] = sm.v;
+          const size_t a = P.run_at[r], b = r + 1 < nr ? P.run_at[r + 1] : P.samples.size();
+          for (size_t i = a; i < b; ++i) {
+            const Sample& sm = P.samples[i];
+            const size_t cell = (size_t)row[sm.lc] * S + rk;
+            if (seen[cell]) continue;
+            seen[cell] = 1;
+            out->X[cell] = sm.v;
+          }
         }
+      }
     };
     if (nt <= 1) {
       fill(0, (uint32_t)S);
@@ -504,7 +534,7 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
       prev_key.swap(key);
       have_prev = true;
     }
-    b.samples.push_back({t, (float)v, prev_s});
+    b.add(t, (float)v, prev_s);
   }
   return ANOMOD_OK;
 }
@@ -578,16 +608,15 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
         anomod::set_error(nullptr, "out of host memory decoding a metric CSV");
       if (rc[k] != ANOMOD_OK) return rc[k];  // (row numbers in the message are per piece)
     }
-    // the pieces' series into the builder (file order), their samples
-    // referenced in place, not copied
+    // the pieces' series into the builder (file order); their samples move
+    // with them, not copied
     for (size_t k = 0; k < np; ++k) {
       Builder& pb = part[k];
-      b.part_maps.emplace_back(pb.series.size());
-      std::vector<uint32_t>& map = b.part_maps.back();
+      b.parts.push_back(std::move(pb.own));
+      std::vector<uint32_t>& map = b.parts.back().map;
+      map.resize(pb.series.size());
       for (size_t s = 0; s < pb.series.size(); ++s)
         map[s] = b.series_of_key(pb.keys[s], [&] { return std::move(pb.series[s]); });
-      b.part_samples.push_back(std::move(pb.samples));
-      b.runs.push_back({&b.part_samples.back(), &map});
     }
     return ANOMOD_OK;
   }
@@ -628,7 +657,7 @@ int decode_prom(const char* data, uint64_t len, const std::string& stem, Builder
     }
     labels[0].second.assign(field(c_met));
     const uint32_t s = b.series_of(stem, labels);
-    b.samples.push_back({t, (float)v, s});
+    b.add(t, (float)v, s);
   }
   return ANOMOD_OK;
 }
