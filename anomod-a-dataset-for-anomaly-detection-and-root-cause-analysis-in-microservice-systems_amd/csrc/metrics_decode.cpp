@@ -23,6 +23,10 @@
 // 1e6), timestamps = the sorted distinct values over all rows, series sorted
 // as Python sorts the key tuples, X f32 with NaN where a series has no row.
 #include <algorithm>
+#ifdef ANOMOD_DECODE_TIMING
+#include <chrono>
+#include <cstdio>
+#endif
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -58,6 +62,19 @@ struct anomod_metrics {
 };
 
 namespace {
+
+#ifdef ANOMOD_DECODE_TIMING  // stage times to stderr (scripts/r06/decode_stages.sh only)
+void dt_mark(const char* name) {
+  static auto last = std::chrono::steady_clock::now();
+  const auto now = std::chrono::steady_clock::now();
+  fprintf(stderr, "  %-14s %8.2f ms\n", name,
+          std::chrono::duration<double, std::milli>(now - last).count());
+  last = now;
+}
+#define DT_MARK(name) dt_mark(name)
+#else
+#define DT_MARK(name) ((void)0)
+#endif
 
 using Labels = std::vector<std::pair<std::string, std::string>>;
 
@@ -400,21 +417,38 @@ struct Builder {
     if (it != index.end()) return it->second;
     const uint32_t id = (uint32_t)series.size();
     index.emplace(key, id);
+    keys.push_back(key);
     series.push_back({name, labels});
     return id;
   }
 
   anomod_metrics* finish() {
+    DT_MARK("decode return");
     auto* out = new anomod_metrics();
-    // series in Python tuple order
+    // series in Python tuple order: the serialised keys (name \0 k1 \0 v1 ...,
+    // no NUL inside a field) compare bytewise as the (name, labels) tuples do —
+    // a name or field that is a prefix of another ends at \0, which sorts first,
+    // and a key with fewer labels ends first — so one memcmp per comparison
     std::vector<uint32_t> order(series.size());
     for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-      if (series[a].name != series[b].name) return series[a].name < series[b].name;
-      return series[a].labels < series[b].labels;
-    });
+    bool nul = keys.size() != series.size();
+    for (size_t i = 0; !nul && i < series.size(); ++i) {
+      nul = series[i].name.find('\0') != std::string::npos;
+      for (const auto& kv : series[i].labels)
+        nul = nul || kv.first.find('\0') != std::string::npos ||
+              kv.second.find('\0') != std::string::npos;
+    }
+    if (!nul) {
+      std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+    } else {
+      std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        if (series[a].name != series[b].name) return series[a].name < series[b].name;
+        return series[a].labels < series[b].labels;
+      });
+    }
     std::vector<uint32_t> rank(series.size());
     for (uint32_t i = 0; i < order.size(); ++i) rank[order[i]] = i;
+    DT_MARK("series sort");
     out->series.reserve(series.size());
     for (uint32_t i : order) out->series.push_back(std::move(series[i]));
     std::vector<const Piece*> ps;
@@ -451,6 +485,7 @@ struct Builder {
     out->ts.swap(sorted_ts);
     for (auto& r : row_of)
       for (uint32_t& x : r) x = crank[x];
+    DT_MARK("timestamps");
     const size_t T = out->ts.size(), S = out->series.size();
     out->X.assign(T * S, std::nanf(""));
     // first occurrence per (series, t): later rows of the same cell skipped.
@@ -461,6 +496,7 @@ struct Builder {
     // T x S/threads block).  Cells are disjoint between threads and each cell
     // sees its samples in row order, so the result is the one-thread one.
     std::vector<uint8_t> seen(T * S, 0);
+    DT_MARK("X alloc");
     const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)metric_threads(),
                                                              n_samples / (1u << 16)));
     auto fill = [&](uint32_t lo, uint32_t hi) {
@@ -492,6 +528,7 @@ struct Builder {
                         (uint32_t)(S * (size_t)(k + 1) / (size_t)nt));
       for (auto& x : th) x.join();
     }
+    DT_MARK("fill");
     return out;
   }
 };
@@ -637,6 +674,7 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
         }
       });
     for (auto& x : th) x.join();
+    DT_MARK("parse");
     bool any_quote = false;
     for (size_t k = 0; k < np; ++k) any_quote |= quoted[k] != 0;
     if (any_quote) return decode_long_rows(H, body, end, b, 0);
@@ -655,6 +693,7 @@ int decode_long(const char* data, uint64_t len, Builder& b) {
       for (size_t s = 0; s < pb.series.size(); ++s)
         map[s] = b.series_of_key(pb.keys[s], [&] { return std::move(pb.series[s]); });
     }
+    DT_MARK("merge");
     return ANOMOD_OK;
   }
   return decode_long_rows(H, body, end, b, 0);
@@ -710,9 +749,14 @@ int anomod_decode_metric_long_csv(const char* data, uint64_t len, anomod_metrics
   }
   *out = nullptr;
   try {
-    Builder b;
-    if (int rc = decode_long(data, len, b)) return rc;
-    *out = b.finish();
+    DT_MARK("start");
+    {
+      Builder b;
+      if (int rc = decode_long(data, len, b)) return rc;
+      *out = b.finish();
+      DT_MARK("finish");
+    }
+    DT_MARK("builder free");
   } catch (const std::bad_alloc&) {
     anomod::set_error(nullptr, "out of host memory decoding a metric CSV");
     return ANOMOD_ENOMEM;
