@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import math
 import re
+import threading
 from dataclasses import dataclass, field
 from pathlib import Path
 
@@ -124,13 +125,32 @@ def load_experiment(source, *, metrics=None, name: str | None = None,
             if not cands:
                 raise FileNotFoundError(f"no trace JSON under {path}")
             doc_path = cands[-1]
-    spans = decode.load_trace_file(doc_path, services)
-    mm = None
+    # the metric file decodes on a second host thread while the trace file
+    # decodes here: both decoders are native and release the GIL, and each
+    # has a serial stretch the other's threads fill
+    got: dict = {}
+    worker = None
     if metrics is not None:
         mp = Path(metrics)
-        mm = (decode.decode_prometheus_csv_dir_native(mp) if mp.is_dir()
-              else decode.decode_metric_long_csv_native(mp))
-    return Experiment(exp_name, spans, mm, fault_target(exp_name), {"trace_file": str(doc_path)})
+
+        def _metrics():
+            try:
+                got["m"] = (decode.decode_prometheus_csv_dir_native(mp) if mp.is_dir()
+                            else decode.decode_metric_long_csv_native(mp))
+            except BaseException as e:  # noqa: BLE001 (re-raised below)
+                got["e"] = e
+
+        worker = threading.Thread(target=_metrics, name="anomod-metrics-decode")
+        worker.start()
+    try:
+        spans = decode.load_trace_file(doc_path, services)
+    finally:
+        if worker is not None:
+            worker.join()
+    if "e" in got:
+        raise got["e"]
+    return Experiment(exp_name, spans, got.get("m"), fault_target(exp_name),
+                      {"trace_file": str(doc_path)})
 
 
 @dataclass
