@@ -29,6 +29,7 @@
 // register, or when ANOMOD_UPLOAD_DIRECT=0 asks for it.
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -37,6 +38,18 @@
 #include "common.h"
 
 namespace anomod {
+
+#ifdef ANOMOD_UPLOAD_TIMING  // step times to stderr (timing-only builds, scripts/r06)
+void ut_mark(const char* step) {
+  static double last = host_now_ms();
+  const double now = host_now_ms();
+  fprintf(stderr, "upload %-28s %8.2f ms\n", step, now - last);
+  last = now;
+}
+#define UT_MARK(step) ut_mark(step)
+#else
+#define UT_MARK(step) ((void)0)
+#endif
 
 struct Uploader {
   static constexpr size_t kPiece = size_t(8) << 20;  // bytes of device data per piece
@@ -206,6 +219,7 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
   // the ctx stream's earlier work on these buffers (a previous call's kernels
   // reading a reused set) must be done before other streams write them
   ANOMOD_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  UT_MARK("enter + stream sync");
   const char* de = getenv("ANOMOD_UPLOAD_DIRECT");
   const bool direct_ok = !(de && de[0] == '0');
   std::vector<const void*> registered;
@@ -255,7 +269,9 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
     }
     if (it.kind == 0) {
       if (!reg(it.a, it.n)) continue;
+      UT_MARK("register column");
       err = hipMemcpyAsync(it.dst, it.a, it.n, hipMemcpyHostToDevice, ctx->stream);
+      UT_MARK("issue copy");
       done[i] = 1;
       continue;
     }
@@ -267,6 +283,7 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
       unreg_last();
       continue;
     }
+    UT_MARK("register svc + flags");
     void* scr = nullptr;
     const uint64_t half = (it.n * 2 + 255) & ~255ull;
     if (ensure_scratch(ctx, kScratchUpload, 2 * half + 256, &scr) != ANOMOD_OK) {
@@ -274,6 +291,7 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
       unreg_last();
       continue;
     }
+    UT_MARK("scratch");
     char* base = static_cast<char*>(scr);
     auto* dsv = reinterpret_cast<uint16_t*>(base);
     auto* dfl = reinterpret_cast<uint16_t*>(base + half);
@@ -288,6 +306,7 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
                          dsv, dfl, static_cast<uint32_t*>(it.dst), it.n, d_mx);
       err = hipGetLastError();
     }
+    UT_MARK("issue svc/flags + pack");
     done[i] = 1;
   }
   // the rest (a refused registration, or ANOMOD_UPLOAD_DIRECT=0): the bounce
@@ -319,9 +338,11 @@ int upload_items(anomod_ctx* ctx, const UpItem* items, int n_items, uint32_t* ma
   }
   const hipError_t sync = hipStreamSynchronize(ctx->stream);
   if (err == hipSuccess) err = sync;
+  UT_MARK("sync (copies done)");
   uint32_t dmx = 0;
   if (err == hipSuccess && d_mx) err = hipMemcpy(&dmx, d_mx, 4, hipMemcpyDeviceToHost);
   for (const void* a : registered) (void)hipHostUnregister(const_cast<void*>(a));
+  UT_MARK("max readback + unregister");
   if (err != hipSuccess) {
     set_error(ctx, "span upload failed: %s", hipGetErrorString(err));
     return ANOMOD_EHIP;
