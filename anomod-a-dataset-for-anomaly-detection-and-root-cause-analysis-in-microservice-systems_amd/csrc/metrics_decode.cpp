@@ -193,38 +193,30 @@ struct CsvReader {
   }
 };
 
-// Clinger's fast path: [-]digits[.digits] with <= 15 significant digits and
-// <= 22 fraction digits is m / 10^k with both exact doubles, so the one IEEE
-// division is the correctly rounded value strtod returns.
+// Clinger's fast path: [-]digits[.digits] whose digits, read as one integer
+// m, give m <= 2^53 (exactly a double) with <= 22 fraction digits (10^k exact)
+// is m / 10^k, the one IEEE division being the correctly rounded value strtod
+// returns.  One pass, no per-digit branches beyond the digit test.
 bool fast_decimal(std::string_view v, double& out) {
   static const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
                                   1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
                                   1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-  size_t i = 0;
-  const bool neg = !v.empty() && v[0] == '-';
-  if (neg) ++i;
-  uint64_t m = 0;
-  int nd = 0, frac = -1;
-  for (; i < v.size(); ++i) {
-    const char c = v[i];
-    if (c >= '0' && c <= '9') {
-      if (m == 0 && c == '0') {  // leading zeros do not count
-        if (frac >= 0) ++frac;
-        continue;
-      }
-      if (++nd > 15) return false;
-      m = m * 10 + (uint64_t)(c - '0');
-      if (frac >= 0) ++frac;
-    } else if (c == '.' && frac < 0) {
-      frac = 0;
-    } else {
-      return false;
-    }
+  const char* p = v.data();
+  const char* const e = p + v.size();
+  const bool neg = p < e && *p == '-';
+  p += neg ? 1 : 0;
+  const char* const s = p;
+  uint64_t m = 0;  // (wraps past 19 digits: such strings are rejected below)
+  while (p < e && (unsigned)(*p - '0') < 10u) m = m * 10u + (unsigned)(*p++ - '0');
+  const size_t ni = (size_t)(p - s);
+  size_t nf = 0;
+  if (p < e && *p == '.') {
+    const char* const f = ++p;
+    while (p < e && (unsigned)(*p - '0') < 10u) m = m * 10u + (unsigned)(*p++ - '0');
+    nf = (size_t)(p - f);
   }
-  if (i == (neg ? 1u : 0u) || (frac == 0 && nd == 0 && v.size() - (neg ? 1 : 0) == 1)) return false;
-  const int k = frac < 0 ? 0 : frac;
-  if (k > 22) return false;
-  const double d = (double)m / kPow10[k];
+  if (p != e || ni + nf == 0 || ni + nf > 19 || nf > 22 || m > (1ull << 53)) return false;
+  const double d = (double)m / kPow10[nf];
   out = neg ? -d : d;
   return true;
 }

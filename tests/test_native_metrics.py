@@ -143,3 +143,32 @@ def test_long_csv_threaded_pieces_and_fill(order, tmp_path, monkeypatch):
     _same(many, one)
     _same(one, anomod.decode_metric_long_csv(p))
     assert one.S == len(set(series)) and one.T == 180
+
+
+@pytest.mark.filterwarnings("ignore:overflow encountered in cast")  # 1.8e308 -> f32 inf
+def test_value_and_timestamp_number_forms(tmp_path):
+    """The native number parser's fast path (digits[.digits] as one integer
+    over a power of ten) and its strtod fallback against Python float() —
+    the reference's rule — on the forms a CSV can hold: signs, leading
+    zeros, a bare point on either side, exponents, spaces, integers above
+    2^53, more than 19 digits, more than 22 fraction digits.  Bit-equal
+    (sign of zero included)."""
+    vals = ["-0", "0", "0.0", "-0.0", "5.", ".5", "-.5", "00001.5", "1e5", "1E-3", "+3",
+            "  7", "7  ", "9007199254740992", "9007199254740993", "18446744073709551617",
+            "123456789012345678901", "0.1234567890123456789012", "0.00000000000000000000001",
+            "3.14159265358979323846", "-123.456", "1.7976931348623157e308", "inf", "-inf",
+            "nan", "2.5e-310", "0.30000000000000004", "1234567890123456.5"]
+    rows = ["metric_name,timestamp,datetime,value,service"]
+    for k, v in enumerate(vals):
+        rows.append(f'up,{k * 15}{".0" if k % 2 else ""},x,"{v}",svc')  # quoted: spaces kept
+        rows.append(f"up2,{k}.{k:03d},x,{v.strip()},svc")
+    data = ("\n".join(rows) + "\n").encode()
+    p = tmp_path / "m.csv"
+    p.write_bytes(data)
+    nat = anomod.decode_metric_long_csv_native(data)
+    ref = anomod.decode_metric_long_csv(p)
+    assert nat.series == ref.series
+    np.testing.assert_array_equal(nat.timestamps.view(np.uint64), ref.timestamps.view(np.uint64))
+    a, b = nat.X.view(np.uint32), ref.X.view(np.uint32)
+    nan = np.isnan(nat.X) & np.isnan(ref.X)
+    assert np.array_equal(a[~nan], b[~nan])
