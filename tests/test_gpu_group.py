@@ -184,6 +184,26 @@ def test_large_interleaved_conservation(ctx):
     assert g.n_traces == 1 << 23 and g.n_spans == inter.n_spans
 
 
+@pytest.mark.slow
+def test_full_size_ungrouped_equals_grouped(ctx):
+    """The bench's ungrouped workload at its full size (BASELINE config 3 on
+    one GPU: 2^27 SN traces, 1.15e9 spans, the spans of every 4096
+    consecutive traces interleaved): the table the two-level scatter + join
+    path computes equals, bit for bit, the grouped set's table — a
+    size-independent property where the oracle cannot follow (unique ids, so
+    the table does not depend on in-trace order); the path is the join."""
+    dev = ctx.generate(anomod.SynthSpec("SN", seed=20251103, p_orphan_ppm=100), 1 << 27)
+    want = ctx.edge_aggregate(dev, with_hist=True)
+    inter = ctx.shuffle(dev, seed=20251105, window_traces=4096)
+    dev.free()
+    got = ctx.edge_aggregate(inter, with_hist=True)
+    assert ctx.group_info()["path"] == "join"
+    inter.free()
+    for k in ("count", "errors", "sum_us", "min_us", "max_us", "hist", "p50_us", "p99_us"):
+        np.testing.assert_array_equal(getattr(got, k), getattr(want, k), err_msg=k)
+    assert int(got.count.sum()) == int(want.count.sum()) > 10**9
+
+
 @pytest.fixture
 def env_knob(monkeypatch):
     """Set a libanomod environment knob for one test (read on every call)."""
