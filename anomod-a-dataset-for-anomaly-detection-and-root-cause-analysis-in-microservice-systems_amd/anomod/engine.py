@@ -240,11 +240,22 @@ def features(exp: Experiment, ctx: Context | None = None, *, W: int = 60,
         # a single spike), then take the max over the series of a service
         k = max(1, Z.shape[0] // 20)
         top = np.sort(Z, axis=0)[-k:].mean(axis=0) if Z.shape[0] else np.zeros(Z.shape[1])
+        # series -> service, decided once per distinct label set (a TT matrix
+        # holds ~6 k series over ~50 label sets), then one scatter-max
         memo: dict = {}
+        by_labels: dict = {}
+        idx = np.empty(len(series), np.int64)
         for j, key in enumerate(series):
-            i = _series_service(key, edges.services, memo)
-            if i is not None:
-                metric_score[i] = max(metric_score[i], float(top[j]))
+            labels = key[1] if len(key) > 1 else ()
+            if not isinstance(labels, tuple):  # (a caller's list of pairs: made hashable)
+                labels = tuple(tuple(kv) for kv in labels)
+            i = by_labels.get(labels)
+            if i is None:
+                i = _series_service(key, edges.services, memo)
+                i = by_labels[labels] = -1 if i is None else i
+            idx[j] = i
+        ok = idx >= 0
+        np.maximum.at(metric_score, idx[ok], np.asarray(top, np.float64)[ok])
     # error rate of the calls each service serves
     cnt = edges.count.reshape(S + 2, S).sum(axis=0).astype(np.float64)
     err = edges.errors.reshape(S + 2, S).sum(axis=0).astype(np.float64)
