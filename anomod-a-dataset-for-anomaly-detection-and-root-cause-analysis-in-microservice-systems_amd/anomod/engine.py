@@ -243,17 +243,14 @@ def features(exp: Experiment, ctx: Context | None = None, *, W: int = 60,
         # series -> service, decided once per distinct label set (a TT matrix
         # holds ~6 k series over ~50 label sets), then one scatter-max
         memo: dict = {}
-        by_labels: dict = {}
-        idx = np.empty(len(series), np.int64)
-        for j, key in enumerate(series):
-            labels = key[1] if len(key) > 1 else ()
-            if not isinstance(labels, tuple):  # (a caller's list of pairs: made hashable)
-                labels = tuple(tuple(kv) for kv in labels)
-            i = by_labels.get(labels)
-            if i is None:
-                i = _series_service(key, edges.services, memo)
-                i = by_labels[labels] = -1 if i is None else i
-            idx[j] = i
+        labs = [k[1] if len(k) > 1 else () for k in series]
+        if not all(isinstance(lb, tuple) for lb in labs):  # a caller's lists of pairs
+            labs = [lb if isinstance(lb, tuple) else tuple(tuple(kv) for kv in lb) for lb in labs]
+        by_labels = {}
+        for lb in dict.fromkeys(labs):
+            i = _series_service(("", lb), edges.services, memo)
+            by_labels[lb] = -1 if i is None else i
+        idx = np.fromiter(map(by_labels.__getitem__, labs), np.int64, len(labs))
         ok = idx >= 0
         np.maximum.at(metric_score, idx[ok], np.asarray(top, np.float64)[ok])
     # error rate of the calls each service serves
