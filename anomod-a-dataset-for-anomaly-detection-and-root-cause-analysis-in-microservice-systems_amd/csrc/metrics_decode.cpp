@@ -556,6 +556,14 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
   std::string key, prev_key;
   uint32_t prev_s = 0;
   bool have_prev = false;
+  // the previous row's series fields (name, then the label columns), when
+  // they all view the input itself (a quoted field views the reader's
+  // scratch, which the next record reuses)
+  std::vector<std::string_view> prev_id(1 + H.label_cols.size());
+  bool prev_views = false;
+  const auto in_input = [&](std::string_view x) {
+    return x.empty() || (x.data() >= p && x.data() + x.size() <= end);
+  };
   uint64_t row = row0;
   while (rd.next()) {
     if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;  // blank line (skipped)
@@ -564,14 +572,21 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
       return c >= 0 && (size_t)c < rd.fields.size() ? rd.fields[c] : std::string_view();
     };
     const std::string_view nm = field(H.c_name);
-    key.assign(nm.data(), nm.size());
-    for (int c : H.label_cols) {
-      const std::string_view v = field(c);
-      if (v.empty()) continue;
-      key.push_back('\0');
-      key.append(H.hdr[c]);
-      key.push_back('\0');
-      key.append(v.data(), v.size());
+    // series-major files: the row's series is usually the previous row's,
+    // seen here as the same bytes in the same fields (no key built)
+    bool same = prev_views && nm == prev_id[0];
+    for (size_t j = 0; same && j < H.label_cols.size(); ++j)
+      same = field(H.label_cols[j]) == prev_id[j + 1];
+    if (!same) {
+      key.assign(nm.data(), nm.size());
+      for (int c : H.label_cols) {
+        const std::string_view v = field(c);
+        if (v.empty()) continue;
+        key.push_back('\0');
+        key.append(H.hdr[c]);
+        key.push_back('\0');
+        key.append(v.data(), v.size());
+      }
     }
     double t;
     if (!parse_float(field(H.c_ts), t) || std::isnan(t)) {
@@ -586,9 +601,8 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
                         (int)vs.size(), vs.data());
       return ANOMOD_EINVAL;
     }
-    // series-major files: the row's series is usually the previous row's
-    // (one compare instead of hashing the key)
-    if (!have_prev || key != prev_key) {
+    // otherwise one compare of the built key before hashing it
+    if (!same && (!have_prev || key != prev_key)) {
       prev_s = b.series_of_key(key, [&] {
         labels.clear();
         for (int c : H.label_cols) {
@@ -599,6 +613,14 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
       });
       prev_key.swap(key);
       have_prev = true;
+    }
+    if (!same) {
+      prev_id[0] = nm;
+      prev_views = in_input(nm);
+      for (size_t j = 0; j < H.label_cols.size(); ++j) {
+        prev_id[j + 1] = field(H.label_cols[j]);
+        prev_views = prev_views && in_input(prev_id[j + 1]);
+      }
     }
     b.add(t, (float)v, prev_s);
   }
