@@ -565,6 +565,11 @@ int decode_long_rows(const LongHeader& H, const char* p, const char* end, Builde
     return x.empty() || (x.data() >= p && x.data() + x.size() <= end);
   };
   uint64_t row = row0;
+  // room for the rows up front (a collector row is ~80 bytes; one row per 32
+  // bytes leaves slack, and shorter rows only fall back to growing): growing
+  // by doubling would copy the samples and fault fresh pages for each copy;
+  // reserved pages are touched only as rows arrive
+  b.own.samples.reserve(b.own.samples.size() + (size_t)(end - p) / 32u);
   while (rd.next()) {
     if (rd.fields.size() == 1 && rd.fields[0].empty()) continue;  // blank line (skipped)
     ++row;
