@@ -14,7 +14,10 @@ int main(int argc, char** argv) {
   for (int r = 0; r < 3; ++r) {
     auto t0 = std::chrono::steady_clock::now();
     anomod_metrics* out = nullptr;
-    int rc = anomod_decode_metric_long_csv(m, st.st_size, &out);
+    // the library's file entry (a fresh mapping per call, as load_experiment
+    // uses it); argv[2] == "mem": the in-memory entry on one mapping
+    int rc = argc > 2 ? anomod_decode_metric_long_csv(m, st.st_size, &out)
+                      : anomod_decode_metric_long_csv_file(argv[1], &out);
     auto t1 = std::chrono::steady_clock::now();
     printf("rc %d %.1f ms\n", rc, std::chrono::duration<double, std::milli>(t1 - t0).count());
     anomod_metrics_free(out);
